@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""PLA-GNN training-step benchmark on MI355X (BASELINE.json metric).
+
+metric: edges aggregated / s per training epoch, full graph. One step = one full-graph
+training epoch of the reference (code/train.py:197-207: zero_grad, forward, multi_loss on
+the train rows, backward, Adam.step, val loss on the same logits); edges per step =
+L_sage * E' (E' = PPI edges + N self-loops). Workload (BASELINE configs[1]): synthetic
+PPI stand-in S0 (N = 24,041, power-law, mean degree 50, E' ~ 1.23 M), 3 SAGE-pool layers
+of hidden 256 (503 -> 256 -> 256 -> 256, MLP 256 -> 100 -> 12), fp32.
+
+Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): every rank trains a full-graph
+replica on its own graph (rank r: synthetic seed 70 + r, the perturbation-graph replicas
+of BASELINE configs[3]) with ONE all-reduce (average) of the flat gradient bucket per step
+before Adam; weak scaling. value = sum over ranks of edges / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pla-gnn_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+CONFIGS = {
+    # name: (graph kind, dims, description)
+    "cfg2": ("s0", [503, 256, 256, 256, 100, 12],
+             "S0 PPI stand-in (N=24041, mean deg 50), 3x SAGE-pool hidden 256, fp32"),
+    "ref": ("s0", [503, 400, 300, 200, 100, 12],
+            "S0 PPI stand-in, reference dims GNN32(503,400,300,200,100,12), fp32"),
+    "cfg3": ("s0", [503, 512, 512, 512, 100, 12],
+             "S0 PPI stand-in with ECC-style edge weights, hidden 512, fp32"),
+}
+PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_F32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
+
+
+def _group(name: str) -> str:
+    if name.startswith("gemm"):
+        return "gemm_f32"
+    return name.split(".")[0]
+
+
+def cpu_baseline(ds, dims, train_idx, w, seconds: float = 15.0):
+    """The oracle (C restatement of DGL's CPU loops + torch-CPU fp32 dense algebra) timed
+    on this host on the same graph and dims; bounded to ~`seconds` of work."""
+    import oracle
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    og = oracle.OracleGraph(ds.row, ds.col, ds.n)
+    x = torch.from_numpy(ds.feat)
+    labels = torch.from_numpy(ds.loc.astype(np.float32))
+    p = oracle.init_params(dims, seed=0)
+    keys = list(p)
+    m = [torch.zeros_like(p[k]) for k in keys]
+    v = [torch.zeros_like(p[k]) for k in keys]
+    times = []
+    t_start = time.perf_counter()
+    step = 0
+    while True:
+        t0 = time.perf_counter()
+        _, _, grads = oracle.train_step(og, x, labels, train_idx, w, p)
+        step += 1
+        oracle.adam_step_torch110([p[k] for k in keys], [grads[k] for k in keys], m, v, step, 5e-5)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > seconds or step >= 5:
+            break
+    t = float(np.median(times))
+    L = len(dims) - 3
+    return {"value": L * og.num_edges / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"{step} full training step(s) of the oracle on the same S0 graph and dims "
+                      f"(median {t:.2f} s/step; SpMM in single-thread C, dense in torch-CPU with "
+                      f"{threads} threads)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--breakdown-reps", type=int, default=5)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    import plagnn
+    from plagnn import data
+    from plagnn.train import fold_splits, weight_cal
+
+    kind, dims, desc = CONFIGS[args.config]
+    ds = data.make_dataset(kind, seed=70 + rank)
+    src, dst = ds.edges_with_self_loops()
+    graph = plagnn.CSRGraph(src, dst, ds.n)
+    label = [int(i) for i in ds.labelled]
+    train_idx, val_idx = next(fold_splits(label, 10, 12))  # round 1, fold 1 (train.py:162-178)
+    w = weight_cal(ds.loc)
+    ew = None
+    if args.config == "cfg3":
+        ew = torch.from_numpy(np.random.default_rng(70 + rank).uniform(0, 1, len(src)).astype(np.float32))
+    engine = plagnn.TrainEngine(graph, torch.from_numpy(ds.feat), torch.from_numpy(ds.loc.astype(np.float32)),
+                                dims, w, train_idx, val_idx, lr=5e-5, device=dev, edge_weight=ew,
+                                seed=rank)
+    allreduce = None
+    if dist is not None:
+        def allreduce(t):
+            dist.all_reduce(t, op=dist.ReduceOp.AVG)
+
+    n_cap_warm = min(2, args.warmup)
+    engine.capture(warmup=n_cap_warm, allreduce=allreduce)
+    for _ in range(args.warmup - n_cap_warm):
+        engine.step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        engine.step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    edges = torch.tensor([float(engine.edges_per_step)], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(edges, op=dist.ReduceOp.SUM)
+    t_max = t.item()
+    value = edges.item() * args.steps / t_max
+    loss_tr, loss_va = engine.losses()
+    if not (np.isfinite(loss_tr) and np.isfinite(loss_va)):
+        raise SystemExit(f"non-finite loss after training: {loss_tr}, {loss_va}")
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    # per-kernel HIP-event breakdown (eager diagnostic steps, after the timed region)
+    bd = engine.kernel_breakdown(args.breakdown_reps)
+    groups = {}
+    for name, r in bd.items():
+        gname = _group(name)
+        g = groups.setdefault(gname, {"ms": 0.0, "work": 0.0, "launches": 0.0})
+        g["ms"] += r["ms"]
+        g["work"] += r["work"]
+        g["launches"] += r["calls"]
+    dom = max(groups, key=lambda k: groups[k]["ms"])
+
+    def roof(gname):
+        g = groups[gname]
+        sec = g["ms"] / 1e3
+        if gname == "gemm_f32":
+            ach = g["work"] / sec / 1e12
+            return {"kernel": gname, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F32_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_TFLOPS, 4),
+                    "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
+        ach = g["work"] / sec / 1e9
+        return {"kernel": gname, "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
+                "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
+
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    rf = roof(dom)
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tj = json.load(f)
+        traffic = tj.get(args.config, {}).get(dom)
+    rf["traffic"] = traffic
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(ds, dims, train_idx, w)
+
+    out = {
+        "metric": "edges aggregated/sec per training epoch, full PPI graph",
+        "value": round(value, 1),
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded power-law PPI stand-in; real PPI/GEO/UniProt inputs are not shipped)",
+        "config": {"workload": f"{args.config}: {desc}", "nodes": ds.n, "edges_with_self_loops": graph.num_edges,
+                   "sage_layers": len(dims) - 3, "dims": dims, "edges_per_step": engine.edges_per_step,
+                   "parallelism": f"replicas{world}+grad-allreduce" if world > 1 else "single"},
+        "roofline": rf,
+        "spmm_roofline": {k: roof(k) for k in ("spmm_max_fwd", "spmm_max_bwd") if k in groups},
+        "kernels_ms_per_step": {k: round(v["ms"], 4) for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])},
+        "cpu_baseline": cpu,
+        "loss": {"train": loss_tr, "val": loss_va},
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,233 @@
+/*
+ * plagnn.h — C-ABI of the MI355X-native message-passing engine for PLA-GNN.
+ *
+ * This is the drop-in boundary for the reference's hot path. The reference
+ * (quinlanW/PLA-GNN) reaches its message passing only through DGL 0.8.2's
+ * Python API; every entry point below replaces one native operation that
+ * DGL/torch runs underneath the reference's call sites:
+ *
+ *   pg_csr_from_coo      <- dgl.graph((start, end), num_nodes=N) + dgl.add_self_loop
+ *                           and DGL's lazy COO->CSC (in-CSR) build
+ *                           (code/utils.py:74-75, first update_all at code/model.py:20)
+ *   pg_csr_transpose     <- DGL's reverse-graph CSR used by GSpMM.backward
+ *   pg_spmm_max_fwd      <- update_all(copy_u('h','m'), max('m','neigh')) inside
+ *                           SAGEConv(..., 'pool')  (code/model.py:13-15, 20, 22, 24)
+ *                           = DGL SpMMCmpCsr<copy_lhs, Max> (argmax recorded)
+ *   pg_spmm_max_bwd      <- DGL GSpMM.backward, copy_lhs/max branch:
+ *                           dX = zeros; dX.scatter_add_(0, argX, dZ)   (reached from
+ *                           train_loss.backward(), code/train.py:204), fused with the
+ *                           relu' mask of fc_pool's activation
+ *   pg_spmm_max_bwd_scatter  same, in DGL's scatter form (float atomics)
+ *   pg_spmm_sum          <- update_all(copy_u / u_mul_e, sum|mean) (SAGEConv 'mean',
+ *                           GraphConv, edge_weight=...) and their backward on the
+ *                           transposed CSR. Not run by the reference: reference-unpinned.
+ *   pg_argpos_to_src     <- DGL's argX (source node id of the max) from our compact
+ *                           per-row edge positions
+ *   pg_sigmoid_multi_loss<- th.sigmoid (code/model.py:29) + multi_loss
+ *                           (code/train.py:89-108) forward and backward
+ *   pg_adam_*            <- torch.optim.Adam(model.parameters(), lr) .step()
+ *                           (code/train.py:180, 205), torch 1.10 formula
+ *   pg_bias_act[_bwd]    <- nn.Linear bias add + F.relu / F.leaky_relu(0.01)
+ *                           (code/model.py:21-27), fused
+ *   pg_col_sum           <- bias gradients (sum of dY over nodes)
+ *   pg_gemm_f32          <- nn.Linear GEMMs (fc_pool / fc_self / fc_neigh / liner1-2),
+ *                           fp32 MFMA (v_mfma_f32_32x32x2_f32), exact f32
+ *
+ * Conventions
+ *   - All buffers are caller-owned. Device entry points take device pointers and
+ *     enqueue asynchronously on `stream` (a hipStream_t; NULL = default stream);
+ *     they never allocate, copy to host or synchronise, so they can be captured
+ *     into a HIP graph. Scratch comes from the caller through (ws, ws_bytes),
+ *     sized by the matching *_workspace() query.
+ *   - Host entry points (pg_csr_*, pg_schedule_*) take host pointers.
+ *   - Dense matrices are row-major with an explicit leading dimension (elements).
+ *   - Return 0 on success, a negative PG_ERR_* code for an argument error, or a
+ *     positive hipError_t for a launch error. pg_last_error_string() gives a
+ *     thread-local message for the last failure. No C++ exception crosses the ABI.
+ *   - Entry points suffixed _cpu are the same operations on host pointers (OpenMP)
+ *     for tensors the caller keeps on the CPU device (DGL's CPU backend role,
+ *     main_normal.py -d cpu). They are never used as a fallback for a GPU call.
+ */
+#ifndef PLAGNN_H
+#define PLAGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* pg_stream_t; /* hipStream_t */
+
+#define PG_OK 0
+#define PG_ERR_INVALID (-1)     /* bad argument / shape */
+#define PG_ERR_UNSUPPORTED (-2) /* valid but not implemented for these arguments */
+#define PG_ERR_WORKSPACE (-3)   /* ws_bytes smaller than the *_workspace() query */
+#define PG_ERR_HOST (-4)        /* host-side failure (allocation, ...) */
+
+/* element type of the per-(row, feature) argmax record */
+#define PG_ARG_U16 16 /* position of the winning edge inside its row, 0xFFFF = none */
+#define PG_ARG_I32 32 /* same, int32, -1 = none (rows with degree >= 65535) */
+
+/* activation codes for pg_bias_act / pg_gemm_f32 epilogues */
+#define PG_ACT_NONE 0
+#define PG_ACT_RELU 1
+#define PG_ACT_LEAKY 2 /* F.leaky_relu, negative_slope given separately */
+
+/*
+ * A compressed sparse row view of one graph direction plus its launch schedule.
+ * For the in-CSR (DGL's CSC): rows = destination nodes, col = source node ids,
+ * entries of a row in ascending edge id (the order DGL reduces them in).
+ * For its transpose (out-CSR): rows = source nodes, col = destination ids in
+ * ascending order, eslot = the in-CSR slot j of the same edge.
+ * Work schedule (built by pg_schedule_build): items {row, k0, k1, slot} cover every
+ * row; a row longer than `chunk` entries is split into several items that write
+ * partial results to `slot`; merges {row, first_slot, n_slots, 0} combine them.
+ */
+typedef struct pg_csr {
+  int64_t n_rows;
+  int64_t n_cols;
+  int64_t nnz;
+  const int32_t* ptr;    /* [n_rows + 1] */
+  const int32_t* col;    /* [nnz] */
+  const int32_t* eslot;  /* [nnz] or NULL (NULL: slot == k) */
+  const float* ew;       /* edge weights indexed by in-CSR slot, or NULL */
+  const int32_t* items;  /* [4 * n_items] */
+  int64_t n_items;
+  const int32_t* merges; /* [4 * n_merges] */
+  int64_t n_merges;
+  int64_t n_slots;
+  int32_t max_deg;
+  int32_t chunk;
+} pg_csr_t;
+
+/* ---------------- host: graph construction (code/utils.py:74-75) ---------------- */
+
+/* COO (src[e], dst[e]) -> in-CSR: ptr[n_dst+1], col[nnz] = src, eid[nnz] = edge id.
+ * Stable counting sort by dst, so each row lists its edges in ascending edge id. */
+int pg_csr_from_coo(const int64_t* src, const int64_t* dst, int64_t nnz, int64_t n_src,
+                    int64_t n_dst, int32_t* ptr, int32_t* col, int32_t* eid);
+
+/* Transpose: tptr[n_cols+1], tcol[nnz] = row ids ascending, tslot[nnz] = slot in the
+ * input CSR. */
+int pg_csr_transpose(const int32_t* ptr, const int32_t* col, int64_t n_rows, int64_t n_cols,
+                     int64_t nnz, int32_t* tptr, int32_t* tcol, int32_t* tslot);
+
+/* Work schedule sizes for rows of `ptr` split at `chunk` entries. */
+int pg_schedule_count(const int32_t* ptr, int64_t n_rows, int32_t chunk, int64_t* n_items,
+                      int64_t* n_merges, int64_t* n_slots, int32_t* max_deg);
+/* Fill items[4*n_items] (longest first) and merges[4*n_merges]. */
+int pg_schedule_build(const int32_t* ptr, int64_t n_rows, int32_t chunk, int32_t* items,
+                      int32_t* merges);
+
+/* ---------------- device: message passing ---------------- */
+
+/* out[v,f] = max_{k in row v} (ew? ew[k]:1) * X[col[k], f]  (strict >, first wins, start -inf);
+ * argpos[v,f] = k - ptr[v] of the winner. Rows with no entries: out = 0, argpos = none.
+ * A +-inf result is stored as 0 (DGL's replace_inf_with_zero after a max reduce).
+ * Requires X, out 4-byte aligned; the vector path is taken when ldx, ldo, F are
+ * multiples of 4 and the base pointers are 16-byte aligned. */
+size_t pg_spmm_max_fwd_workspace(const pg_csr_t* g, int64_t F, int arg_kind);
+int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
+                    int64_t ldo, void* argpos, int64_t lda, int arg_kind, void* ws,
+                    size_t ws_bytes, pg_stream_t stream);
+
+/* Deterministic backward (gather over the transposed CSR gt of g):
+ *   dx[u,f] = sum_{(v,j) in gt row u, ascending v} [argpos[v,f] == j - g.ptr[v]] * ew[j] * dout[v,f]
+ * then, if mask_src != NULL, dx[u,f] *= (mask_src[u,f] > 0)  (relu' of fc_pool).
+ * Every dx element is written (no zero-fill needed). */
+size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F);
+int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
+                    int arg_kind, const float* dout, int64_t ldd, int64_t F,
+                    const float* mask_src, int64_t ldm, float* dx, int64_t ldx, void* ws,
+                    size_t ws_bytes, pg_stream_t stream);
+
+/* DGL-form backward: dx = 0; dx[src(argpos[v,f]), f] += ew * dout[v,f] with f32
+ * atomics (summation order not reproducible). The callee zero-fills dx. */
+int pg_spmm_max_bwd_scatter(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,
+                            const float* dout, int64_t ldd, int64_t F, float* dx, int64_t ldx,
+                            int64_t n_src, pg_stream_t stream);
+
+/* out[r,f] = sum_{k in row r} coef_k * X[col[k], f] with
+ *   coef_k = (ew ? ew[eslot ? eslot[k] : k] : 1)
+ *   norm_mode 0: plain sum; 1: divide the row sum by the row's entry count (mean);
+ *   2: each term divided by the entry count of col[k] in norm_ptr (mean backward).
+ * Rows with no entries get 0. */
+size_t pg_spmm_sum_workspace(const pg_csr_t* g, int64_t F);
+int pg_spmm_sum(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, int norm_mode,
+                const int32_t* norm_ptr, float* out, int64_t ldo, void* ws, size_t ws_bytes,
+                pg_stream_t stream);
+
+/* argx[v,f] = col[ptr[v] + argpos[v,f]] (DGL's argX, int64), -1 where none. */
+int pg_argpos_to_src(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,
+                     int64_t F, int64_t* argx, int64_t ldx, pg_stream_t stream);
+
+/* ---------------- device: dense helpers of the training step ---------------- */
+
+/* y = act(y + bias) in place (bias may be NULL). */
+int pg_bias_act(float* y, int64_t ldy, int64_t rows, int64_t cols, const float* bias, int act,
+                float slope, pg_stream_t stream);
+/* dy = dy * act'(y) in place, from the activation OUTPUT y (relu: y>0; leaky: y>0?1:slope). */
+int pg_act_bwd(float* dy, int64_t lddy, const float* y, int64_t ldy, int64_t rows, int64_t cols,
+               int act, float slope, pg_stream_t stream);
+/* out[c] (+)= sum_r x[r,c]; deterministic (fixed two-level order). */
+size_t pg_col_sum_workspace(int64_t rows, int64_t cols);
+int pg_col_sum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
+               int accumulate, void* ws, size_t ws_bytes, pg_stream_t stream);
+
+/* Sigmoid + class-weighted BCE of code/train.py:89-108 on the rows in index[]:
+ *   prob = sigmoid(z) for all n_rows rows (written if prob != NULL)
+ *   loss[0] = sum_c -(1/n) sum_{r in index} (t log(clamp(p,1e-9,10)) w_c
+ *                                   + (1-t) log(clamp(1-p,1e-9,10))) / (w_c+1) * 2
+ *   dz (if not NULL) = d loss / d z for rows in index, 0 elsewhere (all n_rows rows written).
+ * class_w[2c] = (float)w_c and class_w[2c+1] = (float)(w_c + 1), both rounded from the
+ * float64 weights of weight_cal (code/train.py:111-126). C <= 64. loss may be NULL. */
+size_t pg_sigmoid_multi_loss_workspace(int64_t n_index, int32_t C);
+int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C,
+                          const float* labels, int64_t ldl, const float* class_w,
+                          const int32_t* index, int64_t n_index, float* prob, int64_t ldp,
+                          float* loss, float* dz, int64_t lddz, void* ws, size_t ws_bytes,
+                          pg_stream_t stream);
+
+/* Adam, torch 1.10 formula (code/train.py:180,205 with the pinned torch 1.10.0):
+ *   m = m*b1 + (1-b1)*g;  v = v*b2 + (1-b2)*g*g;
+ *   p = p + (-lr/bc1) * (m / (sqrt(v)/sqrt(bc2) + eps)),  bc_i = 1 - b_i^step
+ * Hyper-parameters are doubles, as the Python floats torch receives; scalar factors are
+ * formed in double and rounded to float once, like torch's scalar arguments.
+ * state[0] = step count (float, exact to 2^24), advanced on the device by
+ * pg_adam_prepare so a captured graph replays correctly; state[1..3] scratch. */
+int pg_adam_prepare(float* state, double lr, double beta1, double beta2, pg_stream_t stream);
+int pg_adam_apply(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                  const float* state, double beta1, double beta2, double eps,
+                  double weight_decay, pg_stream_t stream);
+
+/* C[M,N] = alpha * op(A) * op(B) + beta * C, then epilogue: + bias[N] (row vector), act.
+ * op(A) = A (M x K, lda) or A^T when transa (A stored K x M); op(B) = B (K x N) or B^T when
+ * transb (B stored N x K). fp32 in, fp32 accumulate on MFMA. When split_k > 1, beta must be
+ * 0 or 1 and no bias/act is applied (partials combined in the workspace). */
+size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k);
+int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
+                const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
+                int64_t ldc, const float* bias, int act, float slope, int split_k, void* ws,
+                size_t ws_bytes, pg_stream_t stream);
+
+/* ---------------- host (_cpu): the same operations on host pointers ---------------- */
+int pg_spmm_max_fwd_cpu(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
+                        int64_t ldo, void* argpos, int64_t lda, int arg_kind);
+int pg_spmm_max_bwd_cpu(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
+                        int arg_kind, const float* dout, int64_t ldd, int64_t F,
+                        const float* mask_src, int64_t ldm, float* dx, int64_t ldx);
+int pg_spmm_sum_cpu(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, int norm_mode,
+                    const int32_t* norm_ptr, float* out, int64_t ldo);
+int pg_argpos_to_src_cpu(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,
+                         int64_t F, int64_t* argx, int64_t ldx);
+
+/* ---------------- misc ---------------- */
+const char* pg_last_error_string(void);
+int pg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLAGNN_H */

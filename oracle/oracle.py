@@ -1,0 +1,268 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker (or the timed CPU baseline). The product
+(``pla-gnn_amd/``) never imports it; its GPU path fails loudly when the HIP library is
+missing instead of routing here.
+
+CPU restatement of the reference's training hot path:
+
+* graph construction — ``dgl.graph((start, end), num_nodes)`` + ``dgl.add_self_loop``
+  (code/utils.py:71-75) with DGL's CSC in ascending edge id (C: ``oracle_csc_build``);
+* ``SAGEConv(in, out, 'pool')`` of DGL 0.8.2.post1 (code/model.py:7, 13-15, 20-25):
+  ``P = relu(fc_pool(h))``; ``update_all(copy_u('h','m'), max('m','neigh'))`` with argmax
+  (C: ``oracle_spmm_max``); ``rst = fc_self(h) + fc_neigh(neigh) + bias``; backward of the
+  max through ``scatter_add_`` on argX (C: ``oracle_spmm_max_bwd``);
+* ``GNN32.forward`` (code/model.py:19-31): leaky_relu(0.01) after each conv and liner1,
+  sigmoid at the end;
+* ``multi_loss`` / ``weight_cal`` (code/train.py:89-126);
+* ``torch.optim.Adam`` step as torch 1.10.0 computes it (code/train.py:180, 205).
+
+Dense algebra runs in torch-CPU float32 (the "plain PyTorch fp32 reference"); the
+message passing runs in the C restatement, single-threaded, in DGL's loop order.
+
+Pinning: ``multi_loss``/``weight_cal`` are checked against golden vectors produced by the
+reference's own functions (tests/golden/gen_golden.py). The DGL message-passing
+semantics are PARITY UNPINNED by reference tests (the reference has none and DGL is not
+installable here); they are pinned by the known-answer tests in tests/test_oracle.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+def build() -> str:
+    """Compile the C restatement (gcc) into oracle/build/liboracle.so."""
+    import subprocess
+
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_csc_build.argtypes = [_i64p, _i64p, ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, _i64p]
+        L.oracle_csc_build.restype = ctypes.c_int
+        L.oracle_spmm_max.argtypes = [_i64p, _i64p, _i64p, _f32p, _f32p, ctypes.c_int64, ctypes.c_int64,
+                                      _f32p, _i64p, _i64p]
+        L.oracle_spmm_max.restype = None
+        L.oracle_spmm_max_bwd.argtypes = [_i64p, _i64p, _f32p, _f32p, _u8p, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_int64, _f32p]
+        L.oracle_spmm_max_bwd.restype = None
+        L.oracle_spmm_sum.argtypes = [_i64p, _i64p, _i64p, _f32p, _f32p, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_int, _f32p]
+        L.oracle_spmm_sum.restype = None
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+# ---------------------------------------------------------------- graph construction
+class OracleGraph:
+    """COO edge list + DGL-ordered CSC (int64 ids), as DGL 0.8 holds it."""
+
+    def __init__(self, src, dst, num_nodes: int, self_loop: bool = True,
+                 edge_weight: Optional[np.ndarray] = None):
+        src = np.asarray(src, dtype=np.int64)
+        dst = np.asarray(dst, dtype=np.int64)
+        n = int(num_nodes)
+        if self_loop:  # dgl.add_self_loop: loops appended, edge ids E..E+N-1 (utils.py:75)
+            loops = np.arange(n, dtype=np.int64)
+            src = np.concatenate([src, loops])
+            dst = np.concatenate([dst, loops])
+            if edge_weight is not None:
+                edge_weight = np.concatenate([np.asarray(edge_weight, np.float32),
+                                              np.ones(n, np.float32)])
+        self.src, self.dst, self.n = src, dst, n
+        self.ew = None if edge_weight is None else np.ascontiguousarray(edge_weight, np.float32)
+        self.indptr = np.zeros(n + 1, np.int64)
+        self.indices = np.zeros(len(src), np.int64)
+        self.eids = np.zeros(len(src), np.int64)
+        rc = lib().oracle_csc_build(_p(src, _i64p), _p(dst, _i64p), len(src), n,
+                                    _p(self.indptr, _i64p), _p(self.indices, _i64p), _p(self.eids, _i64p))
+        if rc != 0:
+            raise ValueError("oracle_csc_build: bad edge list")
+
+    @property
+    def num_edges(self) -> int:
+        return int(len(self.src))
+
+    def in_degrees(self) -> np.ndarray:
+        return np.diff(self.indptr)
+
+
+# ---------------------------------------------------------------- message passing
+def spmm_max(g: OracleGraph, X: np.ndarray, use_weight: bool = False):
+    X = np.ascontiguousarray(X, np.float32)
+    F = X.shape[1]
+    out = np.empty((g.n, F), np.float32)
+    argx = np.empty((g.n, F), np.int64)
+    arge = np.empty((g.n, F), np.int64)
+    w = g.ew if use_weight else None
+    lib().oracle_spmm_max(_p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p),
+                          _p(w, _f32p), _p(X, _f32p), g.n, F, _p(out, _f32p), _p(argx, _i64p),
+                          _p(arge, _i64p))
+    return out, argx, arge
+
+
+def spmm_max_bwd(g: OracleGraph, argx, arge, dZ: np.ndarray, use_weight: bool = False):
+    dZ = np.ascontiguousarray(dZ, np.float32)
+    F = dZ.shape[1]
+    dX = np.empty((g.n, F), np.float32)
+    has_in = (g.in_degrees() > 0).astype(np.uint8)
+    w = g.ew if use_weight else None
+    lib().oracle_spmm_max_bwd(_p(np.ascontiguousarray(argx), _i64p), _p(np.ascontiguousarray(arge), _i64p),
+                              _p(w, _f32p), _p(dZ, _f32p), _p(has_in, _u8p), g.n, g.n, F, _p(dX, _f32p))
+    return dX
+
+
+def spmm_sum(g: OracleGraph, X: np.ndarray, mean: bool = False, use_weight: bool = False):
+    X = np.ascontiguousarray(X, np.float32)
+    out = np.empty((g.n, X.shape[1]), np.float32)
+    w = g.ew if use_weight else None
+    lib().oracle_spmm_sum(_p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p), _p(w, _f32p),
+                          _p(X, _f32p), g.n, X.shape[1], int(mean), _p(out, _f32p))
+    return out
+
+
+class _MaxAggregate(torch.autograd.Function):
+    """update_all(copy_u|u_mul_e, max) with DGL's GSpMM backward (scatter_add_ on argX)."""
+
+    @staticmethod
+    def forward(ctx, P, g, use_weight):
+        out, argx, arge = spmm_max(g, P.detach().numpy(), use_weight)
+        ctx.g, ctx.argx, ctx.arge, ctx.use_weight = g, argx, arge, use_weight
+        return torch.from_numpy(out)
+
+    @staticmethod
+    def backward(ctx, dZ):
+        dX = spmm_max_bwd(ctx.g, ctx.argx, ctx.arge, dZ.contiguous().numpy(), ctx.use_weight)
+        return torch.from_numpy(dX), None, None
+
+
+# ---------------------------------------------------------------- model (code/model.py)
+def leaky_relu(x):
+    return torch.nn.functional.leaky_relu(x)  # negative_slope 0.01 (model.py:21,23,25,27)
+
+
+def sage_pool(g: OracleGraph, h: torch.Tensor, p: Dict[str, torch.Tensor], prefix: str,
+              use_weight: bool = False) -> torch.Tensor:
+    """DGL 0.8.2 SAGEConv(aggregator_type='pool', feat_drop=0, bias=True, norm=None,
+    activation=None).forward(graph, feat[, edge_weight])."""
+    P = torch.relu(h @ p[prefix + "fc_pool.weight"].t() + p[prefix + "fc_pool.bias"])
+    neigh = _MaxAggregate.apply(P, g, use_weight)
+    h_neigh = neigh @ p[prefix + "fc_neigh.weight"].t()
+    rst = h @ p[prefix + "fc_self.weight"].t() + h_neigh
+    return rst + p[prefix + "bias"]
+
+
+def gnn32_forward(g: OracleGraph, x: torch.Tensor, p: Dict[str, torch.Tensor],
+                  use_weight: bool = False) -> torch.Tensor:
+    """GNN32.forward (code/model.py:19-31), generalised to any number of conv layers."""
+    h = x
+    i = 1
+    while f"conv{i}.fc_pool.weight" in p:
+        h = leaky_relu(sage_pool(g, h, p, f"conv{i}.", use_weight))
+        i += 1
+    h = leaky_relu(h @ p["liner1.weight"].t() + p["liner1.bias"])
+    h = h @ p["liner2.weight"].t() + p["liner2.bias"]
+    return torch.sigmoid(h)
+
+
+def init_params(dims, seed: int = 0) -> Dict[str, torch.Tensor]:
+    """Fresh parameters shaped like GNN32(dims[0], ..., num_classes); DGL 0.8 init
+    (xavier_uniform gain sqrt(2) on fc_pool/fc_self/fc_neigh, zero SAGE bias)."""
+    gen = torch.Generator().manual_seed(seed)
+    n_conv = len(dims) - 3
+    p: Dict[str, torch.Tensor] = {}
+
+    def xavier(o, i):
+        a = (2.0 ** 0.5) * (6.0 / (i + o)) ** 0.5
+        return (torch.rand(o, i, generator=gen) * 2 - 1) * a
+
+    def lin(o, i):
+        b = 1.0 / i ** 0.5
+        return (torch.rand(o, i, generator=gen) * 2 - 1) * b, (torch.rand(o, generator=gen) * 2 - 1) * b
+
+    for li in range(n_conv):
+        fi, fo = dims[li], dims[li + 1]
+        pre = f"conv{li + 1}."
+        p[pre + "fc_pool.weight"] = xavier(fi, fi)
+        p[pre + "fc_pool.bias"] = lin(fi, fi)[1]
+        p[pre + "fc_neigh.weight"] = xavier(fo, fi)
+        p[pre + "fc_self.weight"] = xavier(fo, fi)
+        p[pre + "bias"] = torch.zeros(fo)
+    w1, b1 = lin(dims[-2], dims[-3])
+    w2, b2 = lin(dims[-1], dims[-2])
+    p["liner1.weight"], p["liner1.bias"] = w1, b1
+    p["liner2.weight"], p["liner2.bias"] = w2, b2
+    return p
+
+
+# ---------------------------------------------------------------- loss (code/train.py)
+def multi_loss(input: torch.Tensor, target: torch.Tensor, i_weight) -> torch.Tensor:
+    """code/train.py:89-108."""
+    loss = 0
+    for i in range(len(i_weight)):
+        scl_input = input[:, i]
+        scl_target = target[:, i]
+        a = scl_target * torch.log(torch.clamp(scl_input, 1e-9, 10.)) * i_weight[i]
+        b = (1 - scl_target) * torch.log(torch.clamp(1 - scl_input, 1e-9, 10.))
+        scl_loss = (a + b) / (i_weight[i] + 1) * 2
+        loss += -scl_loss.sum() / len(input)
+    return loss
+
+
+def weight_cal(loc_mat: np.ndarray) -> np.ndarray:
+    """code/train.py:111-126: w_c = (n_labelled - n_c) / n_c (float64)."""
+    class_num = loc_mat.sum(axis=0)
+    sample_num = int((loc_mat.sum(axis=1) != 0).sum())
+    return (sample_num - class_num) / class_num
+
+
+# ---------------------------------------------------------------- optimiser
+def adam_step_torch110(params, grads, exp_avg, exp_avg_sq, step: int, lr: float,
+                       beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8):
+    """torch 1.10.0 F.adam (single tensor), in place; step is the new step count."""
+    import math
+
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    for p, g, m, v in zip(params, grads, exp_avg, exp_avg_sq):
+        m.mul_(beta1).add_(g, alpha=1 - beta1)
+        v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(m, denom, value=-(lr / bc1))
+
+
+# ---------------------------------------------------------------- one training step
+def train_step(g: OracleGraph, x: torch.Tensor, labels: torch.Tensor, train_index,
+               i_weight, p: Dict[str, torch.Tensor], use_weight: bool = False
+               ) -> Tuple[torch.Tensor, torch.Tensor, Dict[str, torch.Tensor]]:
+    """zero_grad -> forward -> multi_loss(train rows) -> backward (code/train.py:197-204).
+    Returns (logits, loss, grads)."""
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
+    logits = gnn32_forward(g, x, leaves, use_weight)
+    loss = multi_loss(logits[train_index], labels[train_index], i_weight)
+    loss.backward()
+    return logits.detach(), loss.detach(), {k: v.grad.detach() for k, v in leaves.items()}

@@ -1,0 +1,335 @@
+// Dense helpers of the PLA-GNN training step on gfx950: fused bias + activation
+// (nn.Linear bias, F.relu of SAGEConv's fc_pool, F.leaky_relu of code/model.py:21-27),
+// activation backward, deterministic column sums (bias gradients), the fused
+// sigmoid + multi_loss forward/backward (code/model.py:29, code/train.py:89-108), and
+// Adam (code/train.py:180, 205; torch 1.10 update order).
+// Everything is written to be capturable in a HIP graph: no host sync, no allocation,
+// the Adam step counter lives in device memory.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline int hip_status(const char* who) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return pg::set_error((int)e, "%s: launch failed: %s", who, hipGetErrorString(e));
+  return pg::ok();
+}
+
+inline int grid_1d(int64_t n, int cap = 8192) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(cap, (n + kBlock - 1) / kBlock));
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float x, float slope) {
+  if constexpr (ACT == PG_ACT_RELU) return x > 0.f ? x : 0.f;
+  else if constexpr (ACT == PG_ACT_LEAKY) return x > 0.f ? x : x * slope;
+  else return x;
+}
+
+template <int ACT>
+__global__ __launch_bounds__(kBlock) void bias_act_kernel(float* __restrict__ y, int64_t ldy,
+                                                          int64_t rows, int cols,
+                                                          const float* __restrict__ bias,
+                                                          float slope) {
+  const int64_t n = rows * (int64_t)cols;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i / cols;
+    const int c = (int)(i - r * cols);
+    float v = y[r * ldy + c];
+    if (bias) v = v + bias[c];
+    y[r * ldy + c] = act_fwd<ACT>(v, slope);
+  }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(kBlock) void act_bwd_kernel(float* __restrict__ dy, int64_t lddy,
+                                                         const float* __restrict__ y, int64_t ldy,
+                                                         int64_t rows, int cols, float slope) {
+  const int64_t n = rows * (int64_t)cols;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i / cols;
+    const int c = (int)(i - r * cols);
+    const float yy = y[r * ldy + c];
+    float g = dy[r * lddy + c];
+    if constexpr (ACT == PG_ACT_RELU) g = yy > 0.f ? g : 0.f;
+    else if constexpr (ACT == PG_ACT_LEAKY) g = yy > 0.f ? g : g * slope;
+    dy[r * lddy + c] = g;
+  }
+}
+
+// column sums, pass 1: block (cx, ry) sums rows ry, ry + R, ... of 64 columns into
+// part[ry][c] with a fixed order (4 row groups per block, combined in order)
+constexpr int kColRowChunks = 64;
+__global__ __launch_bounds__(kBlock) void col_sum_part_kernel(const float* __restrict__ x,
+                                                              int64_t ldx, int64_t rows,
+                                                              int cols,
+                                                              float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const int R = gridDim.y;
+  float s = 0.f;
+  if (c < cols)
+    for (int64_t r = (int64_t)blockIdx.y * 4 + g; r < rows; r += (int64_t)R * 4) s += x[r * ldx + c];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < cols) {
+    const int l = threadIdx.x & 63;
+    part[(int64_t)blockIdx.y * cols + c] = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void col_sum_final_kernel(const float* __restrict__ part,
+                                                               int R, int cols,
+                                                               float* __restrict__ out,
+                                                               int accumulate) {
+  const int c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += part[(int64_t)r * cols + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ---- sigmoid + multi_loss -----------------------------------------------------------
+// pass 1: prob = sigmoid(z) everywhere, dz = 0 everywhere
+__global__ __launch_bounds__(kBlock) void sigmoid_zero_kernel(const float* __restrict__ z,
+                                                              int64_t ldz, int64_t rows, int C,
+                                                              float* __restrict__ prob,
+                                                              int64_t ldp, float* __restrict__ dz,
+                                                              int64_t lddz) {
+  const int64_t n = rows * (int64_t)C;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i / C;
+    const int c = (int)(i - r * C);
+    if (prob) prob[r * ldp + c] = 1.f / (1.f + expf(-z[r * ldz + c]));
+    if (dz) dz[r * lddz + c] = 0.f;
+  }
+}
+
+// pass 2: one thread per (indexed row, class): loss term into part, gradient into dz.
+// Mirrors the autograd graph of code/train.py:103-104 operation by operation.
+constexpr int kLossRowsPerBlock = 256;
+__global__ __launch_bounds__(kBlock) void multi_loss_kernel(
+    const float* __restrict__ z, int64_t ldz, int C, const float* __restrict__ labels,
+    int64_t ldl, const float* __restrict__ cw, const int32_t* __restrict__ index, int64_t n_index,
+    float* __restrict__ part, float* __restrict__ dz, int64_t lddz) {
+  // block b handles indexed rows [b*256, b*256+256); thread t handles class t % C of
+  // rows t / C, ... — keep it simple: loop over (row, class) pairs owned by the block
+  __shared__ float acc[kBlock];
+  const int64_t r0 = (int64_t)blockIdx.x * kLossRowsPerBlock;
+  const int64_t r1 = std::min<int64_t>(n_index, r0 + kLossRowsPerBlock);
+  const float inv_n = 1.0f / (float)n_index;
+  // per-class partial sums with fixed order: thread t sums pairs t, t+256, ...
+  float local[64];
+  for (int c = 0; c < C; ++c) local[c] = 0.f;
+  for (int64_t p = (r0 * C) + threadIdx.x; p < r1 * C; p += kBlock) {
+    const int64_t ri = p / C;
+    const int c = (int)(p - ri * C);
+    const int64_t r = index[ri];
+    const float zz = z[r * ldz + c];
+    const float pr = 1.f / (1.f + expf(-zz));
+    const float t = labels[r * ldl + c];
+    const float w = cw[2 * c];        // (float)w_c
+    const float w1 = cw[2 * c + 1];   // (float)(w_c + 1)
+    const float cp = fminf(fmaxf(pr, 1e-9f), 10.f);
+    const float q = 1.f - pr;
+    const float cq = fminf(fmaxf(q, 1e-9f), 10.f);
+    const float la = logf(cp), lb = logf(cq);
+    const float term = ((t * la) * w + (1.f - t) * lb) / w1 * 2.f;
+    local[c] += term;
+    if (dz) {
+      // d(-sum/n)/d term = -(1/n); then *2, /(w+1)
+      float g = -inv_n;
+      g = g * 2.f;
+      g = g / w1;
+      float ga = (g * w) * t;         // through (t * log(cp)) * w
+      ga = ga / cp;                   // log'
+      if (!(pr >= 1e-9f && pr <= 10.f)) ga = 0.f;  // clamp'
+      float gb = g * (1.f - t);
+      gb = gb / cq;
+      if (!(q >= 1e-9f && q <= 10.f)) gb = 0.f;
+      const float dp = ga + (-gb);
+      dz[r * lddz + c] = (dp * (1.f - pr)) * pr;  // sigmoid_backward(grad, out)
+    }
+  }
+  for (int c = 0; c < C; ++c) {
+    acc[threadIdx.x] = local[c];
+    __syncthreads();
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s) acc[threadIdx.x] += acc[threadIdx.x + s];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[(int64_t)blockIdx.x * C + c] = acc[0];
+    __syncthreads();
+  }
+}
+
+__global__ void multi_loss_final_kernel(const float* __restrict__ part, int nb, int C,
+                                        int64_t n_index, float* __restrict__ loss) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float total = 0.f;
+  for (int c = 0; c < C; ++c) {
+    float s = 0.f;
+    for (int b = 0; b < nb; ++b) s += part[(int64_t)b * C + c];
+    total += -s / (float)n_index;
+  }
+  loss[0] = total;
+}
+
+// ---- Adam ---------------------------------------------------------------------------
+__global__ void adam_prepare_kernel(float* state, double lr, double beta1, double beta2) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const float step = state[0] + 1.f;
+  state[0] = step;
+  const double bc1 = 1.0 - pow(beta1, (double)step);
+  const double bc2 = 1.0 - pow(beta2, (double)step);
+  state[1] = (float)(lr / bc1);  // step_size
+  state[2] = (float)sqrt(bc2);   // sqrt(bias_correction2)
+}
+
+__global__ __launch_bounds__(kBlock) void adam_apply_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+    float* __restrict__ v, int64_t n, const float* __restrict__ state, float beta1, float beta2,
+    float a1, float a2, float eps, float wd) {
+  const float step_size = state[1];
+  const float bc2s = state[2];
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    float gi = g[i];
+    if (wd != 0.f) gi = gi + wd * p[i];
+    const float mi = m[i] * beta1 + a1 * gi;        // exp_avg.mul_(b1).add_(g, alpha=1-b1)
+    const float vi = v[i] * beta2 + a2 * gi * gi;   // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+    const float denom = sqrtf(vi) / bc2s + eps;     // (sqrt / sqrt(bc2)).add_(eps)
+    p[i] = p[i] + (-step_size) * (mi / denom);      // addcdiv_(m, denom, -step_size)
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pg_bias_act(float* y, int64_t ldy, int64_t rows, int64_t cols, const float* bias, int act,
+                float slope, pg_stream_t stream) {
+  if (rows < 0 || cols < 0 || ldy < cols)
+    return pg::set_error(PG_ERR_INVALID, "pg_bias_act: bad shape");
+  if (rows * cols == 0) return pg::ok();
+  hipStream_t st = (hipStream_t)stream;
+  const int g = grid_1d(rows * cols);
+  switch (act) {
+    case PG_ACT_NONE:
+      hipLaunchKernelGGL((bias_act_kernel<PG_ACT_NONE>), dim3(g), dim3(kBlock), 0, st, y, ldy, rows, (int)cols, bias, slope);
+      break;
+    case PG_ACT_RELU:
+      hipLaunchKernelGGL((bias_act_kernel<PG_ACT_RELU>), dim3(g), dim3(kBlock), 0, st, y, ldy, rows, (int)cols, bias, slope);
+      break;
+    case PG_ACT_LEAKY:
+      hipLaunchKernelGGL((bias_act_kernel<PG_ACT_LEAKY>), dim3(g), dim3(kBlock), 0, st, y, ldy, rows, (int)cols, bias, slope);
+      break;
+    default:
+      return pg::set_error(PG_ERR_INVALID, "pg_bias_act: bad act %d", act);
+  }
+  return hip_status("pg_bias_act");
+}
+
+int pg_act_bwd(float* dy, int64_t lddy, const float* y, int64_t ldy, int64_t rows, int64_t cols,
+               int act, float slope, pg_stream_t stream) {
+  if (rows < 0 || cols < 0 || lddy < cols || ldy < cols)
+    return pg::set_error(PG_ERR_INVALID, "pg_act_bwd: bad shape");
+  if (rows * cols == 0 || act == PG_ACT_NONE) return pg::ok();
+  hipStream_t st = (hipStream_t)stream;
+  const int g = grid_1d(rows * cols);
+  if (act == PG_ACT_RELU)
+    hipLaunchKernelGGL((act_bwd_kernel<PG_ACT_RELU>), dim3(g), dim3(kBlock), 0, st, dy, lddy, y, ldy, rows, (int)cols, slope);
+  else if (act == PG_ACT_LEAKY)
+    hipLaunchKernelGGL((act_bwd_kernel<PG_ACT_LEAKY>), dim3(g), dim3(kBlock), 0, st, dy, lddy, y, ldy, rows, (int)cols, slope);
+  else
+    return pg::set_error(PG_ERR_INVALID, "pg_act_bwd: bad act %d", act);
+  return hip_status("pg_act_bwd");
+}
+
+size_t pg_col_sum_workspace(int64_t rows, int64_t cols) {
+  (void)rows;
+  return (size_t)kColRowChunks * (size_t)std::max<int64_t>(cols, 0) * 4;
+}
+
+int pg_col_sum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
+               int accumulate, void* ws, size_t ws_bytes, pg_stream_t stream) {
+  if (rows < 0 || cols < 0 || ldx < cols)
+    return pg::set_error(PG_ERR_INVALID, "pg_col_sum: bad shape");
+  if (cols == 0) return pg::ok();
+  if (ws_bytes < pg_col_sum_workspace(rows, cols))
+    return pg::set_error(PG_ERR_WORKSPACE, "pg_col_sum: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(col_sum_part_kernel, dim3((cols + 63) / 64, kColRowChunks), dim3(kBlock), 0,
+                     st, x, ldx, rows, (int)cols, (float*)ws);
+  hipLaunchKernelGGL(col_sum_final_kernel, dim3((cols + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                     (const float*)ws, kColRowChunks, (int)cols, out, accumulate);
+  return hip_status("pg_col_sum");
+}
+
+size_t pg_sigmoid_multi_loss_workspace(int64_t n_index, int32_t C) {
+  const int64_t nb = std::max<int64_t>(1, (n_index + kLossRowsPerBlock - 1) / kLossRowsPerBlock);
+  return (size_t)(nb * std::max(C, 1) * 4 + 2 * 64 * 4);
+}
+
+int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C,
+                          const float* labels, int64_t ldl, const float* class_w,
+                          const int32_t* index, int64_t n_index, float* prob, int64_t ldp,
+                          float* loss, float* dz, int64_t lddz, void* ws, size_t ws_bytes,
+                          pg_stream_t stream) {
+  if (C <= 0 || C > 64 || n_rows < 0 || ldz < C || ldl < C || (prob && ldp < C) ||
+      (dz && lddz < C) || n_index < 0)
+    return pg::set_error(PG_ERR_INVALID, "pg_sigmoid_multi_loss: bad shape");
+  if (!z || !labels || !class_w || (n_index > 0 && !index))
+    return pg::set_error(PG_ERR_INVALID, "pg_sigmoid_multi_loss: NULL buffer");
+  if (ws_bytes < pg_sigmoid_multi_loss_workspace(n_index, C))
+    return pg::set_error(PG_ERR_WORKSPACE, "pg_sigmoid_multi_loss: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  if ((prob || dz) && n_rows > 0)
+    hipLaunchKernelGGL(sigmoid_zero_kernel, dim3(grid_1d(n_rows * C)), dim3(kBlock), 0, st, z, ldz,
+                       n_rows, (int)C, prob, ldp, dz, lddz);
+  const int nb = (int)std::max<int64_t>(1, (n_index + kLossRowsPerBlock - 1) / kLossRowsPerBlock);
+  float* part = (float*)ws;
+  if (n_index > 0) {
+    hipLaunchKernelGGL(multi_loss_kernel, dim3(nb), dim3(kBlock), 0, st, z, ldz, (int)C, labels, ldl,
+                       class_w, index, n_index, part, dz, lddz);
+    if (loss)
+      hipLaunchKernelGGL(multi_loss_final_kernel, dim3(1), dim3(64), 0, st, (const float*)part, nb,
+                         (int)C, n_index, loss);
+  }
+  return hip_status("pg_sigmoid_multi_loss");
+}
+
+int pg_adam_prepare(float* state, double lr, double beta1, double beta2, pg_stream_t stream) {
+  if (!state) return pg::set_error(PG_ERR_INVALID, "pg_adam_prepare: NULL state");
+  hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state, lr,
+                     beta1, beta2);
+  return hip_status("pg_adam_prepare");
+}
+
+int pg_adam_apply(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                  const float* state, double beta1, double beta2, double eps,
+                  double weight_decay, pg_stream_t stream) {
+  if (n < 0 || !state) return pg::set_error(PG_ERR_INVALID, "pg_adam_apply: bad arguments");
+  if (n == 0) return pg::ok();
+  if (!param || !grad || !exp_avg || !exp_avg_sq)
+    return pg::set_error(PG_ERR_INVALID, "pg_adam_apply: NULL buffer");
+  hipLaunchKernelGGL(adam_apply_kernel, dim3(grid_1d(n, 2048)), dim3(kBlock), 0, (hipStream_t)stream,
+                     param, grad, exp_avg, exp_avg_sq, n, state, (float)beta1, (float)beta2,
+                     (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, (float)weight_decay);
+  return hip_status("pg_adam_apply");
+}
+
+}  // extern "C"

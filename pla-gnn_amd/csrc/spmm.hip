@@ -1,0 +1,843 @@
+// Message-passing kernels for gfx950 (MI355X): CSR SpMM with max/argmax (DGL
+// SpMMCmpCsr<copy_lhs|u_mul_e, Max>, reached from SAGEConv('pool') at
+// code/model.py:20/22/24), its backward (DGL GSpMM.backward scatter_add_ through argX,
+// reached from code/train.py:204), and the sum/mean variants.
+//
+// Work decomposition: one 64-lane wave per schedule item {row, k0, k1, slot}. A row
+// longer than the schedule's chunk is cut into several items whose partial results go
+// to workspace slots and are combined in chunk order by a merge kernel, so hub rows do
+// not serialise on one wave. Items are ordered longest first (pg_schedule_build).
+// Inside a wave each lane owns W consecutive features (W = 4: float4 loads, 1 KiB per
+// wave-instruction; W = 1: scalar path for unaligned rows) in NC chunks of 64*W.
+// Row indices and weights are wave-uniform and come through the scalar cache.
+//
+// Numerics: the max is a selection (bit-exact); ties keep the earlier entry (strict >),
+// matching DGL's in-order loop. Backward sums run in ascending destination order, the
+// same order as a sequential scatter_add_, so unsplit rows are bit-exact against it.
+// Build with -ffp-contract=off (no silent FMA contraction).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <limits>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kMaxNC = 4;       // vector path: F <= 4 * 256 per launch
+constexpr int kMaxNCScalar = 16; // scalar path: F <= 16 * 64 per launch
+constexpr int kUnroll = 4;       // edges in flight per wave
+
+template <typename A>
+__device__ __forceinline__ int arg_none();
+template <>
+__device__ __forceinline__ int arg_none<uint16_t>() { return 0xFFFF; }
+template <>
+__device__ __forceinline__ int arg_none<int32_t>() { return -1; }
+
+__device__ __forceinline__ int wave_id_uniform() {
+  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// ---- per-lane feature tile access ----------------------------------------------------
+template <int W>
+__device__ __forceinline__ void load_tile(const float* __restrict__ row, int f, int F,
+                                          float (&r)[W], float fill) {
+  if constexpr (W == 4) {
+    if (f < F) {
+      const float4 t = *reinterpret_cast<const float4*>(row + f);
+      r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+    } else {
+      r[0] = r[1] = r[2] = r[3] = fill;
+    }
+  } else {
+    r[0] = f < F ? row[f] : fill;
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void store_tile(float* __restrict__ row, int f, int F,
+                                           const float (&r)[W]) {
+  if constexpr (W == 4) {
+    if (f < F) *reinterpret_cast<float4*>(row + f) = make_float4(r[0], r[1], r[2], r[3]);
+  } else {
+    if (f < F) row[f] = r[0];
+  }
+}
+
+template <int W, typename A>
+__device__ __forceinline__ void load_arg(const A* __restrict__ row, int f, int F, int (&r)[W]) {
+  if constexpr (W == 4) {
+    if (f < F) {
+      if constexpr (sizeof(A) == 2) {
+        const uint2 t = *reinterpret_cast<const uint2*>(row + f);
+        r[0] = t.x & 0xFFFF; r[1] = t.x >> 16; r[2] = t.y & 0xFFFF; r[3] = t.y >> 16;
+      } else {
+        const int4 t = *reinterpret_cast<const int4*>(row + f);
+        r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+      }
+    } else {
+      r[0] = r[1] = r[2] = r[3] = arg_none<A>();
+    }
+  } else {
+    r[0] = f < F ? (int)row[f] : arg_none<A>();
+  }
+}
+
+template <int W, typename A>
+__device__ __forceinline__ void store_arg(A* __restrict__ row, int f, int F, const int (&r)[W]) {
+  if constexpr (W == 4) {
+    if (f < F) {
+      if constexpr (sizeof(A) == 2) {
+        uint2 t;
+        t.x = (uint32_t)(r[0] & 0xFFFF) | ((uint32_t)r[1] << 16);
+        t.y = (uint32_t)(r[2] & 0xFFFF) | ((uint32_t)r[3] << 16);
+        *reinterpret_cast<uint2*>(row + f) = t;
+      } else {
+        *reinterpret_cast<int4*>(row + f) = make_int4(r[0], r[1], r[2], r[3]);
+      }
+    }
+  } else {
+    if (f < F) row[f] = (A)r[0];
+  }
+}
+
+// ---- max forward ---------------------------------------------------------------------
+template <int W, int NC, bool HAS_W, typename A>
+__global__ __launch_bounds__(kBlock) void max_fwd_kernel(
+    const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
+    const int32_t* __restrict__ eslot, const float* __restrict__ ew,
+    const int4* __restrict__ items, int n_items, const float* __restrict__ X, int64_t ldx, int F,
+    float* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
+    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw) {
+  const int it = blockIdx.x * kWavesPerBlock + wave_id_uniform();
+  if (it >= n_items) return;
+  const int4 item = items[it];
+  const int row = item.x, k0 = item.y, k1 = item.z, slot = item.w;
+  const int rs = ptr[row];
+  const int lane = lane_id();
+  const float ninf = -std::numeric_limits<float>::infinity();
+
+  float best[NC][W];
+  int bpos[NC][W];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      best[c][i] = ninf;
+      bpos[c][i] = arg_none<A>();
+    }
+
+  int k = k0;
+  for (; k + kUnroll <= k1; k += kUnroll) {
+    float v[kUnroll][NC][W];
+#pragma unroll
+    for (int e = 0; e < kUnroll; ++e) {
+      const float* xr = X + (int64_t)col[k + e] * ldx;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[e][c], ninf);
+    }
+#pragma unroll
+    for (int e = 0; e < kUnroll; ++e) {
+      const int pos = k + e - rs;
+      float w = 1.f;
+      if constexpr (HAS_W) w = ew[eslot ? eslot[k + e] : k + e];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+          const float m = HAS_W ? v[e][c][i] * w : v[e][c][i];
+          if (m > best[c][i]) {
+            best[c][i] = m;
+            bpos[c][i] = pos;
+          }
+        }
+    }
+  }
+  for (; k < k1; ++k) {
+    float v[NC][W];
+    const float* xr = X + (int64_t)col[k] * ldx;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[c], ninf);
+    const int pos = k - rs;
+    float w = 1.f;
+    if constexpr (HAS_W) w = ew[eslot ? eslot[k] : k];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        const float m = HAS_W ? v[c][i] * w : v[c][i];
+        if (m > best[c][i]) {
+          best[c][i] = m;
+          bpos[c][i] = pos;
+        }
+      }
+  }
+
+  if (slot < 0) {
+    // whole row: finalise (+-inf -> 0, empty row -> 0 / none)
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < W; ++i)
+        if (__builtin_isinf(best[c][i])) best[c][i] = 0.f;
+    float* orow = out + (int64_t)row * ldo;
+    A* arow = arg + (int64_t)row * lda;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int f = (c * kWave + lane) * W;
+      store_tile<W>(orow, f, F, best[c]);
+      store_arg<W, A>(arow, f, F, bpos[c]);
+    }
+  } else {
+    float* orow = ws_val + (int64_t)slot * ldw;
+    A* arow = ws_arg + (int64_t)slot * ldw;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int f = (c * kWave + lane) * W;
+      store_tile<W>(orow, f, F, best[c]);
+      store_arg<W, A>(arow, f, F, bpos[c]);
+    }
+  }
+}
+
+// Combine the partial maxima of split rows in chunk order (earlier chunk wins ties).
+template <typename A>
+__global__ __launch_bounds__(kBlock) void max_merge_kernel(const int4* __restrict__ merges,
+                                                           int n_merges, int F,
+                                                           const float* __restrict__ ws_val,
+                                                           const A* __restrict__ ws_arg,
+                                                           int64_t ldw, float* __restrict__ out,
+                                                           int64_t ldo, A* __restrict__ arg,
+                                                           int64_t lda) {
+  const int mi = blockIdx.x * kWavesPerBlock + wave_id_uniform();
+  if (mi >= n_merges) return;
+  const int4 m = merges[mi];
+  const int row = m.x, s0 = m.y, ns = m.z;
+  for (int f = lane_id(); f < F; f += kWave) {
+    float best = -std::numeric_limits<float>::infinity();
+    int bp = arg_none<A>();
+    for (int s = s0; s < s0 + ns; ++s) {
+      const float v = ws_val[(int64_t)s * ldw + f];
+      if (v > best) {
+        best = v;
+        bp = (int)ws_arg[(int64_t)s * ldw + f];
+      }
+    }
+    if (__builtin_isinf(best)) best = 0.f;
+    out[(int64_t)row * ldo + f] = best;
+    arg[(int64_t)row * lda + f] = (A)bp;
+  }
+}
+
+// ---- max backward, deterministic gather over the transposed CSR ----------------------
+template <int W, int NC, bool HAS_W, typename A>
+__global__ __launch_bounds__(kBlock) void max_bwd_kernel(
+    const int32_t* __restrict__ gptr, const float* __restrict__ ew,
+    const int32_t* __restrict__ tptr, const int32_t* __restrict__ tcol,
+    const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
+    const A* __restrict__ arg, int64_t lda, const float* __restrict__ dout, int64_t ldd, int F,
+    const float* __restrict__ mask, int64_t ldm, float* __restrict__ dx, int64_t ldx,
+    float* __restrict__ ws, int64_t ldw) {
+  const int it = blockIdx.x * kWavesPerBlock + wave_id_uniform();
+  if (it >= n_items) return;
+  const int4 item = items[it];
+  const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
+  const int lane = lane_id();
+
+  float acc[NC][W];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < W; ++i) acc[c][i] = 0.f;
+
+  int t = t0;
+  for (; t + kUnroll <= t1; t += kUnroll) {
+    int a[kUnroll][NC][W];
+    int pos[kUnroll];
+    int v[kUnroll];
+    float w[kUnroll];
+#pragma unroll
+    for (int e = 0; e < kUnroll; ++e) {
+      v[e] = tcol[t + e];
+      const int j = tslot ? tslot[t + e] : t + e;
+      pos[e] = j - gptr[v[e]];
+      w[e] = HAS_W ? ew[j] : 1.f;
+      const A* ar = arg + (int64_t)v[e] * lda;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) load_arg<W, A>(ar, (c * kWave + lane) * W, F, a[e][c]);
+    }
+#pragma unroll
+    for (int e = 0; e < kUnroll; ++e) {
+      const float* dr = dout + (int64_t)v[e] * ldd;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int f = (c * kWave + lane) * W;
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < W; ++i) any |= (a[e][c][i] == pos[e]);
+        if (any) {
+          float d[W];
+          load_tile<W>(dr, f, F, d, 0.f);
+#pragma unroll
+          for (int i = 0; i < W; ++i)
+            if (a[e][c][i] == pos[e]) acc[c][i] += HAS_W ? w[e] * d[i] : d[i];
+        }
+      }
+    }
+  }
+  for (; t < t1; ++t) {
+    const int vv = tcol[t];
+    const int j = tslot ? tslot[t] : t;
+    const int p = j - gptr[vv];
+    const float ww = HAS_W ? ew[j] : 1.f;
+    const A* ar = arg + (int64_t)vv * lda;
+    const float* dr = dout + (int64_t)vv * ldd;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int f = (c * kWave + lane) * W;
+      int a[W];
+      load_arg<W, A>(ar, f, F, a);
+      bool any = false;
+#pragma unroll
+      for (int i = 0; i < W; ++i) any |= (a[i] == p);
+      if (any) {
+        float d[W];
+        load_tile<W>(dr, f, F, d, 0.f);
+#pragma unroll
+        for (int i = 0; i < W; ++i)
+          if (a[i] == p) acc[c][i] += HAS_W ? ww * d[i] : d[i];
+      }
+    }
+  }
+
+  if (slot < 0) {
+    float* xr = dx + (int64_t)row * ldx;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int f = (c * kWave + lane) * W;
+      if (mask) {
+        float mk[W];
+        load_tile<W>(mask + (int64_t)row * ldm, f, F, mk, 0.f);
+#pragma unroll
+        for (int i = 0; i < W; ++i)
+          if (!(mk[i] > 0.f)) acc[c][i] = 0.f;
+      }
+      store_tile<W>(xr, f, F, acc[c]);
+    }
+  } else {
+    float* wr = ws + (int64_t)slot * ldw;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) store_tile<W>(wr, (c * kWave + lane) * W, F, acc[c]);
+  }
+}
+
+// Sum partial slots in order; optional relu' mask (bwd) or 1/deg (mean fwd).
+__global__ __launch_bounds__(kBlock) void sum_merge_kernel(
+    const int4* __restrict__ merges, int n_merges, int F, const float* __restrict__ ws,
+    int64_t ldw, const int32_t* __restrict__ ptr, int divide_by_deg,
+    const float* __restrict__ mask, int64_t ldm, float* __restrict__ out, int64_t ldo) {
+  const int mi = blockIdx.x * kWavesPerBlock + wave_id_uniform();
+  if (mi >= n_merges) return;
+  const int4 m = merges[mi];
+  const int row = m.x, s0 = m.y, ns = m.z;
+  const float deg = divide_by_deg ? (float)(ptr[row + 1] - ptr[row]) : 1.f;
+  for (int f = lane_id(); f < F; f += kWave) {
+    float acc = 0.f;
+    for (int s = s0; s < s0 + ns; ++s) acc += ws[(int64_t)s * ldw + f];
+    if (divide_by_deg) acc = acc / deg;
+    if (mask && !(mask[(int64_t)row * ldm + f] > 0.f)) acc = 0.f;
+    out[(int64_t)row * ldo + f] = acc;
+  }
+}
+
+// ---- sum / mean / weighted SpMM ------------------------------------------------------
+template <int W, int NC, bool HAS_W, int NORM>
+__global__ __launch_bounds__(kBlock) void sum_kernel(
+    const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
+    const int32_t* __restrict__ eslot, const float* __restrict__ ew,
+    const int32_t* __restrict__ norm_ptr, const int4* __restrict__ items, int n_items,
+    const float* __restrict__ X, int64_t ldx, int F, float* __restrict__ out, int64_t ldo,
+    float* __restrict__ ws, int64_t ldw) {
+  const int it = blockIdx.x * kWavesPerBlock + wave_id_uniform();
+  if (it >= n_items) return;
+  const int4 item = items[it];
+  const int row = item.x, k0 = item.y, k1 = item.z, slot = item.w;
+  const int lane = lane_id();
+  float acc[NC][W];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < W; ++i) acc[c][i] = 0.f;
+
+  int k = k0;
+  for (; k + kUnroll <= k1; k += kUnroll) {
+    float v[kUnroll][NC][W];
+#pragma unroll
+    for (int e = 0; e < kUnroll; ++e) {
+      const float* xr = X + (int64_t)col[k + e] * ldx;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[e][c], 0.f);
+    }
+#pragma unroll
+    for (int e = 0; e < kUnroll; ++e) {
+      float w = 1.f, dc = 1.f;
+      if constexpr (HAS_W) w = ew[eslot ? eslot[k + e] : k + e];
+      if constexpr (NORM == 2) {
+        const int cc = col[k + e];
+        dc = (float)(norm_ptr[cc + 1] - norm_ptr[cc]);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+          float tv = HAS_W ? v[e][c][i] * w : v[e][c][i];
+          if constexpr (NORM == 2) tv = tv / dc;
+          acc[c][i] += tv;
+        }
+    }
+  }
+  for (; k < k1; ++k) {
+    float v[NC][W];
+    const float* xr = X + (int64_t)col[k] * ldx;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[c], 0.f);
+    float w = 1.f, dc = 1.f;
+    if constexpr (HAS_W) w = ew[eslot ? eslot[k] : k];
+    if constexpr (NORM == 2) {
+      const int cc = col[k];
+      dc = (float)(norm_ptr[cc + 1] - norm_ptr[cc]);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        float tv = HAS_W ? v[c][i] * w : v[c][i];
+        if constexpr (NORM == 2) tv = tv / dc;
+        acc[c][i] += tv;
+      }
+  }
+  if (slot < 0) {
+    if constexpr (NORM == 1) {
+      const int d = ptr[row + 1] - ptr[row];
+      if (d > 0) {
+        const float fd = (float)d;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int i = 0; i < W; ++i) acc[c][i] = acc[c][i] / fd;
+      }
+    }
+    float* orow = out + (int64_t)row * ldo;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) store_tile<W>(orow, (c * kWave + lane) * W, F, acc[c]);
+  } else {
+    float* wr = ws + (int64_t)slot * ldw;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) store_tile<W>(wr, (c * kWave + lane) * W, F, acc[c]);
+  }
+}
+
+// ---- DGL-form scatter backward (float atomics) ----------------------------------------
+__global__ __launch_bounds__(kBlock) void fill2d_kernel(float* __restrict__ x, int64_t ldx,
+                                                        int64_t rows, int cols, float val) {
+  const int64_t n = rows * (int64_t)cols;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i / cols;
+    const int c = (int)(i - r * cols);
+    x[r * ldx + c] = val;
+  }
+}
+
+template <typename A, bool HAS_W>
+__global__ __launch_bounds__(kBlock) void max_bwd_scatter_kernel(
+    const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
+    const int32_t* __restrict__ eslot, const float* __restrict__ ew, int64_t n_rows,
+    const A* __restrict__ arg, int64_t lda, const float* __restrict__ dout, int64_t ldd, int F,
+    float* __restrict__ dx, int64_t ldx) {
+  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int rs = ptr[row];
+  for (int f = lane_id(); f < F; f += kWave) {
+    const int a = (int)arg[row * lda + f];
+    if (a == arg_none<A>()) continue;
+    const int k = rs + a;
+    const int u = col[k];
+    float d = dout[row * ldd + f];
+    if (HAS_W) d = ew[eslot ? eslot[k] : k] * d;
+    atomicAdd(dx + (int64_t)u * ldx + f, d);
+  }
+}
+
+template <typename A>
+__global__ __launch_bounds__(kBlock) void argpos_to_src_kernel(
+    const int32_t* __restrict__ ptr, const int32_t* __restrict__ col, int64_t n_rows,
+    const A* __restrict__ arg, int64_t lda, int F, int64_t* __restrict__ argx, int64_t ldx) {
+  const int64_t n = n_rows * (int64_t)F;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t v = i / F;
+    const int f = (int)(i - v * F);
+    const int a = (int)arg[v * lda + f];
+    argx[v * ldx + f] = a == arg_none<A>() ? -1 : (int64_t)col[ptr[v] + a];
+  }
+}
+
+// ---- host-side dispatch helpers --------------------------------------------------------
+inline int grid_for(int64_t n_work) {
+  return (int)((n_work + kWavesPerBlock - 1) / kWavesPerBlock);
+}
+
+inline int hip_status(const char* who) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pg::set_error((int)e, "%s: launch failed: %s", who, hipGetErrorString(e));
+  return pg::ok();
+}
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// workspace layout: [values: n_slots x ldw floats][args: n_slots x ldw A], 256-B aligned
+inline int64_t ws_ld(int64_t F) { return round_up(F, 4); }
+
+// Feature tiles per launch: the kernel is instantiated for F <= kFTile; wider F is
+// processed in tiles by offsetting the feature pointers.
+constexpr int kFTileVec = kMaxNC * kWave * 4;        // 1024
+constexpr int kFTileScalar = kMaxNCScalar * kWave;   // 1024
+
+template <typename Fn>
+int dispatch_nc_vec(int nc, Fn&& fn) {
+  switch (nc) {
+    case 1: return fn(std::integral_constant<int, 1>{});
+    case 2: return fn(std::integral_constant<int, 2>{});
+    case 3: return fn(std::integral_constant<int, 3>{});
+    case 4: return fn(std::integral_constant<int, 4>{});
+  }
+  return PG_ERR_UNSUPPORTED;
+}
+
+template <typename Fn>
+int dispatch_nc_scalar(int nc, Fn&& fn) {
+  switch (nc) {
+    case 1: return fn(std::integral_constant<int, 1>{});
+    case 2: return fn(std::integral_constant<int, 2>{});
+    case 3: return fn(std::integral_constant<int, 3>{});
+    case 4: return fn(std::integral_constant<int, 4>{});
+    case 5: return fn(std::integral_constant<int, 5>{});
+    case 6: return fn(std::integral_constant<int, 6>{});
+    case 7: return fn(std::integral_constant<int, 7>{});
+    case 8: return fn(std::integral_constant<int, 8>{});
+    case 9: return fn(std::integral_constant<int, 9>{});
+    case 10: return fn(std::integral_constant<int, 10>{});
+    case 11: return fn(std::integral_constant<int, 11>{});
+    case 12: return fn(std::integral_constant<int, 12>{});
+    case 13: return fn(std::integral_constant<int, 13>{});
+    case 14: return fn(std::integral_constant<int, 14>{});
+    case 15: return fn(std::integral_constant<int, 15>{});
+    case 16: return fn(std::integral_constant<int, 16>{});
+  }
+  return PG_ERR_UNSUPPORTED;
+}
+
+struct TilePlan {
+  bool vec;
+  int64_t tile;
+};
+
+inline TilePlan plan_tiles(int64_t F, std::initializer_list<int64_t> lds,
+                           std::initializer_list<const void*> ptrs) {
+  bool vec = (F % 4) == 0;
+  for (int64_t l : lds) vec = vec && (l % 4) == 0;
+  for (const void* p : ptrs) vec = vec && (p == nullptr || aligned16(p));
+  return {vec, vec ? (int64_t)kFTileVec : (int64_t)kFTileScalar};
+}
+
+template <typename A>
+int launch_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
+                   int64_t ldo, A* arg, int64_t lda, float* ws_val, A* ws_arg, int64_t ldw,
+                   hipStream_t st) {
+  // argpos rows: u16 x4 = 8 B -> need 8-B alignment only; treat via the same 16-B check on
+  // the float operands and an 8-B check on arg.
+  TilePlan tp = plan_tiles(F, {ldx, ldo, lda}, {X, out, ws_val});
+  if (tp.vec && (((uintptr_t)arg & (4 * sizeof(A) - 1)) != 0 ||
+                 ((uintptr_t)ws_arg & (4 * sizeof(A) - 1)) != 0))
+    tp.vec = false;
+  if (!tp.vec) tp.tile = kFTileScalar;
+  const bool has_w = g->ew != nullptr;
+  const int blocks = grid_for(g->n_items);
+  for (int64_t f0 = 0; f0 < F; f0 += tp.tile) {
+    const int Ft = (int)std::min<int64_t>(tp.tile, F - f0);
+    auto go = [&](auto nc_c, auto w_c, auto hw_c) -> int {
+      constexpr int NC = decltype(nc_c)::value;
+      constexpr int W = decltype(w_c)::value;
+      constexpr bool HW = decltype(hw_c)::value;
+      hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A>), dim3(blocks), dim3(kBlock), 0, st,
+                         g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
+                         X + f0, ldx, Ft, out + f0, ldo, arg + f0, lda,
+                         ws_val ? ws_val + f0 : nullptr, ws_arg ? ws_arg + f0 : nullptr, ldw);
+      return PG_OK;
+    };
+    int rc;
+    if (tp.vec) {
+      const int nc = (Ft + 255) / 256;
+      rc = has_w ? dispatch_nc_vec(nc, [&](auto n) { return go(n, std::integral_constant<int, 4>{}, std::true_type{}); })
+                 : dispatch_nc_vec(nc, [&](auto n) { return go(n, std::integral_constant<int, 4>{}, std::false_type{}); });
+    } else {
+      const int nc = (Ft + 63) / 64;
+      rc = has_w ? dispatch_nc_scalar(nc, [&](auto n) { return go(n, std::integral_constant<int, 1>{}, std::true_type{}); })
+                 : dispatch_nc_scalar(nc, [&](auto n) { return go(n, std::integral_constant<int, 1>{}, std::false_type{}); });
+    }
+    if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_max_fwd: unsupported feature tile");
+    if (g->n_merges > 0) {
+      hipLaunchKernelGGL((max_merge_kernel<A>), dim3(grid_for(g->n_merges)), dim3(kBlock), 0, st,
+                         (const int4*)g->merges, (int)g->n_merges, Ft, ws_val + f0, ws_arg + f0,
+                         ldw, out + f0, ldo, arg + f0, lda);
+    }
+  }
+  return hip_status("pg_spmm_max_fwd");
+}
+
+template <typename A>
+int launch_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const A* arg, int64_t lda,
+                   const float* dout, int64_t ldd, int64_t F, const float* mask, int64_t ldm,
+                   float* dx, int64_t ldx, float* ws, int64_t ldw, hipStream_t st) {
+  TilePlan tp = plan_tiles(F, {lda, ldd, ldx, mask ? ldm : 4}, {dout, dx, mask, ws});
+  if (tp.vec && ((uintptr_t)arg & (4 * sizeof(A) - 1)) != 0) tp.vec = false;
+  if (!tp.vec) tp.tile = kFTileScalar;
+  const bool has_w = g->ew != nullptr;
+  const int blocks = grid_for(gt->n_items);
+  for (int64_t f0 = 0; f0 < F; f0 += tp.tile) {
+    const int Ft = (int)std::min<int64_t>(tp.tile, F - f0);
+    auto go = [&](auto nc_c, auto w_c, auto hw_c) -> int {
+      constexpr int NC = decltype(nc_c)::value;
+      constexpr int W = decltype(w_c)::value;
+      constexpr bool HW = decltype(hw_c)::value;
+      hipLaunchKernelGGL((max_bwd_kernel<W, NC, HW, A>), dim3(blocks), dim3(kBlock), 0, st,
+                         g->ptr, g->ew, gt->ptr, gt->col, gt->eslot, (const int4*)gt->items,
+                         (int)gt->n_items, arg + f0, lda, dout + f0, ldd, Ft,
+                         mask ? mask + f0 : nullptr, ldm, dx + f0, ldx, ws ? ws + f0 : nullptr,
+                         ldw);
+      return PG_OK;
+    };
+    int rc;
+    if (tp.vec) {
+      const int nc = (Ft + 255) / 256;
+      rc = has_w ? dispatch_nc_vec(nc, [&](auto n) { return go(n, std::integral_constant<int, 4>{}, std::true_type{}); })
+                 : dispatch_nc_vec(nc, [&](auto n) { return go(n, std::integral_constant<int, 4>{}, std::false_type{}); });
+    } else {
+      const int nc = (Ft + 63) / 64;
+      rc = has_w ? dispatch_nc_scalar(nc, [&](auto n) { return go(n, std::integral_constant<int, 1>{}, std::true_type{}); })
+                 : dispatch_nc_scalar(nc, [&](auto n) { return go(n, std::integral_constant<int, 1>{}, std::false_type{}); });
+    }
+    if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_max_bwd: unsupported feature tile");
+    if (gt->n_merges > 0) {
+      hipLaunchKernelGGL(sum_merge_kernel, dim3(grid_for(gt->n_merges)), dim3(kBlock), 0, st,
+                         (const int4*)gt->merges, (int)gt->n_merges, Ft, ws + f0, ldw, gt->ptr, 0,
+                         mask ? mask + f0 : nullptr, ldm, dx + f0, ldx);
+    }
+  }
+  return hip_status("pg_spmm_max_bwd");
+}
+
+int check_ws(size_t have, size_t need, const char* who) {
+  if (have < need)
+    return pg::set_error(PG_ERR_WORKSPACE, "%s: workspace %zu B < required %zu B", who, have, need);
+  return PG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t pg_spmm_max_fwd_workspace(const pg_csr_t* g, int64_t F, int arg_kind) {
+  if (!g || g->n_slots <= 0 || F <= 0) return 0;
+  const int64_t ldw = ws_ld(F);
+  const size_t vals = round_up(g->n_slots * ldw * 4, 256);
+  const size_t args = round_up(g->n_slots * ldw * (int64_t)pg::arg_bytes(arg_kind), 256);
+  return vals + args;
+}
+
+int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
+                    int64_t ldo, void* argpos, int64_t lda, int arg_kind, void* ws,
+                    size_t ws_bytes, pg_stream_t stream) {
+  PG_TRY(pg::check_csr(g, "pg_spmm_max_fwd", true));
+  if (!pg::valid_arg_kind(arg_kind))
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: bad arg_kind %d", arg_kind);
+  if (F < 0 || ldx < F || ldo < F || lda < F)
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: bad F/leading dims");
+  if (arg_kind == PG_ARG_U16 && g->max_deg >= 0xFFFF)
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: max degree %d needs PG_ARG_I32",
+                         g->max_deg);
+  if (F == 0 || g->n_rows == 0) return pg::ok();
+  if (!X || !out || !argpos) return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: NULL buffer");
+  const size_t need = pg_spmm_max_fwd_workspace(g, F, arg_kind);
+  PG_TRY(check_ws(ws_bytes, need, "pg_spmm_max_fwd"));
+  const int64_t ldw = ws_ld(F);
+  float* ws_val = need ? (float*)ws : nullptr;
+  void* ws_arg = need ? (char*)ws + round_up(g->n_slots * ldw * 4, 256) : nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  if (arg_kind == PG_ARG_U16)
+    return launch_max_fwd<uint16_t>(g, X, ldx, F, out, ldo, (uint16_t*)argpos, lda, ws_val,
+                                    (uint16_t*)ws_arg, ldw, st);
+  return launch_max_fwd<int32_t>(g, X, ldx, F, out, ldo, (int32_t*)argpos, lda, ws_val,
+                                 (int32_t*)ws_arg, ldw, st);
+}
+
+size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
+  if (!gt || gt->n_slots <= 0 || F <= 0) return 0;
+  return round_up(gt->n_slots * ws_ld(F) * 4, 256);
+}
+
+int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
+                    int arg_kind, const float* dout, int64_t ldd, int64_t F,
+                    const float* mask_src, int64_t ldm, float* dx, int64_t ldx, void* ws,
+                    size_t ws_bytes, pg_stream_t stream) {
+  PG_TRY(pg::check_csr(g, "pg_spmm_max_bwd", false));
+  PG_TRY(pg::check_csr(gt, "pg_spmm_max_bwd", true));
+  if (!pg::valid_arg_kind(arg_kind))
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: bad arg_kind %d", arg_kind);
+  if (gt->n_cols != g->n_rows || gt->nnz != g->nnz)
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: gt is not the transpose of g");
+  if (F < 0 || ldd < F || ldx < F || lda < F || (mask_src && ldm < F))
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: bad F/leading dims");
+  if (F == 0 || gt->n_rows == 0) return pg::ok();
+  if (!argpos || !dout || !dx) return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: NULL buffer");
+  const size_t need = pg_spmm_max_bwd_workspace(gt, F);
+  PG_TRY(check_ws(ws_bytes, need, "pg_spmm_max_bwd"));
+  hipStream_t st = (hipStream_t)stream;
+  float* w = need ? (float*)ws : nullptr;
+  if (arg_kind == PG_ARG_U16)
+    return launch_max_bwd<uint16_t>(g, gt, (const uint16_t*)argpos, lda, dout, ldd, F, mask_src,
+                                    ldm, dx, ldx, w, ws_ld(F), st);
+  return launch_max_bwd<int32_t>(g, gt, (const int32_t*)argpos, lda, dout, ldd, F, mask_src, ldm,
+                                 dx, ldx, w, ws_ld(F), st);
+}
+
+int pg_spmm_max_bwd_scatter(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,
+                            const float* dout, int64_t ldd, int64_t F, float* dx, int64_t ldx,
+                            int64_t n_src, pg_stream_t stream) {
+  PG_TRY(pg::check_csr(g, "pg_spmm_max_bwd_scatter", false));
+  if (!pg::valid_arg_kind(arg_kind))
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd_scatter: bad arg_kind %d", arg_kind);
+  if (F < 0 || ldd < F || ldx < F || lda < F || n_src < g->n_cols)
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd_scatter: bad F/leading dims");
+  if (F == 0) return pg::ok();
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n_fill = n_src * F;
+  const int fill_blocks = (int)std::min<int64_t>(4096, (n_fill + kBlock - 1) / kBlock);
+  if (fill_blocks > 0)
+    hipLaunchKernelGGL(fill2d_kernel, dim3(fill_blocks), dim3(kBlock), 0, st, dx, ldx, n_src,
+                       (int)F, 0.f);
+  const int blocks = grid_for(g->n_rows);
+  if (blocks > 0) {
+    const bool hw = g->ew != nullptr;
+    if (arg_kind == PG_ARG_U16) {
+      if (hw)
+        hipLaunchKernelGGL((max_bwd_scatter_kernel<uint16_t, true>), dim3(blocks), dim3(kBlock), 0, st,
+                           g->ptr, g->col, g->eslot, g->ew, g->n_rows, (const uint16_t*)argpos, lda,
+                           dout, ldd, (int)F, dx, ldx);
+      else
+        hipLaunchKernelGGL((max_bwd_scatter_kernel<uint16_t, false>), dim3(blocks), dim3(kBlock), 0, st,
+                           g->ptr, g->col, g->eslot, g->ew, g->n_rows, (const uint16_t*)argpos, lda,
+                           dout, ldd, (int)F, dx, ldx);
+    } else {
+      if (hw)
+        hipLaunchKernelGGL((max_bwd_scatter_kernel<int32_t, true>), dim3(blocks), dim3(kBlock), 0, st,
+                           g->ptr, g->col, g->eslot, g->ew, g->n_rows, (const int32_t*)argpos, lda,
+                           dout, ldd, (int)F, dx, ldx);
+      else
+        hipLaunchKernelGGL((max_bwd_scatter_kernel<int32_t, false>), dim3(blocks), dim3(kBlock), 0, st,
+                           g->ptr, g->col, g->eslot, g->ew, g->n_rows, (const int32_t*)argpos, lda,
+                           dout, ldd, (int)F, dx, ldx);
+    }
+  }
+  return hip_status("pg_spmm_max_bwd_scatter");
+}
+
+size_t pg_spmm_sum_workspace(const pg_csr_t* g, int64_t F) {
+  if (!g || g->n_slots <= 0 || F <= 0) return 0;
+  return round_up(g->n_slots * ws_ld(F) * 4, 256);
+}
+
+int pg_spmm_sum(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, int norm_mode,
+                const int32_t* norm_ptr, float* out, int64_t ldo, void* ws, size_t ws_bytes,
+                pg_stream_t stream) {
+  PG_TRY(pg::check_csr(g, "pg_spmm_sum", true));
+  if (F < 0 || ldx < F || ldo < F)
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_sum: bad F/leading dims");
+  if (norm_mode < 0 || norm_mode > 2 || (norm_mode == 2 && !norm_ptr))
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_sum: bad norm_mode %d", norm_mode);
+  if (F == 0 || g->n_rows == 0) return pg::ok();
+  if (!X || !out) return pg::set_error(PG_ERR_INVALID, "pg_spmm_sum: NULL buffer");
+  const size_t need = pg_spmm_sum_workspace(g, F);
+  PG_TRY(check_ws(ws_bytes, need, "pg_spmm_sum"));
+  float* w = need ? (float*)ws : nullptr;
+  const int64_t ldw = ws_ld(F);
+  hipStream_t st = (hipStream_t)stream;
+  TilePlan tp = plan_tiles(F, {ldx, ldo}, {X, out, w});
+  const bool has_w = g->ew != nullptr;
+  const int blocks = grid_for(g->n_items);
+  for (int64_t f0 = 0; f0 < F; f0 += tp.tile) {
+    const int Ft = (int)std::min<int64_t>(tp.tile, F - f0);
+    auto go = [&](auto nc_c, auto w_c, auto hw_c, auto norm_c) -> int {
+      constexpr int NC = decltype(nc_c)::value;
+      constexpr int W = decltype(w_c)::value;
+      constexpr bool HW = decltype(hw_c)::value;
+      constexpr int NORM = decltype(norm_c)::value;
+      hipLaunchKernelGGL((sum_kernel<W, NC, HW, NORM>), dim3(blocks), dim3(kBlock), 0, st, g->ptr,
+                         g->col, g->eslot, g->ew, norm_ptr, (const int4*)g->items, (int)g->n_items,
+                         X + f0, ldx, Ft, out + f0, ldo, w ? w + f0 : nullptr, ldw);
+      return PG_OK;
+    };
+    auto by_norm = [&](auto nc_c, auto w_c, auto hw_c) -> int {
+      switch (norm_mode) {
+        case 0: return go(nc_c, w_c, hw_c, std::integral_constant<int, 0>{});
+        case 1: return go(nc_c, w_c, hw_c, std::integral_constant<int, 1>{});
+        default: return go(nc_c, w_c, hw_c, std::integral_constant<int, 2>{});
+      }
+    };
+    int rc;
+    if (tp.vec) {
+      const int nc = (Ft + 255) / 256;
+      rc = has_w ? dispatch_nc_vec(nc, [&](auto n) { return by_norm(n, std::integral_constant<int, 4>{}, std::true_type{}); })
+                 : dispatch_nc_vec(nc, [&](auto n) { return by_norm(n, std::integral_constant<int, 4>{}, std::false_type{}); });
+    } else {
+      const int nc = (Ft + 63) / 64;
+      rc = has_w ? dispatch_nc_scalar(nc, [&](auto n) { return by_norm(n, std::integral_constant<int, 1>{}, std::true_type{}); })
+                 : dispatch_nc_scalar(nc, [&](auto n) { return by_norm(n, std::integral_constant<int, 1>{}, std::false_type{}); });
+    }
+    if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_sum: unsupported feature tile");
+    if (g->n_merges > 0)
+      hipLaunchKernelGGL(sum_merge_kernel, dim3(grid_for(g->n_merges)), dim3(kBlock), 0, st,
+                         (const int4*)g->merges, (int)g->n_merges, Ft, w + f0, ldw, g->ptr,
+                         norm_mode == 1 ? 1 : 0, nullptr, 0, out + f0, ldo);
+  }
+  return hip_status("pg_spmm_sum");
+}
+
+int pg_argpos_to_src(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,
+                     int64_t F, int64_t* argx, int64_t ldx, pg_stream_t stream) {
+  PG_TRY(pg::check_csr(g, "pg_argpos_to_src", false));
+  if (!pg::valid_arg_kind(arg_kind))
+    return pg::set_error(PG_ERR_INVALID, "pg_argpos_to_src: bad arg_kind %d", arg_kind);
+  if (F < 0 || lda < F || ldx < F)
+    return pg::set_error(PG_ERR_INVALID, "pg_argpos_to_src: bad F/leading dims");
+  const int64_t n = g->n_rows * F;
+  if (n == 0) return pg::ok();
+  const int blocks = (int)std::min<int64_t>(4096, (n + kBlock - 1) / kBlock);
+  hipStream_t st = (hipStream_t)stream;
+  if (arg_kind == PG_ARG_U16)
+    hipLaunchKernelGGL((argpos_to_src_kernel<uint16_t>), dim3(blocks), dim3(kBlock), 0, st, g->ptr,
+                       g->col, g->n_rows, (const uint16_t*)argpos, lda, (int)F, argx, ldx);
+  else
+    hipLaunchKernelGGL((argpos_to_src_kernel<int32_t>), dim3(blocks), dim3(kBlock), 0, st, g->ptr,
+                       g->col, g->n_rows, (const int32_t*)argpos, lda, (int)F, argx, ldx);
+  return hip_status("pg_argpos_to_src");
+}
+
+}  // extern "C"

@@ -1,0 +1,129 @@
+"""ctypes binding of libplagnn.so (the C-ABI declared in include/plagnn.h).
+
+torch is imported first on purpose: libplagnn.so links the HIP runtime by SONAME
+(libamdhip64.so.7) and must bind to the copy PyTorch already loaded, so both share one
+runtime, one device context and the same streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load order: see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libplagnn.so")
+
+PG_ARG_U16 = 16
+PG_ARG_I32 = 32
+PG_ACT_NONE = 0
+PG_ACT_RELU = 1
+PG_ACT_LEAKY = 2
+
+
+class PgCsr(ctypes.Structure):
+    """pg_csr_t (include/plagnn.h)."""
+
+    _fields_ = [
+        ("n_rows", ctypes.c_int64),
+        ("n_cols", ctypes.c_int64),
+        ("nnz", ctypes.c_int64),
+        ("ptr", ctypes.c_void_p),
+        ("col", ctypes.c_void_p),
+        ("eslot", ctypes.c_void_p),
+        ("ew", ctypes.c_void_p),
+        ("items", ctypes.c_void_p),
+        ("n_items", ctypes.c_int64),
+        ("merges", ctypes.c_void_p),
+        ("n_merges", ctypes.c_int64),
+        ("n_slots", ctypes.c_int64),
+        ("max_deg", ctypes.c_int32),
+        ("chunk", ctypes.c_int32),
+    ]
+
+
+_i = ctypes.c_int
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+_d = ctypes.c_double
+_sz = ctypes.c_size_t
+_vp = ctypes.c_void_p
+_csr = ctypes.POINTER(PgCsr)
+
+# name -> (restype, argtypes); every symbol of include/plagnn.h
+SIGNATURES = {
+    "pg_csr_from_coo": (_i, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp]),
+    "pg_csr_transpose": (_i, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp]),
+    "pg_schedule_count": (_i, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "pg_schedule_build": (_i, [_vp, _i64, _i32, _vp, _vp]),
+    "pg_spmm_max_fwd_workspace": (_sz, [_csr, _i64, _i]),
+    "pg_spmm_max_fwd": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i, _vp, _sz, _vp]),
+    "pg_spmm_max_bwd_workspace": (_sz, [_csr, _i64]),
+    "pg_spmm_max_bwd": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
+                             _vp, _sz, _vp]),
+    "pg_spmm_max_bwd_scatter": (_i, [_csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
+    "pg_spmm_sum_workspace": (_sz, [_csr, _i64]),
+    "pg_spmm_sum": (_i, [_csr, _vp, _i64, _i64, _i, _vp, _vp, _i64, _vp, _sz, _vp]),
+    "pg_argpos_to_src": (_i, [_csr, _vp, _i64, _i, _i64, _vp, _i64, _vp]),
+    "pg_bias_act": (_i, [_vp, _i64, _i64, _i64, _vp, _i, _f, _vp]),
+    "pg_act_bwd": (_i, [_vp, _i64, _vp, _i64, _i64, _i64, _i, _f, _vp]),
+    "pg_col_sum_workspace": (_sz, [_i64, _i64]),
+    "pg_col_sum": (_i, [_vp, _i64, _i64, _i64, _vp, _i, _vp, _sz, _vp]),
+    "pg_sigmoid_multi_loss_workspace": (_sz, [_i64, _i32]),
+    "pg_sigmoid_multi_loss": (_i, [_vp, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _i64,
+                                   _vp, _vp, _i64, _vp, _sz, _vp]),
+    "pg_adam_prepare": (_i, [_vp, _d, _d, _d, _vp]),
+    "pg_adam_apply": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _d, _d, _d, _d, _vp]),
+    "pg_gemm_f32_workspace": (_sz, [_i64, _i64, _i64, _i]),
+    "pg_gemm_f32": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _vp,
+                         _i, _f, _i, _vp, _sz, _vp]),
+    "pg_spmm_max_fwd_cpu": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i]),
+    "pg_spmm_max_bwd_cpu": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64]),
+    "pg_spmm_sum_cpu": (_i, [_csr, _vp, _i64, _i64, _i, _vp, _vp, _i64]),
+    "pg_argpos_to_src_cpu": (_i, [_csr, _vp, _i64, _i, _i64, _vp, _i64]),
+    "pg_last_error_string": (ctypes.c_char_p, []),
+    "pg_version": (_i, []),
+}
+
+_LIB = None
+
+
+class PlagnnError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libplagnn.so. Raises (never falls back) when it has not been built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise PlagnnError(
+                f"{LIB_PATH} is missing: build the HIP extension first "
+                "(make -C pla-gnn_amd, or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        msg = lib().pg_last_error_string().decode(errors="replace")
+        raise PlagnnError(f"{name} failed (code {rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def stream_handle(device: torch.device):
+    """hipStream_t of torch's current stream on `device` (as an int for ctypes)."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

@@ -1,0 +1,453 @@
+"""TrainEngine — the full PLA-GNN training step as one explicit, graph-captured sequence of
+engine kernels.
+
+One step is exactly the reference's epoch body (code/train.py:197-207):
+  optimizer.zero_grad(); logits = model(g, features)            (model.py:19-31)
+  train_loss = multi_loss(logits[train_index], labels[train_index], w); backward(); Adam.step()
+  val_loss = multi_loss(logits[val_index], ...)                 (same pre-step logits)
+computed without autograd: forward and backward are written out layer by layer and the
+whole step is captured once into a HIP graph (torch.cuda.CUDAGraph) and replayed.
+
+Layout in HBM (all fp32, row-major, every width padded to a multiple of 4 with zero pads
+that stay exactly zero through forward, backward and Adam):
+  * parameters: ONE flat buffer (Adam is one launch, a multi-GPU all-reduce is one
+    bucket). Per SAGE layer l (Fi -> Fo): Wpool[Fi][Fi], bpool[Fi],
+    Wcat[Fo][2Fi] = [Wself | Wneigh] (so Y = [H | M] @ Wcat^T is a single K = 2Fi GEMM),
+    b[Fo]; then liner1 W1/b1 and liner2 W2/b2.
+  * activations: HM_l[N][2Fi] = [H_l | M_l] — the layer's input H_l (the previous layer's
+    leaky_relu output, written there directly by that layer's GEMM epilogue) beside the
+    max-aggregated neighbourhood M_l (written there by the SpMM); P_l[N][Fi]
+    (relu(fc_pool)); argpos_l[N][Fi] (u16 winning in-row positions).
+"""
+from __future__ import annotations
+
+import contextlib
+from collections import defaultdict
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib, ops
+from ._lib import call, ptr
+from .graph import CSRGraph, DeviceGraph
+from .ops import LEAKY_SLOPE, round4
+
+RELU, LEAKY, NONE = _lib.PG_ACT_RELU, _lib.PG_ACT_LEAKY, _lib.PG_ACT_NONE
+
+
+class _Flat:
+    """Named, padded views into one flat fp32 buffer."""
+
+    def __init__(self):
+        self.layout: List = []  # (name, shape_padded, shape_true, offset)
+        self.size = 0
+
+    def add(self, name, shape_p, shape_t):
+        n = int(np.prod(shape_p))
+        self.layout.append((name, tuple(shape_p), tuple(shape_t), self.size))
+        self.size += (n + 63) // 64 * 64  # 256-B aligned views
+
+    def views(self, buf: torch.Tensor) -> Dict[str, torch.Tensor]:
+        return {name: buf[off:off + int(np.prod(sp))].view(*sp) for name, sp, _, off in self.layout}
+
+
+class TrainEngine:
+    def __init__(self, graph: CSRGraph, features: torch.Tensor, labels: torch.Tensor,
+                 dims: Sequence[int], class_weight, train_index, val_index=None,
+                 lr: float = 5e-5, betas=(0.9, 0.999), eps: float = 1e-8,
+                 device="cuda", edge_weight: Optional[torch.Tensor] = None,
+                 params: Optional[Dict[str, torch.Tensor]] = None, seed: int = 0):
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("TrainEngine runs on a HIP device; use the dgl shim for -d cpu")
+        self.dims = list(dims)
+        self.L = len(self.dims) - 3
+        N = graph.num_nodes
+        self.N = N
+        self.dg: DeviceGraph = graph.on(self.device)
+        self.ews = self.dg.edge_weight_slots(edge_weight)
+        self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
+        C = self.dims[-1]
+        self.C = C
+        dev = self.device
+
+        # ---- parameters (flat, padded) ----
+        fl = _Flat()
+        pd = [round4(d) for d in self.dims]
+        self.pd = pd
+        for l in range(self.L):
+            Fi, Fo = pd[l], pd[l + 1]
+            fi, fo = self.dims[l], self.dims[l + 1]
+            fl.add(f"conv{l + 1}.Wpool", (Fi, Fi), (fi, fi))
+            fl.add(f"conv{l + 1}.bpool", (Fi,), (fi,))
+            fl.add(f"conv{l + 1}.Wcat", (Fo, 2 * Fi), (fo, 2 * fi))
+            fl.add(f"conv{l + 1}.b", (Fo,), (fo,))
+        fl.add("liner1.W", (pd[-2], pd[-3]), (self.dims[-2], self.dims[-3]))
+        fl.add("liner1.b", (pd[-2],), (self.dims[-2],))
+        fl.add("liner2.W", (pd[-1], pd[-2]), (self.dims[-1], self.dims[-2]))
+        fl.add("liner2.b", (pd[-1],), (self.dims[-1],))
+        self.flat_layout = fl
+        self.flat = torch.zeros(fl.size, dtype=torch.float32, device=dev)
+        self.gflat = torch.zeros_like(self.flat)
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self.adam_state = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.P = fl.views(self.flat)
+        self.G = fl.views(self.gflat)
+        if params is None:
+            from .model import GNN
+
+            torch.manual_seed(seed)
+            params = GNN(self.dims).state_dict()
+        self.load_state_dict(params)
+
+        # ---- inputs ----
+        if features.shape != (N, self.dims[0]):
+            raise ValueError(f"features must be ({N}, {self.dims[0]})")
+        self.labels = torch.zeros(N, pd[-1], dtype=torch.float32, device=dev)
+        self.labels[:, :C] = labels.to(dev, torch.float32)
+        cw = np.asarray(class_weight, dtype=np.float64)
+        if cw.shape != (C,):
+            raise ValueError(f"class_weight must have {C} entries")
+        cwp = np.empty(2 * C, np.float32)
+        cwp[0::2] = cw.astype(np.float32)          # (float)w_c
+        cwp[1::2] = (cw + 1.0).astype(np.float32)  # (float)(w_c + 1)
+        self.cw = torch.from_numpy(cwp).to(dev)
+        self.train_index = torch.as_tensor(np.asarray(train_index, np.int32), device=dev)
+        self.val_index = None if val_index is None else torch.as_tensor(
+            np.asarray(val_index, np.int32), device=dev)
+
+        # ---- activations ----
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.HM, self.Pl, self.arg = [], [], []
+        for l in range(self.L):
+            Fi = pd[l]
+            self.HM.append(torch.zeros(N, 2 * Fi, **f32))
+            self.Pl.append(torch.zeros(N, Fi, **f32))
+            self.arg.append(torch.zeros(N, Fi, dtype=self.dg.arg_dtype, device=dev))
+        self.HM[0][:, :self.dims[0]] = features.to(dev, torch.float32)
+        self.A3 = torch.zeros(N, pd[-3], **f32)
+        self.A4 = torch.zeros(N, pd[-2], **f32)
+        self.Z = torch.zeros(N, pd[-1], **f32)
+        self.prob = torch.zeros(N, pd[-1], **f32)
+        self.loss = torch.zeros(2, **f32)  # [train, val]
+        # backward buffers
+        self.dZ = torch.zeros(N, pd[-1], **f32)
+        self.dA4 = torch.zeros(N, pd[-2], **f32)
+        self.dA3 = torch.zeros(N, pd[-3], **f32)
+        self.dHM = [torch.zeros(N, 2 * pd[l], **f32) for l in range(self.L)]
+        self.dP = [torch.zeros(N, pd[l], **f32) for l in range(self.L)]
+
+        # ---- workspace (one buffer, sized for the largest call) ----
+        L = _lib.lib()
+        need = 0
+        for l in range(self.L):
+            Fi = pd[l]
+            need = max(need, L.pg_spmm_max_fwd_workspace(self.dg.fwd.struct(self.ews), Fi, self.dg.arg_kind))
+            need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd.struct(None), Fi))
+        self._gemm_plans = {}
+        for (M_, N_, K_) in self._wgrad_shapes():
+            sk = ops._split_k(M_, N_, K_)
+            self._gemm_plans[(M_, N_, K_)] = sk
+            need = max(need, L.pg_gemm_f32_workspace(M_, N_, K_, sk))
+        for w in pd:
+            need = max(need, L.pg_col_sum_workspace(N, w))
+        need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C))
+        self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
+        self.ws_bytes = self.ws.numel()
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.graph_adam: Optional[torch.cuda.CUDAGraph] = None
+        self.allreduce = None
+        self.steps_done = 0
+        self._timing: Optional[list] = None  # [(name, work, start_event, end_event)]
+
+    # ------------------------------------------------------------------ parameters
+    def _wgrad_shapes(self):
+        pd = self.pd
+        N = self.N
+        out = []
+        for l in range(self.L):
+            Fi, Fo = pd[l], pd[l + 1]
+            out += [(Fo, 2 * Fi, N), (Fi, Fi, N)]
+        out += [(pd[-2], pd[-3], N), (pd[-1], pd[-2], N)]
+        return out
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
+        """Load DGL/GNN32-named parameters (code/model.py names) into the padded buffer."""
+        with torch.no_grad():
+            self.flat.zero_()
+            for l in range(self.L):
+                p = f"conv{l + 1}."
+                fi, fo = self.dims[l], self.dims[l + 1]
+                self.P[p + "Wpool"][:fi, :fi] = sd[p + "fc_pool.weight"]
+                self.P[p + "bpool"][:fi] = sd[p + "fc_pool.bias"]
+                Fi = self.pd[l]
+                self.P[p + "Wcat"][:fo, :fi] = sd[p + "fc_self.weight"]
+                self.P[p + "Wcat"][:fo, Fi:Fi + fi] = sd[p + "fc_neigh.weight"]
+                if p + "bias" in sd and sd[p + "bias"] is not None:
+                    self.P[p + "b"][:fo] = sd[p + "bias"]
+            d = self.dims
+            self.P["liner1.W"][:d[-2], :d[-3]] = sd["liner1.weight"]
+            self.P["liner1.b"][:d[-2]] = sd["liner1.bias"]
+            self.P["liner2.W"][:d[-1], :d[-2]] = sd["liner2.weight"]
+            self.P["liner2.b"][:d[-1]] = sd["liner2.bias"]
+
+    def _unpad(self, views: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        out = {}
+        for l in range(self.L):
+            p = f"conv{l + 1}."
+            fi, fo, Fi = self.dims[l], self.dims[l + 1], self.pd[l]
+            out[p + "fc_pool.weight"] = views[p + "Wpool"][:fi, :fi].clone()
+            out[p + "fc_pool.bias"] = views[p + "bpool"][:fi].clone()
+            out[p + "fc_neigh.weight"] = views[p + "Wcat"][:fo, Fi:Fi + fi].clone()
+            out[p + "fc_self.weight"] = views[p + "Wcat"][:fo, :fi].clone()
+            out[p + "bias"] = views[p + "b"][:fo].clone()
+        d = self.dims
+        out["liner1.weight"] = views["liner1.W"][:d[-2], :d[-3]].clone()
+        out["liner1.bias"] = views["liner1.b"][:d[-2]].clone()
+        out["liner2.weight"] = views["liner2.W"][:d[-1], :d[-2]].clone()
+        out["liner2.bias"] = views["liner2.b"][:d[-1]].clone()
+        return out
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return self._unpad(self.P)
+
+    def grads(self) -> Dict[str, torch.Tensor]:
+        return self._unpad(self.G)
+
+    @property
+    def num_params(self) -> int:
+        return sum(int(np.prod(st)) for _, _, st, _ in self.flat_layout.layout)
+
+    # ------------------------------------------------------------------ timing
+    @contextlib.contextmanager
+    def _t(self, name: str, work: float = 0.0):
+        """HIP events around one launch on the engine's stream (diagnostic passes only)."""
+        if self._timing is None:
+            yield
+            return
+        st = torch.cuda.current_stream(self.device)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        yield
+        b.record(st)
+        self._timing.append((name, work, a, b))
+
+    def kernel_breakdown(self, reps: int = 5) -> Dict[str, Dict[str, float]]:
+        """Per-launch-site mean duration (ms) and work over `reps` eager steps, timed with
+        HIP events on the launch stream. Returns {name: {ms, work, calls}} per step."""
+        acc: Dict[str, List[float]] = defaultdict(lambda: [0.0, 0.0, 0])
+        for _ in range(reps):
+            self._timing = []
+            self.step_eager(self.allreduce)
+            torch.cuda.synchronize(self.device)
+            for name, work, a, b in self._timing:
+                r = acc[name]
+                r[0] += a.elapsed_time(b)
+                r[1] += work
+                r[2] += 1
+            self._timing = None
+        return {k: {"ms": v[0] / reps, "work": v[1] / reps, "calls": v[2] / reps} for k, v in acc.items()}
+
+    # ------------------------------------------------------------------ kernels
+    def _s(self):
+        return _lib.stream_handle(self.device)
+
+    def _gemm(self, A, B, C, transa=False, transb=False, beta=0.0, bias=None, act=NONE, tag="gemm"):
+        M = A.shape[1] if transa else A.shape[0]
+        K = A.shape[0] if transa else A.shape[1]
+        N = B.shape[0] if transb else B.shape[1]
+        sk = self._gemm_plans.get((M, N, K), 1) if (bias is None and act == NONE) else 1
+        with self._t(tag, 2.0 * M * N * K):
+            self._gemm_call(A, B, C, transa, transb, beta, bias, act, M, N, K, sk)
+
+    def _gemm_call(self, A, B, C, transa, transb, beta, bias, act, M, N, K, sk):
+        call("pg_gemm_f32", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
+             B.stride(0), beta, ptr(C), C.stride(0), ptr(bias), act, LEAKY_SLOPE, sk, ptr(self.ws),
+             self.ws_bytes, self._s())
+
+    def _colsum(self, x, out):
+        with self._t("col_sum", 4.0 * x.shape[0] * x.shape[1]):
+            call("pg_col_sum", ptr(x), x.stride(0), x.shape[0], x.shape[1], ptr(out), 0, ptr(self.ws),
+                 self.ws_bytes, self._s())
+
+    def forward(self) -> None:
+        """Logits (self.prob) and both losses; dZ = d train_loss / d z."""
+        st = self._s()
+        g = self.dg.fwd.struct(self.ews)
+        for l in range(self.L):
+            p = f"conv{l + 1}."
+            Fi = self.pd[l]
+            HM = self.HM[l]
+            H = HM[:, :Fi]
+            # P = relu(H Wpool^T + bpool)
+            self._gemm(H, self.P[p + "Wpool"], self.Pl[l], transb=True, bias=self.P[p + "bpool"], act=RELU,
+                       tag=f"gemm.fwd.pool.l{l + 1}")
+            # M = max-aggregate(P) -> right half of HM
+            M = HM[:, Fi:]
+            with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
+                call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(M), HM.stride(0), ptr(self.arg[l]),
+                     Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
+            # Y = [H | M] Wcat^T + b, leaky_relu -> next layer's input
+            out = self.HM[l + 1][:, :self.pd[l + 1]] if l + 1 < self.L else self.A3
+            self._gemm(HM, self.P[p + "Wcat"], out, transb=True, bias=self.P[p + "b"], act=LEAKY,
+                       tag=f"gemm.fwd.cat.l{l + 1}")
+        self._gemm(self.A3, self.P["liner1.W"], self.A4, transb=True, bias=self.P["liner1.b"], act=LEAKY,
+                   tag="gemm.fwd.liner1")
+        self._gemm(self.A4, self.P["liner2.W"], self.Z, transb=True, bias=self.P["liner2.b"], act=NONE,
+                   tag="gemm.fwd.liner2")
+        C = self.C
+        cp = self.pd[-1]
+        with self._t("loss"):
+            call("pg_sigmoid_multi_loss", ptr(self.Z), cp, self.N, C, ptr(self.labels), cp, ptr(self.cw),
+                 ptr(self.train_index), self.train_index.numel(), ptr(self.prob), cp, ptr(self.loss[0:1]),
+                 ptr(self.dZ), cp, ptr(self.ws), self.ws_bytes, st)
+            if self.val_index is not None and self.val_index.numel() > 0:
+                call("pg_sigmoid_multi_loss", ptr(self.Z), cp, self.N, C, ptr(self.labels), cp, ptr(self.cw),
+                     ptr(self.val_index), self.val_index.numel(), 0, cp, ptr(self.loss[1:2]), 0, cp,
+                     ptr(self.ws), self.ws_bytes, st)
+
+    def _act_bwd(self, dy, y, cols, tag):
+        with self._t(tag, 12.0 * self.N * cols):
+            call("pg_act_bwd", ptr(dy), dy.stride(0), ptr(y), y.stride(0), self.N, cols, LEAKY,
+                 LEAKY_SLOPE, self._s())
+
+    def backward(self) -> None:
+        st = self._s()
+        G, P = self.G, self.P
+        g = self.dg.fwd.struct(self.ews)
+        gt = self.dg.bwd.struct(None)
+        # liner2
+        self._gemm(self.dZ, self.A4, G["liner2.W"], transa=True, tag="gemm.wgrad.liner2")
+        self._colsum(self.dZ, G["liner2.b"])
+        self._gemm(self.dZ, P["liner2.W"], self.dA4, tag="gemm.dgrad.liner2")
+        self._act_bwd(self.dA4, self.A4, self.dA4.shape[1], "act_bwd")
+        # liner1
+        self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, tag="gemm.wgrad.liner1")
+        self._colsum(self.dA4, G["liner1.b"])
+        self._gemm(self.dA4, P["liner1.W"], self.dA3, tag="gemm.dgrad.liner1")
+        self._act_bwd(self.dA3, self.A3, self.dA3.shape[1], "act_bwd")
+        dY = self.dA3
+        for l in reversed(range(self.L)):
+            p = f"conv{l + 1}."
+            Fi = self.pd[l]
+            HM, dHM = self.HM[l], self.dHM[l]
+            # weight / bias grads of Y = [H | M] Wcat^T + b
+            self._gemm(dY, HM, G[p + "Wcat"], transa=True, tag=f"gemm.wgrad.cat.l{l + 1}")
+            self._colsum(dY, G[p + "b"])
+            # d[H | M] = dY Wcat   (layer 1: only dM is needed)
+            if l > 0:
+                self._gemm(dY, P[p + "Wcat"], dHM, tag=f"gemm.dgrad.cat.l{l + 1}")
+            else:
+                self._gemm(dY, P[p + "Wcat"][:, Fi:], dHM[:, Fi:], tag=f"gemm.dgrad.cat.l{l + 1}")
+            # max backward + relu' of fc_pool, fused
+            with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
+                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
+                     dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(self.dP[l]), Fi, ptr(self.ws),
+                     self.ws_bytes, st)
+            self._gemm(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, tag=f"gemm.wgrad.pool.l{l + 1}")
+            self._colsum(self.dP[l], G[p + "bpool"])
+            if l > 0:
+                dH = dHM[:, :Fi]
+                self._gemm(self.dP[l], P[p + "Wpool"], dH, beta=1.0, tag=f"gemm.dgrad.pool.l{l + 1}")
+                # through the previous layer's leaky_relu (its output is H = HM[:, :Fi])
+                self._act_bwd(dH, HM, Fi, "act_bwd")
+                dY = dH
+
+    def adam(self) -> None:
+        st = self._s()
+        with self._t("adam", 16.0 * self.flat.numel()):
+            call("pg_adam_prepare", ptr(self.adam_state), self.lr, self.betas[0], self.betas[1], st)
+            call("pg_adam_apply", ptr(self.flat), ptr(self.gflat), ptr(self.m), ptr(self.v),
+                 self.flat.numel(), ptr(self.adam_state), self.betas[0], self.betas[1], self.eps, 0.0, st)
+
+    def step_eager(self, allreduce=None) -> None:
+        self.forward()
+        self.backward()
+        if allreduce is not None:
+            allreduce(self.gflat)
+        self.adam()
+        self.steps_done += 1
+
+    # ------------------------------------------------------------------ graph capture
+    def capture(self, warmup: int = 2, allreduce=None) -> None:
+        """Capture the step into HIP graphs. Warm-up steps run eagerly first (they are real
+        training steps and count as such). With `allreduce` (multi-GPU data parallel),
+        forward+backward and Adam are two graphs and the gradient all-reduce runs between
+        them on the same stream."""
+        self.allreduce = allreduce
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step_eager(allreduce)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        if allreduce is None:
+            with torch.cuda.graph(self.graph):
+                self.forward()
+                self.backward()
+                self.adam()
+            self.graph_adam = None
+        else:
+            with torch.cuda.graph(self.graph):
+                self.forward()
+                self.backward()
+            self.graph_adam = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_adam):
+                self.adam()
+
+    def step(self) -> None:
+        if self.graph is None:
+            self.step_eager(getattr(self, "allreduce", None))
+            return
+        self.graph.replay()
+        if self.graph_adam is not None:
+            self.allreduce(self.gflat)
+            self.graph_adam.replay()
+        self.steps_done += 1
+
+    def losses(self):
+        return self.loss.detach().cpu().tolist()
+
+    def logits(self) -> torch.Tensor:
+        return self.prob[:, :self.C]
+
+    # ------------------------------------------------------------------ accounting
+    @property
+    def edges_per_step(self) -> int:
+        """Edges aggregated per training step: one aggregation per SAGE layer over E'
+        (self-loops included) — SURVEY.md §8(d)."""
+        return self.L * self.dg.num_edges
+
+    def spmm_bytes(self, layer: int) -> int:
+        """Algorithmic HBM bytes of one max-aggregation forward:
+        4(N+1) + 4E' + s*F*E' + s*F*N + a*F*N, s = 4 (f32), a = argpos bytes."""
+        N, E, F = self.N, self.dg.num_edges, self.pd[layer]
+        a = 2 if self.dg.arg_kind == _lib.PG_ARG_U16 else 4
+        return 4 * (N + 1) + 4 * E + 4 * F * E + 4 * F * N + a * F * N
+
+    def spmm_bwd_bytes(self, layer: int) -> int:
+        """Algorithmic bytes of one deterministic max backward (gather form): transposed
+        CSR (4(N+1) + 8E': column + slot), the argmax row of each out-neighbour
+        (a*F*E'), the upstream gradient and the relu mask read once (8*F*N), dX written
+        once (4*F*N). The dout rows of non-matching features are not needed."""
+        N, E, F = self.N, self.dg.num_edges, self.pd[layer]
+        a = 2 if self.dg.arg_kind == _lib.PG_ARG_U16 else 4
+        return 4 * (N + 1) + 8 * E + a * F * E + 12 * F * N
+
+    def flops_per_step(self) -> int:
+        """Dense GEMM flops of one step (forward + backward, layer-1 input grad skipped)."""
+        N, d = self.N, self.dims
+        f = 0
+        for l in range(self.L):
+            fi, fo = d[l], d[l + 1]
+            fwd = 2 * N * fi * fi + 2 * N * (2 * fi) * fo
+            wgrad = fwd
+            igrad = 2 * N * fo * fi + (2 * N * fo * fi + 2 * N * fi * fi if l > 0 else 0)
+            f += fwd + wgrad + igrad
+        for (a, b) in ((d[-3], d[-2]), (d[-2], d[-1])):
+            f += 3 * 2 * N * a * b
+        return f

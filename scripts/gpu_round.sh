@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU session: parity tests, then (only if no crash) a short bench and a kernel-trace
+# profile. Every GPU step has its own time limit; a crash/timeout (exit >= 2 from pytest,
+# anything non-zero from the others) ends the script.
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS=${STEPS:-20}
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+if [ $rc -ge 2 ]; then echo "pytest crashed/timed out; stopping"; exit $rc; fi
+if [ "${SKIP_BENCH:-0}" = "1" ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --steps $STEPS --warmup 5 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc2=$?
+echo "bench rc=$rc2"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err
+if [ $rc2 -ne 0 ]; then exit $rc2; fi
+if [ "${PROFILE:-1}" = "1" ]; then
+  cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps $STEPS --warmup 5 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/prof.err
+  rc3=$?; cd $GRAFT_REPO_ROOT
+  echo "rocprof rc=$rc3"; tail -3 gpurun_out/prof.err
+  exit $rc3
+fi
+exit $rc

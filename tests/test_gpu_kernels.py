@@ -1,0 +1,253 @@
+"""GPU parity of the HIP kernels, called through the C-ABI, against the oracle.
+
+Bars: the max aggregation and its argmax are bit-exact (selection, integer positions);
+the max backward is bit-exact on rows that are not split across work items (same
+ascending-destination summation order as the oracle's sequential scatter_add_) and
+within 1e-6 relative on split rows; sums / GEMMs within the fp32 tolerances stated per
+test.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import hub_graph, random_graph
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _graph(src, dst, n, chunk=256):
+    import plagnn
+
+    return plagnn.CSRGraph(src, dst, n, chunk=chunk)
+
+
+@pytest.mark.parametrize("F", [1, 3, 63, 64, 65, 256, 300, 400, 503, 504, 512, 1100])
+def test_spmm_max_fwd_bitexact(oracle_mod, F):
+    from plagnn import ops
+
+    n = 500
+    src, dst = hub_graph(n, 1500, seed=F)  # one in-hub (split rows) + one out-hub
+    g = _graph(src, dst, n)
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False)
+    rng = np.random.default_rng(F)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    X[rng.random((n, F)) < 0.4] = 0.0  # ties at zero (post-relu)
+    X[7] = X[11]  # exact positive ties between nodes
+    dg = g.on(DEV)
+    out, argpos = ops.spmm_max(dg, torch.from_numpy(X).to(DEV))
+    ref, argx, arge = oracle_mod.spmm_max(og, X)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(ops.argpos_to_src(dg, argpos).cpu().numpy(), argx)
+
+
+@pytest.mark.parametrize("F", [4, 65, 256, 503])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_max_bwd(oracle_mod, F, weighted):
+    from plagnn import ops
+
+    n = 400
+    src, dst = hub_graph(n, 1200, seed=F + 1)
+    rng = np.random.default_rng(F)
+    w = rng.uniform(-1, 2, len(src)).astype(np.float32) if weighted else None
+    g = _graph(src, dst, n)
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False, edge_weight=w)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    X[rng.random((n, F)) < 0.4] = 0.0
+    dZ = rng.standard_normal((n, F)).astype(np.float32)
+    dg = g.on(DEV)
+    ews = dg.edge_weight_slots(None if w is None else torch.from_numpy(w))
+    out, argpos = ops.spmm_max(dg, torch.from_numpy(X).to(DEV), ews)
+    ref, argx, arge = oracle_mod.spmm_max(og, X, use_weight=weighted)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    dX_ref = oracle_mod.spmm_max_bwd(og, argx, arge, dZ, use_weight=weighted)
+    dX = ops.spmm_max_backward(dg, argpos, torch.from_numpy(dZ).to(DEV), ews).cpu().numpy()
+    split_rows = set(g.bwd.merges.reshape(-1, 4)[: g.bwd.n_merges, 0].tolist())
+    exact = np.array([u not in split_rows for u in range(n)])
+    np.testing.assert_array_equal(dX[exact], dX_ref[exact])
+    np.testing.assert_allclose(dX, dX_ref, rtol=1e-5, atol=1e-5)
+    # fused relu' mask
+    mask = torch.from_numpy(X).to(DEV)
+    dXm = ops.spmm_max_backward(dg, argpos, torch.from_numpy(dZ).to(DEV), ews, mask=mask).cpu().numpy()
+    np.testing.assert_array_equal(dXm, np.where(X > 0, dX, 0.0))
+    # DGL scatter form (atomics)
+    dXs = ops.spmm_max_backward_scatter(dg, argpos, torch.from_numpy(dZ).to(DEV), ews).cpu().numpy()
+    np.testing.assert_allclose(dXs, dX_ref, rtol=1e-5, atol=1e-5)
+
+
+def test_spmm_max_int32_positions(oracle_mod):
+    """A row of >= 65535 entries forces int32 argmax positions."""
+    from plagnn import _lib, ops
+
+    n = 70
+    deg = 70000
+    rng = np.random.default_rng(0)
+    src = np.concatenate([rng.integers(0, n, deg), np.arange(n)]).astype(np.int64)
+    dst = np.concatenate([np.zeros(deg, np.int64), np.arange(n)])
+    g = _graph(src, dst, n)
+    assert g.arg_kind == _lib.PG_ARG_I32
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False)
+    X = rng.standard_normal((n, 8)).astype(np.float32)
+    dg = g.on(DEV)
+    out, argpos = ops.spmm_max(dg, torch.from_numpy(X).to(DEV))
+    ref, argx, arge = oracle_mod.spmm_max(og, X)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(ops.argpos_to_src(dg, argpos).cpu().numpy(), argx)
+
+
+def test_spmm_empty_rows_and_edges():
+    from plagnn import ops
+
+    n = 10
+    src = np.array([1, 2], np.int64)
+    dst = np.array([0, 0], np.int64)
+    g = _graph(src, dst, n)  # rows 1..9 have no in-edges
+    dg = g.on(DEV)
+    X = torch.arange(n * 4, dtype=torch.float32, device=DEV).reshape(n, 4)
+    out, argpos = ops.spmm_max(dg, X)
+    o = out.cpu()
+    assert torch.equal(o[0], X[2].cpu()) and torch.all(o[1:] == 0)
+    assert torch.all(ops.argpos_to_src(dg, argpos)[1:] == -1)
+    dX = ops.spmm_max_backward(dg, argpos, torch.ones(n, 4, device=DEV)).cpu()
+    assert torch.equal(dX[2], torch.ones(4)) and dX[1].sum() == 0 and dX[0].sum() == 0
+
+
+@pytest.mark.parametrize("mean", [False, True])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_sum_fwd_bwd(oracle_mod, mean, weighted):
+    from plagnn import ops
+
+    n, F = 300, 70
+    src, dst = hub_graph(n, 800, seed=3)
+    rng = np.random.default_rng(2)
+    w = rng.uniform(0, 1, len(src)).astype(np.float32) if weighted else None
+    g = _graph(src, dst, n)
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False, edge_weight=w)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    dg = g.on(DEV)
+    ews = dg.edge_weight_slots(None if w is None else torch.from_numpy(w))
+    Xd = torch.from_numpy(X).to(DEV).requires_grad_(True)
+    out = ops.SumAggregate.apply(Xd, dg, ews, mean)
+    ref = oracle_mod.spmm_sum(og, X, mean=mean, use_weight=weighted)
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    # backward against the dense adjacency (float64)
+    A = np.zeros((n, n))
+    for k, (s, d) in enumerate(zip(src, dst)):
+        A[d, s] += 1.0 if w is None else w[k]
+    if mean:
+        A = A / np.maximum(np.bincount(dst, minlength=n), 1)[:, None]
+    dZ = rng.standard_normal((n, F)).astype(np.float32)
+    out.backward(torch.from_numpy(dZ).to(DEV))
+    np.testing.assert_allclose(Xd.grad.cpu().numpy(), A.T @ dZ, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("shape", [(300, 200, 100), (1000, 503, 503), (37, 12, 2000), (256, 504, 24041)])
+def test_gemm_f32(ta, tb, shape):
+    from plagnn import ops
+
+    M, N, K = shape
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    ref = (A.double().t() if ta else A.double()) @ (B.double().t() if tb else B.double())
+    C = ops.gemm(A.to(DEV), B.to(DEV), transa=ta, transb=tb).cpu().double()
+    tol = 2e-6 * (K ** 0.5) * 4
+    assert (C - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item()), (C - ref).abs().max()
+
+
+def test_gemm_epilogue_and_beta():
+    from plagnn import _lib, ops
+
+    torch.manual_seed(0)
+    A = torch.randn(200, 64)
+    B = torch.randn(48, 64)
+    bias = torch.randn(48)
+    C0 = torch.randn(200, 48)
+    Cd = C0.to(DEV)
+    ops.gemm(A.to(DEV), B.to(DEV), transb=True, out=Cd, beta=1.0, bias=bias.to(DEV),
+             act=_lib.PG_ACT_LEAKY)
+    ref = torch.nn.functional.leaky_relu(A.double() @ B.double().t() + C0.double() + bias.double())
+    torch.testing.assert_close(Cd.cpu().double(), ref, rtol=1e-5, atol=1e-5)
+    # strided (padded) output view, relu
+    buf = torch.zeros(200, 52, device=DEV)
+    ops.gemm(A.to(DEV), B.to(DEV), transb=True, out=buf[:, :48], bias=bias.to(DEV), act=_lib.PG_ACT_RELU)
+    torch.testing.assert_close(buf[:, :48].cpu().double(), torch.relu(A.double() @ B.double().t() + bias.double()),
+                               rtol=1e-5, atol=1e-5)
+    assert torch.all(buf[:, 48:] == 0)
+
+
+def test_col_sum_act_bwd():
+    from plagnn import _lib, ops
+
+    torch.manual_seed(0)
+    x = torch.randn(24041, 100)
+    s = ops.col_sum(x.to(DEV)).cpu()
+    torch.testing.assert_close(s.double(), x.double().sum(0), rtol=1e-5, atol=1e-3)
+    y = torch.randn(300, 40)
+    dy = torch.randn(300, 40)
+    yd, dyd = y.to(DEV), dy.to(DEV)
+    _lib.call("pg_act_bwd", dyd.data_ptr(), 40, yd.data_ptr(), 40, 300, 40, _lib.PG_ACT_LEAKY, 0.01,
+              _lib.stream_handle(yd.device))
+    ref = torch.where(y > 0, dy, dy * 0.01)
+    torch.testing.assert_close(dyd.cpu(), ref, rtol=0, atol=0)
+
+
+def test_sigmoid_multi_loss_matches_reference_golden(oracle_mod):
+    """Loss and d loss / d prob of the fused kernel vs the reference's multi_loss
+    (golden vectors from code/train.py:89-108)."""
+    import os
+
+    from plagnn import _lib
+
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "multi_loss.npz"))
+    probs = np.clip(d["probs"].astype(np.float64), 1e-6, 1 - 1e-6)
+    z = np.log(probs / (1 - probs)).astype(np.float32)  # logits whose sigmoid ~ probs
+    p32 = torch.sigmoid(torch.from_numpy(z))
+    target = d["target"]
+    w = d["weight"]
+    n, C = z.shape
+    # oracle: multi_loss on sigmoid(z) through autograd
+    zt = torch.from_numpy(z).requires_grad_(True)
+    ref = oracle_mod.multi_loss(torch.sigmoid(zt), torch.from_numpy(target), w)
+    ref.backward()
+    cw = np.empty(2 * C, np.float32)
+    cw[0::2] = w.astype(np.float32)
+    cw[1::2] = (w + 1.0).astype(np.float32)
+    zd = torch.from_numpy(z).to(DEV)
+    lab = torch.from_numpy(target).to(DEV)
+    cwd = torch.from_numpy(cw).to(DEV)
+    idx = torch.arange(n, dtype=torch.int32, device=DEV)
+    prob = torch.empty(n, C, device=DEV)
+    loss = torch.empty(1, device=DEV)
+    dz = torch.empty(n, C, device=DEV)
+    L = _lib.lib()
+    ws = torch.empty(L.pg_sigmoid_multi_loss_workspace(n, C), dtype=torch.uint8, device=DEV)
+    _lib.call("pg_sigmoid_multi_loss", zd.data_ptr(), C, n, C, lab.data_ptr(), C, cwd.data_ptr(),
+              idx.data_ptr(), n, prob.data_ptr(), C, loss.data_ptr(), dz.data_ptr(), C, ws.data_ptr(),
+              ws.numel(), _lib.stream_handle(zd.device))
+    torch.testing.assert_close(prob.cpu(), p32, rtol=1e-6, atol=1e-7)
+    assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    torch.testing.assert_close(dz.cpu(), zt.grad, rtol=1e-5, atol=1e-8)
+
+
+def test_adam_matches_oracle_and_torch(oracle_mod):
+    from plagnn import _lib
+
+    torch.manual_seed(0)
+    n = 100_003
+    p0 = torch.randn(n)
+    p_ref = p0.clone()
+    m_ref, v_ref = torch.zeros(n), torch.zeros(n)
+    pd, md, vd = p0.to(DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    st = torch.zeros(4, device=DEV)
+    s = _lib.stream_handle(pd.device)
+    for step in range(1, 8):
+        g = torch.randn(n)
+        gd = g.to(DEV)
+        _lib.call("pg_adam_prepare", st.data_ptr(), 5e-5, 0.9, 0.999, s)
+        _lib.call("pg_adam_apply", pd.data_ptr(), gd.data_ptr(), md.data_ptr(), vd.data_ptr(), n,
+                  st.data_ptr(), 0.9, 0.999, 1e-8, 0.0, s)
+        oracle_mod.adam_step_torch110([p_ref], [g], [m_ref], [v_ref], step, 5e-5)
+    torch.testing.assert_close(pd.cpu(), p_ref, rtol=1e-6, atol=1e-9)
+    assert st[0].item() == 7.0

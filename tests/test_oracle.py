@@ -1,0 +1,117 @@
+"""The oracle itself: known-answer tests for the DGL 0.8.2 semantics it restates, and the
+golden vectors produced by the reference's own functions (tests/golden/gen_golden.py)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_csc_is_stable_by_edge_id(oracle_mod):
+    # dst 0 receives edges 3, 1, 0 (ids) -> listed in id order 0, 1, 3; self-loop (id E+v) last
+    src = [5, 2, 9, 7, 1]
+    dst = [0, 0, 1, 0, 1]
+    g = oracle_mod.OracleGraph(src, dst, 10)
+    assert list(g.indptr[:3]) == [0, 4, 7]
+    assert list(g.indices[0:4]) == [5, 2, 7, 0]
+    assert list(g.eids[0:4]) == [0, 1, 3, 5]
+    assert list(g.indices[4:7]) == [9, 1, 1]
+
+
+def test_triangle_pendant_max(oracle_mod):
+    # triangle 0-1-2 + pendant 0-3, symmetric, self-loops appended
+    r = [0, 1, 0, 2, 1, 2, 0, 3]
+    c = [1, 0, 2, 0, 2, 1, 3, 0]
+    g = oracle_mod.OracleGraph(r, c, 4)
+    X = np.array([[1.0, 0.0], [3.0, -1.0], [2.0, 5.0], [0.5, 7.0]], np.float32)
+    out, argx, _ = oracle_mod.spmm_max(g, X)
+    # node 0 in-neighbours: 1, 2, 3 (edge order) then itself
+    np.testing.assert_array_equal(out[0], [3.0, 7.0])
+    np.testing.assert_array_equal(argx[0], [1, 3])
+    np.testing.assert_array_equal(out[3], [1.0, 7.0])
+    np.testing.assert_array_equal(argx[3], [0, 3])
+
+
+def test_ties_first_in_edge_order_wins(oracle_mod):
+    # all-zero messages: argmax = first in-edge (edge order), not the self-loop
+    src = [3, 1, 2]
+    dst = [0, 0, 0]
+    g = oracle_mod.OracleGraph(src, dst, 4)
+    out, argx, _ = oracle_mod.spmm_max(g, np.zeros((4, 3), np.float32))
+    np.testing.assert_array_equal(out[0], 0.0)
+    np.testing.assert_array_equal(argx[0], [3, 3, 3])
+    # exact positive tie between nodes 1 and 2 -> node 1 (edge id 1 before 2)
+    X = np.zeros((4, 1), np.float32)
+    X[1] = X[2] = 4.0
+    out, argx, _ = oracle_mod.spmm_max(g, X)
+    assert out[0, 0] == 4.0 and argx[0, 0] == 1
+
+
+def test_duplicate_self_loop_and_backward_accumulates(oracle_mod):
+    # explicit self-loop 0->0 (PPI_inter diagonal) + DGL's appended loop: two entries
+    src = [0, 1, 1]
+    dst = [0, 0, 2]
+    g = oracle_mod.OracleGraph(src, dst, 3)
+    X = np.array([[2.0], [1.0], [0.0]], np.float32)
+    out, argx, arge = oracle_mod.spmm_max(g, X)
+    assert out[0, 0] == 2.0 and argx[0, 0] == 0 and arge[0, 0] == 0  # first of the two loops
+    # node 1 is the argmax of nodes 1 and 2: its gradient accumulates both
+    dZ = np.array([[1.0], [10.0], [100.0]], np.float32)
+    dX = oracle_mod.spmm_max_bwd(g, argx, arge, dZ)
+    np.testing.assert_array_equal(dX[:, 0], [1.0, 110.0, 0.0])
+
+
+def test_inf_masked_to_zero_and_zero_in_degree(oracle_mod):
+    g = oracle_mod.OracleGraph([0], [1], 3, self_loop=False)
+    X = np.array([[-np.inf], [1.0], [2.0]], np.float32)
+    out, _, _ = oracle_mod.spmm_max(g, X)
+    assert out[1, 0] == 0.0  # max = -inf -> 0 (replace_inf_with_zero)
+    assert out[0, 0] == 0.0 and out[2, 0] == 0.0  # no in-edges -> 0
+
+
+def test_weighted_max_and_sum_mean(oracle_mod):
+    src = [1, 2, 3]
+    dst = [0, 0, 0]
+    w = np.array([2.0, -1.0, 0.5], np.float32)
+    g = oracle_mod.OracleGraph(src, dst, 4, edge_weight=w)
+    X = np.array([[0.0], [1.0], [-3.0], [8.0]], np.float32)
+    out, argx, _ = oracle_mod.spmm_max(g, X, use_weight=True)
+    assert out[0, 0] == 4.0 and argx[0, 0] == 3  # max(2, 3, 4, 0 (self, w=1))
+    s = oracle_mod.spmm_sum(g, X, use_weight=True)
+    assert s[0, 0] == 2.0 + 3.0 + 4.0 + 0.0
+    m = oracle_mod.spmm_sum(g, X, mean=True)
+    assert m[0, 0] == pytest.approx((1.0 - 3.0 + 8.0 + 0.0) / 4)
+
+
+def test_multi_loss_matches_reference_golden(oracle_mod):
+    d = np.load(os.path.join(GOLD, "multi_loss.npz"))
+    w = oracle_mod.weight_cal(d["loc"])
+    np.testing.assert_array_equal(w, d["weight"])
+    inp = torch.tensor(d["probs"], requires_grad=True)
+    loss = oracle_mod.multi_loss(inp, torch.tensor(d["target"]), w)
+    loss.backward()
+    assert loss.item() == d["loss"]
+    np.testing.assert_array_equal(inp.grad.numpy(), d["grad"])
+
+
+def test_adam_torch110_matches_torch_adam(oracle_mod):
+    torch.manual_seed(0)
+    p0 = torch.randn(1000)
+    p_ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([p_ref], lr=5e-3)
+    p = p0.clone()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    for step in range(1, 6):
+        g = torch.randn(1000)
+        p_ref.grad = g.clone()
+        opt.step()
+        oracle_mod.adam_step_torch110([p], [g], [m], [v], step, 5e-3)
+    torch.testing.assert_close(p, p_ref.detach(), rtol=1e-6, atol=1e-7)
+
+
+def test_ecc_golden_present():
+    d = np.load(os.path.join(GOLD, "ecc.npz"))
+    e = d["tri_ecc"]
+    assert e[0, 1] == 1.0 and e[1, 2] == 1.0 and e[0, 3] == 0.0
