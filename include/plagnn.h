@@ -80,7 +80,8 @@ typedef void* pg_stream_t; /* hipStream_t */
  * For the in-CSR (DGL's CSC): rows = destination nodes, col = source node ids,
  * entries of a row in ascending edge id (the order DGL reduces them in).
  * For its transpose (out-CSR): rows = source nodes, col = destination ids in
- * ascending order, eslot = the in-CSR slot j of the same edge.
+ * ascending order, eslot = the in-CSR slot j of the same edge, epos = j - ptr_in[col]
+ * (the edge's position inside its in-CSR row, which is what argmax records hold).
  * Work schedule (built by pg_schedule_build): items {row, k0, k1, slot} cover every
  * row; a row longer than `chunk` entries is split into several items that write
  * partial results to `slot`; merges {row, first_slot, n_slots, 0} combine them.
@@ -92,6 +93,7 @@ typedef struct pg_csr {
   const int32_t* ptr;    /* [n_rows + 1] */
   const int32_t* col;    /* [nnz] */
   const int32_t* eslot;  /* [nnz] or NULL (NULL: slot == k) */
+  const int32_t* epos;   /* [nnz] transposed CSR only: position inside the in-CSR row */
   const float* ew;       /* edge weights indexed by in-CSR slot, or NULL */
   const int32_t* items;  /* [4 * n_items] */
   int64_t n_items;
@@ -110,9 +112,9 @@ int pg_csr_from_coo(const int64_t* src, const int64_t* dst, int64_t nnz, int64_t
                     int64_t n_dst, int32_t* ptr, int32_t* col, int32_t* eid);
 
 /* Transpose: tptr[n_cols+1], tcol[nnz] = row ids ascending, tslot[nnz] = slot in the
- * input CSR. */
+ * input CSR, tpos[nnz] = tslot - ptr[tcol] (may be NULL). */
 int pg_csr_transpose(const int32_t* ptr, const int32_t* col, int64_t n_rows, int64_t n_cols,
-                     int64_t nnz, int32_t* tptr, int32_t* tcol, int32_t* tslot);
+                     int64_t nnz, int32_t* tptr, int32_t* tcol, int32_t* tslot, int32_t* tpos);
 
 /* Work schedule sizes for rows of `ptr` split at `chunk` entries. */
 int pg_schedule_count(const int32_t* ptr, int64_t n_rows, int32_t chunk, int64_t* n_items,
@@ -133,7 +135,7 @@ int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, f
                     int64_t ldo, void* argpos, int64_t lda, int arg_kind, void* ws,
                     size_t ws_bytes, pg_stream_t stream);
 
-/* Deterministic backward (gather over the transposed CSR gt of g):
+/* Deterministic backward (gather over the transposed CSR gt of g; gt->epos required):
  *   dx[u,f] = sum_{(v,j) in gt row u, ascending v} [argpos[v,f] == j - g.ptr[v]] * ew[j] * dout[v,f]
  * then, if mask_src != NULL, dx[u,f] *= (mask_src[u,f] > 0)  (relu' of fc_pool).
  * Every dx element is written (no zero-fill needed). */

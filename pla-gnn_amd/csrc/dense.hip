@@ -66,9 +66,9 @@ __global__ __launch_bounds__(kBlock) void act_bwd_kernel(float* __restrict__ dy,
   }
 }
 
-// column sums, pass 1: block (cx, ry) sums rows ry, ry + R, ... of 64 columns into
-// part[ry][c] with a fixed order (4 row groups per block, combined in order)
-constexpr int kColRowChunks = 64;
+// column sums, pass 1: block (cx, ry) owns 64 columns x one chunk of rows; its 4 waves
+// take interleaved rows with 8 loads in flight per lane, then combine in wave order.
+constexpr int kColRowChunks = 128;
 __global__ __launch_bounds__(kBlock) void col_sum_part_kernel(const float* __restrict__ x,
                                                               int64_t ldx, int64_t rows,
                                                               int cols,
@@ -76,10 +76,21 @@ __global__ __launch_bounds__(kBlock) void col_sum_part_kernel(const float* __res
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
-  const int R = gridDim.y;
+  const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = (int64_t)blockIdx.y * per;
+  const int64_t r1 = min(rows, r0 + per);
   float s = 0.f;
-  if (c < cols)
-    for (int64_t r = (int64_t)blockIdx.y * 4 + g; r < rows; r += (int64_t)R * 4) s += x[r * ldx + c];
+  if (c < cols) {
+    int64_t r = r0 + g;
+    for (; r + 28 < r1; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = x[(r + 4 * e) * ldx + c];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[e];
+    }
+    for (; r < r1; r += 4) s += x[r * ldx + c];
+  }
   red[g][threadIdx.x & 63] = s;
   __syncthreads();
   if (g == 0 && c < cols) {
@@ -95,7 +106,13 @@ __global__ __launch_bounds__(kBlock) void col_sum_final_kernel(const float* __re
   const int c = blockIdx.x * kBlock + threadIdx.x;
   if (c >= cols) return;
   float s = 0.f;
-  for (int r = 0; r < R; ++r) s += part[(int64_t)r * cols + c];
+  for (int r = 0; r < R; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = r + e < R ? part[(int64_t)(r + e) * cols + c] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[e];
+  }
   out[c] = accumulate ? out[c] + s : s;
 }
 
@@ -116,26 +133,23 @@ __global__ __launch_bounds__(kBlock) void sigmoid_zero_kernel(const float* __res
   }
 }
 
-// pass 2: one thread per (indexed row, class): loss term into part, gradient into dz.
+// pass 2: block b owns indexed rows [b*R, b*R+R); one thread per (row, class) pair writes
+// the pair's loss term into LDS and its gradient into dz; then thread c < C sums its
+// class over the block's rows in row order (deterministic), giving part[b][c].
 // Mirrors the autograd graph of code/train.py:103-104 operation by operation.
-constexpr int kLossRowsPerBlock = 256;
+constexpr int kLossRows = 64;  // rows per block; kLossRows * C <= 64 * 64 pairs
 __global__ __launch_bounds__(kBlock) void multi_loss_kernel(
     const float* __restrict__ z, int64_t ldz, int C, const float* __restrict__ labels,
     int64_t ldl, const float* __restrict__ cw, const int32_t* __restrict__ index, int64_t n_index,
     float* __restrict__ part, float* __restrict__ dz, int64_t lddz) {
-  // block b handles indexed rows [b*256, b*256+256); thread t handles class t % C of
-  // rows t / C, ... — keep it simple: loop over (row, class) pairs owned by the block
-  __shared__ float acc[kBlock];
-  const int64_t r0 = (int64_t)blockIdx.x * kLossRowsPerBlock;
-  const int64_t r1 = std::min<int64_t>(n_index, r0 + kLossRowsPerBlock);
+  __shared__ float terms[kLossRows * 64];
+  const int64_t r0 = (int64_t)blockIdx.x * kLossRows;
+  const int nr = (int)min<int64_t>(kLossRows, n_index - r0);
   const float inv_n = 1.0f / (float)n_index;
-  // per-class partial sums with fixed order: thread t sums pairs t, t+256, ...
-  float local[64];
-  for (int c = 0; c < C; ++c) local[c] = 0.f;
-  for (int64_t p = (r0 * C) + threadIdx.x; p < r1 * C; p += kBlock) {
-    const int64_t ri = p / C;
-    const int c = (int)(p - ri * C);
-    const int64_t r = index[ri];
+  for (int p = threadIdx.x; p < nr * C; p += kBlock) {
+    const int ri = p / C;
+    const int c = p - ri * C;
+    const int64_t r = index[r0 + ri];
     const float zz = z[r * ldz + c];
     const float pr = 1.f / (1.f + expf(-zz));
     const float t = labels[r * ldl + c];
@@ -145,8 +159,7 @@ __global__ __launch_bounds__(kBlock) void multi_loss_kernel(
     const float q = 1.f - pr;
     const float cq = fminf(fmaxf(q, 1e-9f), 10.f);
     const float la = logf(cp), lb = logf(cq);
-    const float term = ((t * la) * w + (1.f - t) * lb) / w1 * 2.f;
-    local[c] += term;
+    terms[p] = ((t * la) * w + (1.f - t) * lb) / w1 * 2.f;
     if (dz) {
       // d(-sum/n)/d term = -(1/n); then *2, /(w+1)
       float g = -inv_n;
@@ -162,28 +175,31 @@ __global__ __launch_bounds__(kBlock) void multi_loss_kernel(
       dz[r * lddz + c] = (dp * (1.f - pr)) * pr;  // sigmoid_backward(grad, out)
     }
   }
-  for (int c = 0; c < C; ++c) {
-    acc[threadIdx.x] = local[c];
-    __syncthreads();
-    for (int s = kBlock / 2; s > 0; s >>= 1) {
-      if ((int)threadIdx.x < s) acc[threadIdx.x] += acc[threadIdx.x + s];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) part[(int64_t)blockIdx.x * C + c] = acc[0];
-    __syncthreads();
+  __syncthreads();
+  if ((int)threadIdx.x < C) {
+    float s = 0.f;
+    for (int ri = 0; ri < nr; ++ri) s += terms[ri * C + threadIdx.x];
+    part[(int64_t)blockIdx.x * C + threadIdx.x] = s;
   }
 }
 
-__global__ void multi_loss_final_kernel(const float* __restrict__ part, int nb, int C,
-                                        int64_t n_index, float* __restrict__ loss) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  float total = 0.f;
-  for (int c = 0; c < C; ++c) {
+// pass 3: one wave; lane c sums class c over the blocks in order, lane 0 adds classes.
+__global__ __launch_bounds__(64) void multi_loss_final_kernel(const float* __restrict__ part,
+                                                              int nb, int C, int64_t n_index,
+                                                              float* __restrict__ loss) {
+  __shared__ float cls[64];
+  const int c = threadIdx.x;
+  if (c < C) {
     float s = 0.f;
     for (int b = 0; b < nb; ++b) s += part[(int64_t)b * C + c];
-    total += -s / (float)n_index;
+    cls[c] = -s / (float)n_index;
   }
-  loss[0] = total;
+  __syncthreads();
+  if (c == 0) {
+    float total = 0.f;
+    for (int k = 0; k < C; ++k) total += cls[k];
+    loss[0] = total;
+  }
 }
 
 // ---- Adam ---------------------------------------------------------------------------
@@ -272,15 +288,16 @@ int pg_col_sum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* o
   if (ws_bytes < pg_col_sum_workspace(rows, cols))
     return pg::set_error(PG_ERR_WORKSPACE, "pg_col_sum: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(col_sum_part_kernel, dim3((cols + 63) / 64, kColRowChunks), dim3(kBlock), 0,
+  const int R = (int)std::max<int64_t>(1, std::min<int64_t>(kColRowChunks, (rows + 63) / 64));
+  hipLaunchKernelGGL(col_sum_part_kernel, dim3((cols + 63) / 64, R), dim3(kBlock), 0,
                      st, x, ldx, rows, (int)cols, (float*)ws);
   hipLaunchKernelGGL(col_sum_final_kernel, dim3((cols + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
-                     (const float*)ws, kColRowChunks, (int)cols, out, accumulate);
+                     (const float*)ws, R, (int)cols, out, accumulate);
   return hip_status("pg_col_sum");
 }
 
 size_t pg_sigmoid_multi_loss_workspace(int64_t n_index, int32_t C) {
-  const int64_t nb = std::max<int64_t>(1, (n_index + kLossRowsPerBlock - 1) / kLossRowsPerBlock);
+  const int64_t nb = std::max<int64_t>(1, (n_index + kLossRows - 1) / kLossRows);
   return (size_t)(nb * std::max(C, 1) * 4 + 2 * 64 * 4);
 }
 
@@ -300,7 +317,7 @@ int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C
   if ((prob || dz) && n_rows > 0)
     hipLaunchKernelGGL(sigmoid_zero_kernel, dim3(grid_1d(n_rows * C)), dim3(kBlock), 0, st, z, ldz,
                        n_rows, (int)C, prob, ldp, dz, lddz);
-  const int nb = (int)std::max<int64_t>(1, (n_index + kLossRowsPerBlock - 1) / kLossRowsPerBlock);
+  const int nb = (int)std::max<int64_t>(1, (n_index + kLossRows - 1) / kLossRows);
   float* part = (float*)ws;
   if (n_index > 0) {
     hipLaunchKernelGGL(multi_loss_kernel, dim3(nb), dim3(kBlock), 0, st, z, ldz, (int)C, labels, ldl,

@@ -4,12 +4,20 @@
 // PLA-GNN step: SAGEConv's fc_pool / fc_self / fc_neigh (code/model.py:13-15) and
 // liner1 / liner2 (code/model.py:16-17), forward and backward.
 //
-// Tile: 128 x 64 per 256-thread workgroup, K step 16; each wave owns a 32 x 64 strip
-// (two 32x32 accumulators, 32 AGPR/VGPR). Global -> register prefetch of the next K
-// tile overlaps the MFMAs of the current one; LDS holds A as [k][m] and B as [k][n]
-// so every MFMA operand is one conflict-free ds_read_b32 per lane.
+// Tiling: BM x BN per 256-thread workgroup (BM, BN in {64, 128}), K step 32; the four
+// waves form a 2 x 2 grid, each owning (BM/2) x (BN/2) = TM x TN MFMA tiles of 32 x 32.
+// Global -> register prefetch of the next K tile overlaps the MFMAs of the current one.
+// LDS layout follows the global layout so every staging store is a ds_write_b128:
+//   A not transposed (A[m][k]) -> As[m][k] (k contiguous, row stride 36 floats: the
+//   16-lane groups of ds_read_b128 hit 16 distinct 4-bank slots since 9 is odd);
+//   A transposed (A[k][m])     -> As[k][m] (m contiguous, read by ds_read_b32);
+//   the same for B with n in place of m.
+// K is consumed in a permuted order: at MFMA step s a lane of half h supplies
+// k = 16 h + s (not 2 s + h) for A and B alike, so one lane's 16 k-values are contiguous
+// in a [row][k] image (four ds_read_b128). Each MFMA still pairs A and B at equal k, so
+// the product is exact f32 with a fixed (permuted) summation order.
 // MFMA 32x32x2 f32 operand map (cdna_hip_programming.md §3): lane l holds
-// A[i = l & 31][k = l >> 5] and B[k = l >> 5][j = l & 31]; the accumulator holds
+// A[i = l & 31][kk = l >> 5] and B[kk = l >> 5][j = l & 31]; the accumulator holds
 // C[row = (r & 3) + 8 (r >> 2) + 4 (l >> 5)][col = l & 31] in register r.
 // Long-K products (weight gradients, K = number of nodes) use split-K with partial
 // slabs summed in a fixed order (deterministic).
@@ -19,30 +27,11 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 64, BK = 16;
+constexpr int BK = 32;
 constexpr int kThreads = 256;
-constexpr int LDA_S = BM + 4;  // [k][m] rows padded: 2-way worst case on the transposing store
-constexpr int LDB_S = BN + 4;
+constexpr int KPAD = BK + 4;  // [row][k] image row stride (floats)
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
-
-template <bool VEC>
-__device__ __forceinline__ void ld4(const float* __restrict__ p, bool ok0, bool ok1, bool ok2,
-                                    bool ok3, float (&r)[4]) {
-  if constexpr (VEC) {
-    if (ok0) {
-      const float4 t = *reinterpret_cast<const float4*>(p);
-      r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
-    } else {
-      r[0] = r[1] = r[2] = r[3] = 0.f;
-    }
-  } else {
-    r[0] = ok0 ? p[0] : 0.f;
-    r[1] = ok1 ? p[1] : 0.f;
-    r[2] = ok2 ? p[2] : 0.f;
-    r[3] = ok3 ? p[3] : 0.f;
-  }
-}
 
 template <int ACT>
 __device__ __forceinline__ float epi_act(float x, float slope) {
@@ -51,110 +40,160 @@ __device__ __forceinline__ float epi_act(float x, float slope) {
   else return x;
 }
 
+// Load a ROWS x BK tile of a matrix stored [row][k] (k contiguous) or [k][row] (KMAJ),
+// rows [r0, r0+ROWS) x k [k0, k0+BK), zero outside [0,R) x [0,kz1). 4 floats per unit.
+template <int ROWS, bool KMAJ, bool VEC>
+struct TileLoader {
+  static constexpr int UNITS = ROWS * BK / 4;          // float4 units per tile
+  static constexpr int PER = UNITS / kThreads;         // per thread (1, 2 or 4)
+  float r[PER][4];
+
+  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int r0, int R,
+                                       int k0, int kz1, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = tid + i * kThreads;
+      int row, k;
+      if constexpr (!KMAJ) {  // [row][k]: 8 units per row
+        row = q >> 3;
+        k = (q & 7) << 2;
+      } else {  // [k][row]: ROWS/4 units per k
+        k = q / (ROWS / 4);
+        row = (q % (ROWS / 4)) << 2;
+      }
+      const int gr = r0 + row, gk = k0 + k;
+      if constexpr (!KMAJ) {
+        const float* p = P + (int64_t)gr * ld + gk;
+        const bool okr = gr < R;
+        if constexpr (VEC) {
+          if (okr && gk < kz1) {
+            const float4 t = *reinterpret_cast<const float4*>(p);
+            r[i][0] = t.x; r[i][1] = t.y; r[i][2] = t.z; r[i][3] = t.w;
+          } else {
+            r[i][0] = r[i][1] = r[i][2] = r[i][3] = 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[i][j] = (okr && gk + j < kz1) ? p[j] : 0.f;
+        }
+      } else {
+        const float* p = P + (int64_t)gk * ld + gr;
+        const bool okk = gk < kz1;
+        if constexpr (VEC) {
+          if (okk && gr < R) {
+            const float4 t = *reinterpret_cast<const float4*>(p);
+            r[i][0] = t.x; r[i][1] = t.y; r[i][2] = t.z; r[i][3] = t.w;
+          } else {
+            r[i][0] = r[i][1] = r[i][2] = r[i][3] = 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[i][j] = (okk && gr + j < R) ? p[j] : 0.f;
+        }
+      }
+    }
+  }
+
+  // store into the LDS image: [row][KPAD] (!KMAJ) or [k][ROWS + 4] (KMAJ)
+  __device__ __forceinline__ void store(float* __restrict__ S, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = tid + i * kThreads;
+      float* d;
+      if constexpr (!KMAJ) {
+        d = S + (q >> 3) * KPAD + ((q & 7) << 2);
+      } else {
+        d = S + (q / (ROWS / 4)) * (ROWS + 4) + ((q % (ROWS / 4)) << 2);
+      }
+      *reinterpret_cast<float4*>(d) = make_float4(r[i][0], r[i][1], r[i][2], r[i][3]);
+    }
+  }
+};
+
+template <int ROWS, bool KMAJ>
+constexpr int image_floats() {
+  return KMAJ ? BK * (ROWS + 4) : ROWS * KPAD;
+}
+
+// Fragment of 16 k-values for MFMA row/col `rc` of lane half h from an LDS image.
+template <int ROWS, bool KMAJ>
+__device__ __forceinline__ void read_frag(const float* __restrict__ S, int rc, int h,
+                                          float (&f)[16]) {
+  if constexpr (!KMAJ) {
+    const float4* p = reinterpret_cast<const float4*>(S + rc * KPAD + h * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 t = p[q];
+      f[4 * q + 0] = t.x; f[4 * q + 1] = t.y; f[4 * q + 2] = t.z; f[4 * q + 3] = t.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) f[s] = S[(h * 16 + s) * (ROWS + 4) + rc];
+  }
+}
+
 // TA: A stored K x M (use A^T). TB: B stored N x K (use B^T).
-// VA/VB: 16-byte vector loads legal for A/B (alignment + leading dim multiple of 4).
-template <bool TA, bool TB, bool VA, bool VB, int ACT, bool SPLIT>
+template <int BM, int BN, bool TA, bool TB, bool VA, bool VB, int ACT, bool SPLIT>
 __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
     int M, int N, int K, int k_per_split, float alpha, const float* __restrict__ A, int64_t lda,
     const float* __restrict__ B, int64_t ldb, float beta, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias, float slope, float* __restrict__ ws) {
-  __shared__ float As[BK][LDA_S];
-  __shared__ float Bs[BK][LDB_S];
+  constexpr bool AK = TA;    // A image k-major ([k][m]) when A is stored transposed
+  constexpr bool BKM = !TB;  // B image k-major ([k][n]) when B is stored K x N
+  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
+  __shared__ __attribute__((aligned(16))) float As[image_floats<BM, AK>()];
+  __shared__ __attribute__((aligned(16))) float Bs[image_floats<BN, BKM>()];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.y * BM;
   const int n0 = blockIdx.x * BN;
   const int kz0 = blockIdx.z * k_per_split;
   const int kz1 = min(K, kz0 + k_per_split);
+  const int h = lane >> 5;
+  const int l32 = lane & 31;
 
-  f32x16 acc0 = {0}, acc1 = {0};
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // per-thread global load coordinates ------------------------------------------------
-  // A tile: 128 (m) x 16 (k) = 512 float4 -> 2 per thread
-  // B tile: 64 (n) x 16 (k) = 256 float4 -> 1 per thread
-  float ra[2][4], rb[4];
-
-  auto load_a = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = tid + i * kThreads;
-      if constexpr (!TA) {  // A[m][k], float4 along k
-        const int m = m0 + (q >> 2), k = k0 + ((q & 3) << 2);
-        const bool okm = m < M;
-        const float* p = A + (int64_t)m * lda + k;
-        ld4<VA>(p, okm && k < kz1, okm && k + 1 < kz1, okm && k + 2 < kz1, okm && k + 3 < kz1, ra[i]);
-      } else {  // A[k][m], float4 along m
-        const int k = k0 + (q >> 5), m = m0 + ((q & 31) << 2);
-        const bool okk = k < kz1;
-        const float* p = A + (int64_t)k * lda + m;
-        ld4<VA>(p, okk && m < M, okk && m + 1 < M, okk && m + 2 < M, okk && m + 3 < M, ra[i]);
-      }
-    }
-  };
-  auto load_b = [&](int k0) {
-    if constexpr (TB) {  // B[n][k], float4 along k
-      const int n = n0 + (tid >> 2), k = k0 + ((tid & 3) << 2);
-      const bool okn = n < N;
-      const float* p = B + (int64_t)n * ldb + k;
-      ld4<VB>(p, okn && k < kz1, okn && k + 1 < kz1, okn && k + 2 < kz1, okn && k + 3 < kz1, rb);
-    } else {  // B[k][n], float4 along n
-      const int k = k0 + (tid >> 4), n = n0 + ((tid & 15) << 2);
-      const bool okk = k < kz1;
-      const float* p = B + (int64_t)k * ldb + n;
-      ld4<VB>(p, okk && n < N, okk && n + 1 < N, okk && n + 2 < N, okk && n + 3 < N, rb);
-    }
-  };
-  auto store_ab = [&]() {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = tid + i * kThreads;
-      if constexpr (!TA) {
-        const int m = q >> 2, k = (q & 3) << 2;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) As[k + j][m] = ra[i][j];
-      } else {
-        const int k = q >> 5, m = (q & 31) << 2;
-        *reinterpret_cast<float4*>(&As[k][m]) = make_float4(ra[i][0], ra[i][1], ra[i][2], ra[i][3]);
-      }
-    }
-    if constexpr (TB) {
-      const int n = tid >> 2, k = (tid & 3) << 2;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) Bs[k + j][n] = rb[j];
-    } else {
-      const int k = tid >> 4, n = (tid & 15) << 2;
-      *reinterpret_cast<float4*>(&Bs[k][n]) = make_float4(rb[0], rb[1], rb[2], rb[3]);
-    }
-  };
-
-  const int am = wave * 32 + (lane & 31);
-  const int kh = lane >> 5;
-  const int bn = lane & 31;
+  TileLoader<BM, AK, VA> la;
+  TileLoader<BN, BKM, VB> lb;
 
   if (kz0 < kz1) {
-    load_a(kz0);
-    load_b(kz0);
-    store_ab();
+    la.load(A, lda, m0, M, kz0, kz1, tid);
+    lb.load(B, ldb, n0, N, kz0, kz1, tid);
+    la.store(As, tid);
+    lb.store(Bs, tid);
     __syncthreads();
     for (int k0 = kz0; k0 < kz1; k0 += BK) {
       const bool more = k0 + BK < kz1;
       if (more) {
-        load_a(k0 + BK);
-        load_b(k0 + BK);
+        la.load(A, lda, m0, M, k0 + BK, kz1, tid);
+        lb.load(B, ldb, n0, N, k0 + BK, kz1, tid);
       }
+      float fa[TM][16], fb[TN][16];
 #pragma unroll
-      for (int kk = 0; kk < BK; kk += 2) {
-        const float a = As[kk + kh][am];
-        const float b0 = Bs[kk + kh][bn];
-        const float b1 = Bs[kk + kh][32 + bn];
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
-      }
+      for (int i = 0; i < TM; ++i) read_frag<BM, AK>(As, wm * (BM / 2) + i * 32 + l32, h, fa[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) read_frag<BN, BKM>(Bs, wn * (BN / 2) + j * 32 + l32, h, fb[j]);
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
       __syncthreads();
       if (more) {
-        store_ab();
+        la.store(As, tid);
+        lb.store(Bs, tid);
         __syncthreads();
       }
     }
@@ -162,22 +201,24 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
 
   // epilogue ----------------------------------------------------------------------------
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const f32x16& acc = t == 0 ? acc0 : acc1;
-    const int col = n0 + t * 32 + (lane & 31);
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * (BN / 2) + j * 32 + l32;
     if (col >= N) continue;
     const float bv = (!SPLIT && bias) ? bias[col] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row >= M) continue;
-      if constexpr (SPLIT) {
-        ws[((int64_t)blockIdx.z * M + row) * N + col] = acc[r];
-      } else {
-        float v = alpha * acc[r];
-        if (beta != 0.f) v = v + beta * C[(int64_t)row * ldc + col];
-        if (bias) v = v + bv;
-        C[(int64_t)row * ldc + col] = epi_act<ACT>(v, slope);
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= M) continue;
+        if constexpr (SPLIT) {
+          ws[((int64_t)blockIdx.z * M + row) * N + col] = acc[i][j][r];
+        } else {
+          float v = alpha * acc[i][j][r];
+          if (beta != 0.f) v = v + beta * C[(int64_t)row * ldc + col];
+          if (bias) v = v + bv;
+          C[(int64_t)row * ldc + col] = epi_act<ACT>(v, slope);
+        }
       }
     }
   }
@@ -202,27 +243,64 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <bool TA, bool TB, bool SPLIT>
-int launch_typed(bool va, bool vb, int act, dim3 grid, hipStream_t st, int M, int N, int K,
-                 int kps, float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
-                 float beta, float* C, int64_t ldc, const float* bias, float slope, float* ws) {
-#define PG_GEMM_LAUNCH(VA_, VB_, ACT_)                                                        \
-  hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, VA_, VB_, ACT_, SPLIT>), grid, dim3(kThreads), 0, \
-                     st, M, N, K, kps, alpha, A, lda, B, ldb, beta, C, ldc, bias, slope, ws)
-#define PG_GEMM_ACT(VA_, VB_)                                              \
-  switch (act) {                                                          \
-    case PG_ACT_NONE: PG_GEMM_LAUNCH(VA_, VB_, PG_ACT_NONE); break;         \
-    case PG_ACT_RELU: PG_GEMM_LAUNCH(VA_, VB_, PG_ACT_RELU); break;         \
-    case PG_ACT_LEAKY: PG_GEMM_LAUNCH(VA_, VB_, PG_ACT_LEAKY); break;       \
-    default: return PG_ERR_INVALID;                                       \
+struct Args {
+  int M, N, K, kps;
+  float alpha;
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float beta;
+  float* C;
+  int64_t ldc;
+  const float* bias;
+  float slope;
+  float* ws;
+};
+
+template <int BM, int BN, bool TA, bool TB, bool VA, bool VB, bool SPLIT>
+int launch_act(int act, dim3 grid, hipStream_t st, const Args& a) {
+#define PG_L(ACT_)                                                                          \
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, VA, VB, ACT_, SPLIT>), grid,            \
+                     dim3(kThreads), 0, st, a.M, a.N, a.K, a.kps, a.alpha, a.A, a.lda, a.B,   \
+                     a.ldb, a.beta, a.C, a.ldc, a.bias, a.slope, a.ws)
+  if (SPLIT) {
+    PG_L(PG_ACT_NONE);
+    return PG_OK;
   }
-  if (va && vb) { PG_GEMM_ACT(true, true) }
-  else if (va) { PG_GEMM_ACT(true, false) }
-  else if (vb) { PG_GEMM_ACT(false, true) }
-  else { PG_GEMM_ACT(false, false) }
-#undef PG_GEMM_ACT
-#undef PG_GEMM_LAUNCH
+  switch (act) {
+    case PG_ACT_NONE: PG_L(PG_ACT_NONE); break;
+    case PG_ACT_RELU: PG_L(PG_ACT_RELU); break;
+    case PG_ACT_LEAKY: PG_L(PG_ACT_LEAKY); break;
+    default: return PG_ERR_INVALID;
+  }
+#undef PG_L
   return PG_OK;
+}
+
+template <int BM, int BN, bool TA, bool TB, bool SPLIT>
+int launch_vec(bool va, bool vb, int act, dim3 grid, hipStream_t st, const Args& a) {
+  if (va && vb) return launch_act<BM, BN, TA, TB, true, true, SPLIT>(act, grid, st, a);
+  if (va) return launch_act<BM, BN, TA, TB, true, false, SPLIT>(act, grid, st, a);
+  if (vb) return launch_act<BM, BN, TA, TB, false, true, SPLIT>(act, grid, st, a);
+  return launch_act<BM, BN, TA, TB, false, false, SPLIT>(act, grid, st, a);
+}
+
+template <int BM, int BN, bool SPLIT>
+int launch_trans(bool ta, bool tb, bool va, bool vb, int act, dim3 grid, hipStream_t st,
+                 const Args& a) {
+  if (!ta && !tb) return launch_vec<BM, BN, false, false, SPLIT>(va, vb, act, grid, st, a);
+  if (!ta && tb) return launch_vec<BM, BN, false, true, SPLIT>(va, vb, act, grid, st, a);
+  if (ta && !tb) return launch_vec<BM, BN, true, false, SPLIT>(va, vb, act, grid, st, a);
+  return launch_vec<BM, BN, true, true, SPLIT>(va, vb, act, grid, st, a);
+}
+
+// Tile choice: BN = 64 for narrow outputs, else 128; BM = 128 only when that still gives
+// at least ~3 workgroups per CU (256 CUs), so skinny-N products keep the chip filled.
+inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
+  bn = N <= 64 ? 64 : 128;
+  const int64_t tiles128 = ((M + 127) / 128) * ((N + bn - 1) / bn) * split;
+  bm = tiles128 >= 3 * 256 ? 128 : 64;
 }
 
 }  // namespace
@@ -263,22 +341,27 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
     split_k = (int)((K + kps - 1) / kps);
     if (split_k < 1) split_k = 1;
   }
-  dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)split_k);
-  hipStream_t st = (hipStream_t)stream;
   const bool split = split_k > 1;
+  int bm, bn;
+  pick_tile(M, N, split_k, bm, bn);
+  dim3 grid((unsigned)((N + bn - 1) / bn), (unsigned)((M + bm - 1) / bm), (unsigned)split_k);
+  hipStream_t st = (hipStream_t)stream;
+  const Args a{(int)M, (int)N, (int)K, kps, alpha, A, lda, B, ldb, beta, C, ldc, bias, slope,
+               split ? (float*)ws : nullptr};
+  const bool ta = transa != 0, tb = transb != 0;
   int rc;
-#define PG_DISPATCH(TA_, TB_)                                                                  \
-  rc = split ? launch_typed<TA_, TB_, true>(va, vb, act, grid, st, (int)M, (int)N, (int)K, kps,   \
-                                            alpha, A, lda, B, ldb, beta, C, ldc, bias, slope,     \
-                                            (float*)ws)                                           \
-             : launch_typed<TA_, TB_, false>(va, vb, act, grid, st, (int)M, (int)N, (int)K, kps,  \
-                                             alpha, A, lda, B, ldb, beta, C, ldc, bias, slope,    \
-                                             nullptr);
-  if (!transa && !transb) { PG_DISPATCH(false, false) }
-  else if (!transa && transb) { PG_DISPATCH(false, true) }
-  else if (transa && !transb) { PG_DISPATCH(true, false) }
-  else { PG_DISPATCH(true, true) }
-#undef PG_DISPATCH
+  if (bm == 128 && bn == 128)
+    rc = split ? launch_trans<128, 128, true>(ta, tb, va, vb, act, grid, st, a)
+               : launch_trans<128, 128, false>(ta, tb, va, vb, act, grid, st, a);
+  else if (bm == 64 && bn == 128)
+    rc = split ? launch_trans<64, 128, true>(ta, tb, va, vb, act, grid, st, a)
+               : launch_trans<64, 128, false>(ta, tb, va, vb, act, grid, st, a);
+  else if (bm == 128)
+    rc = split ? launch_trans<128, 64, true>(ta, tb, va, vb, act, grid, st, a)
+               : launch_trans<128, 64, false>(ta, tb, va, vb, act, grid, st, a);
+  else
+    rc = split ? launch_trans<64, 64, true>(ta, tb, va, vb, act, grid, st, a)
+               : launch_trans<64, 64, false>(ta, tb, va, vb, act, grid, st, a);
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_f32: dispatch failed");
   if (split) {
     const int64_t n = M * N;

@@ -71,7 +71,7 @@ int pg_csr_from_coo(const int64_t* src, const int64_t* dst, int64_t nnz, int64_t
 }
 
 int pg_csr_transpose(const int32_t* ptr, const int32_t* col, int64_t n_rows, int64_t n_cols,
-                     int64_t nnz, int32_t* tptr, int32_t* tcol, int32_t* tslot) {
+                     int64_t nnz, int32_t* tptr, int32_t* tcol, int32_t* tslot, int32_t* tpos) {
   if (n_rows < 0 || n_cols < 0 || nnz < 0)
     return pg::set_error(PG_ERR_INVALID, "pg_csr_transpose: negative size");
   if (!ptr || !tptr || (nnz > 0 && (!col || !tcol)))
@@ -97,6 +97,7 @@ int pg_csr_transpose(const int32_t* ptr, const int32_t* col, int64_t n_rows, int
       const int32_t t = cursor[col[k]]++;
       tcol[t] = (int32_t)r;
       if (tslot) tslot[t] = k;
+      if (tpos) tpos[t] = k - ptr[r];
     }
   }
   return pg::ok();

@@ -29,7 +29,6 @@ constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kMaxNC = 4;       // vector path: F <= 4 * 256 per launch
 constexpr int kMaxNCScalar = 16; // scalar path: F <= 16 * 64 per launch
-constexpr int kUnroll = 4;       // edges in flight per wave
 
 template <typename A>
 __device__ __forceinline__ int arg_none();
@@ -106,6 +105,23 @@ __device__ __forceinline__ void store_arg(A* __restrict__ row, int f, int F, con
   }
 }
 
+// ---- edge windows ---------------------------------------------------------------------
+// A wave walks its item's entries in windows of 64: one coalesced vector load brings 64
+// column ids (and per-entry scalars) into a VGPR, and each edge's id is broadcast with
+// v_readlane (a uniform lane select), so no per-edge scalar-load round trip sits in front
+// of the row loads. Inside a window, U edges are in flight at once: all their row loads
+// are issued before any is consumed. The last batch of a window is padded by repeating
+// its last valid edge for the loads; its compute is skipped by a uniform branch.
+__device__ __forceinline__ int bcast(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ float bcastf(float v, int j) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
+}
+
+template <int W, int NC>
+struct EdgeU {
+  static constexpr int value = (NC * W <= 8) ? 8 : 4;
+};
+
 // ---- max forward ---------------------------------------------------------------------
 template <int W, int NC, bool HAS_W, typename A>
 __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
@@ -114,6 +130,7 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
     const int4* __restrict__ items, int n_items, const float* __restrict__ X, int64_t ldx, int F,
     float* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
     float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw) {
+  constexpr int U = EdgeU<W, NC>::value;
   const int it = blockIdx.x * kWavesPerBlock + wave_id_uniform();
   if (it >= n_items) return;
   const int4 item = items[it];
@@ -132,50 +149,40 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
       bpos[c][i] = arg_none<A>();
     }
 
-  int k = k0;
-  for (; k + kUnroll <= k1; k += kUnroll) {
-    float v[kUnroll][NC][W];
+  for (int kw = k0; kw < k1; kw += kWave) {
+    const int nw = min(kWave, k1 - kw);
+    const int kl = kw + min(lane, nw - 1);
+    const int idxv = col[kl];
+    float wv = 1.f;
+    if constexpr (HAS_W) wv = ew[eslot ? eslot[kl] : kl];
+    for (int j = 0; j < nw; j += U) {
+      const int nv = min(U, nw - j);
+      float v[U][NC][W];
 #pragma unroll
-    for (int e = 0; e < kUnroll; ++e) {
-      const float* xr = X + (int64_t)col[k + e] * ldx;
+      for (int e = 0; e < U; ++e) {
+        const float* xr = X + (int64_t)bcast(idxv, j + min(e, nv - 1)) * ldx;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[e][c], ninf);
-    }
+        for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[e][c], ninf);
+      }
 #pragma unroll
-    for (int e = 0; e < kUnroll; ++e) {
-      const int pos = k + e - rs;
-      float w = 1.f;
-      if constexpr (HAS_W) w = ew[eslot ? eslot[k + e] : k + e];
+      for (int e = 0; e < U; ++e) {
+        if (e < nv) {
+          const int pos = kw + j + e - rs;
+          float w = 1.f;
+          if constexpr (HAS_W) w = bcastf(wv, j + e);
 #pragma unroll
-      for (int c = 0; c < NC; ++c)
+          for (int c = 0; c < NC; ++c)
 #pragma unroll
-        for (int i = 0; i < W; ++i) {
-          const float m = HAS_W ? v[e][c][i] * w : v[e][c][i];
-          if (m > best[c][i]) {
-            best[c][i] = m;
-            bpos[c][i] = pos;
-          }
-        }
-    }
-  }
-  for (; k < k1; ++k) {
-    float v[NC][W];
-    const float* xr = X + (int64_t)col[k] * ldx;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[c], ninf);
-    const int pos = k - rs;
-    float w = 1.f;
-    if constexpr (HAS_W) w = ew[eslot ? eslot[k] : k];
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-      for (int i = 0; i < W; ++i) {
-        const float m = HAS_W ? v[c][i] * w : v[c][i];
-        if (m > best[c][i]) {
-          best[c][i] = m;
-          bpos[c][i] = pos;
+            for (int i = 0; i < W; ++i) {
+              const float m = HAS_W ? v[e][c][i] * w : v[e][c][i];
+              if (m > best[c][i]) {
+                best[c][i] = m;
+                bpos[c][i] = pos;
+              }
+            }
         }
       }
+    }
   }
 
   if (slot < 0) {
@@ -206,6 +213,7 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
 }
 
 // Combine the partial maxima of split rows in chunk order (earlier chunk wins ties).
+// One workgroup per split row, one thread per feature; slot loads batched.
 template <typename A>
 __global__ __launch_bounds__(kBlock) void max_merge_kernel(const int4* __restrict__ merges,
                                                            int n_merges, int F,
@@ -214,19 +222,21 @@ __global__ __launch_bounds__(kBlock) void max_merge_kernel(const int4* __restric
                                                            int64_t ldw, float* __restrict__ out,
                                                            int64_t ldo, A* __restrict__ arg,
                                                            int64_t lda) {
-  const int mi = blockIdx.x * kWavesPerBlock + wave_id_uniform();
-  if (mi >= n_merges) return;
-  const int4 m = merges[mi];
+  const int4 m = merges[blockIdx.x];
   const int row = m.x, s0 = m.y, ns = m.z;
-  for (int f = lane_id(); f < F; f += kWave) {
+  for (int f = threadIdx.x; f < F; f += kBlock) {
     float best = -std::numeric_limits<float>::infinity();
     int bp = arg_none<A>();
-    for (int s = s0; s < s0 + ns; ++s) {
-      const float v = ws_val[(int64_t)s * ldw + f];
-      if (v > best) {
-        best = v;
-        bp = (int)ws_arg[(int64_t)s * ldw + f];
-      }
+    for (int s = s0; s < s0 + ns; s += 8) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ws_val[(int64_t)min(s + e, s0 + ns - 1) * ldw + f];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (s + e < s0 + ns && v[e] > best) {
+          best = v[e];
+          bp = (int)ws_arg[(int64_t)(s + e) * ldw + f];
+        }
     }
     if (__builtin_isinf(best)) best = 0.f;
     out[(int64_t)row * ldo + f] = best;
@@ -235,14 +245,18 @@ __global__ __launch_bounds__(kBlock) void max_merge_kernel(const int4* __restric
 }
 
 // ---- max backward, deterministic gather over the transposed CSR ----------------------
+// Wave per source row u: for every out-edge (u -> v) at in-row position p (ascending v),
+// read v's argmax record; features whose winner is p take dout[v, f] (* w). The record
+// loads of U edges are issued together, then their dout loads together (lanes with no
+// match read row 0 at the same column instead of branching: a cache hit, no divergence).
 template <int W, int NC, bool HAS_W, typename A>
 __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
-    const int32_t* __restrict__ gptr, const float* __restrict__ ew,
-    const int32_t* __restrict__ tptr, const int32_t* __restrict__ tcol,
-    const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
-    const A* __restrict__ arg, int64_t lda, const float* __restrict__ dout, int64_t ldd, int F,
-    const float* __restrict__ mask, int64_t ldm, float* __restrict__ dx, int64_t ldx,
-    float* __restrict__ ws, int64_t ldw) {
+    const float* __restrict__ ew, const int32_t* __restrict__ tcol,
+    const int32_t* __restrict__ tslot, const int32_t* __restrict__ tpos,
+    const int4* __restrict__ items, int n_items, const A* __restrict__ arg, int64_t lda,
+    const float* __restrict__ dout, int64_t ldd, int F, const float* __restrict__ mask,
+    int64_t ldm, float* __restrict__ dx, int64_t ldx, float* __restrict__ ws, int64_t ldw) {
+  constexpr int U = EdgeU<W, NC>::value;
   const int it = blockIdx.x * kWavesPerBlock + wave_id_uniform();
   if (it >= n_items) return;
   const int4 item = items[it];
@@ -255,62 +269,48 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < W; ++i) acc[c][i] = 0.f;
 
-  int t = t0;
-  for (; t + kUnroll <= t1; t += kUnroll) {
-    int a[kUnroll][NC][W];
-    int pos[kUnroll];
-    int v[kUnroll];
-    float w[kUnroll];
+  for (int tw = t0; tw < t1; tw += kWave) {
+    const int nw = min(kWave, t1 - tw);
+    const int tl = tw + min(lane, nw - 1);
+    const int vv = tcol[tl];
+    const int pv = tpos[tl];
+    float wv = 1.f;
+    if constexpr (HAS_W) wv = ew[tslot[tl]];
+    for (int j = 0; j < nw; j += U) {
+      const int nv = min(U, nw - j);
+      int a[U][NC][W];
 #pragma unroll
-    for (int e = 0; e < kUnroll; ++e) {
-      v[e] = tcol[t + e];
-      const int j = tslot ? tslot[t + e] : t + e;
-      pos[e] = j - gptr[v[e]];
-      w[e] = HAS_W ? ew[j] : 1.f;
-      const A* ar = arg + (int64_t)v[e] * lda;
+      for (int e = 0; e < U; ++e) {
+        const A* ar = arg + (int64_t)bcast(vv, j + min(e, nv - 1)) * lda;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) load_arg<W, A>(ar, (c * kWave + lane) * W, F, a[e][c]);
-    }
+        for (int c = 0; c < NC; ++c) load_arg<W, A>(ar, (c * kWave + lane) * W, F, a[e][c]);
+      }
+      float d[U][NC][W];
 #pragma unroll
-    for (int e = 0; e < kUnroll; ++e) {
-      const float* dr = dout + (int64_t)v[e] * ldd;
+      for (int e = 0; e < U; ++e) {
+        const int je = j + min(e, nv - 1);
+        const int p = bcast(pv, je);
+        const float* dr = dout + (int64_t)bcast(vv, je) * ldd;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int f = (c * kWave + lane) * W;
-        bool any = false;
+        for (int c = 0; c < NC; ++c) {
+          bool any = false;
 #pragma unroll
-        for (int i = 0; i < W; ++i) any |= (a[e][c][i] == pos[e]);
-        if (any) {
-          float d[W];
-          load_tile<W>(dr, f, F, d, 0.f);
-#pragma unroll
-          for (int i = 0; i < W; ++i)
-            if (a[e][c][i] == pos[e]) acc[c][i] += HAS_W ? w[e] * d[i] : d[i];
+          for (int i = 0; i < W; ++i) any |= (a[e][c][i] == p);
+          load_tile<W>(any ? dr : dout, (c * kWave + lane) * W, F, d[e][c], 0.f);
         }
       }
-    }
-  }
-  for (; t < t1; ++t) {
-    const int vv = tcol[t];
-    const int j = tslot ? tslot[t] : t;
-    const int p = j - gptr[vv];
-    const float ww = HAS_W ? ew[j] : 1.f;
-    const A* ar = arg + (int64_t)vv * lda;
-    const float* dr = dout + (int64_t)vv * ldd;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int f = (c * kWave + lane) * W;
-      int a[W];
-      load_arg<W, A>(ar, f, F, a);
-      bool any = false;
+      for (int e = 0; e < U; ++e) {
+        if (e < nv) {
+          const int p = bcast(pv, j + e);
+          float w = 1.f;
+          if constexpr (HAS_W) w = bcastf(wv, j + e);
 #pragma unroll
-      for (int i = 0; i < W; ++i) any |= (a[i] == p);
-      if (any) {
-        float d[W];
-        load_tile<W>(dr, f, F, d, 0.f);
+          for (int c = 0; c < NC; ++c)
 #pragma unroll
-        for (int i = 0; i < W; ++i)
-          if (a[i] == p) acc[c][i] += HAS_W ? ww * d[i] : d[i];
+            for (int i = 0; i < W; ++i)
+              if (a[e][c][i] == p) acc[c][i] += HAS_W ? w * d[e][c][i] : d[e][c][i];
+        }
       }
     }
   }
@@ -337,18 +337,24 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
 }
 
 // Sum partial slots in order; optional relu' mask (bwd) or 1/deg (mean fwd).
+// One workgroup per split row, one thread per feature.
 __global__ __launch_bounds__(kBlock) void sum_merge_kernel(
     const int4* __restrict__ merges, int n_merges, int F, const float* __restrict__ ws,
     int64_t ldw, const int32_t* __restrict__ ptr, int divide_by_deg,
     const float* __restrict__ mask, int64_t ldm, float* __restrict__ out, int64_t ldo) {
-  const int mi = blockIdx.x * kWavesPerBlock + wave_id_uniform();
-  if (mi >= n_merges) return;
-  const int4 m = merges[mi];
+  const int4 m = merges[blockIdx.x];
   const int row = m.x, s0 = m.y, ns = m.z;
   const float deg = divide_by_deg ? (float)(ptr[row + 1] - ptr[row]) : 1.f;
-  for (int f = lane_id(); f < F; f += kWave) {
+  for (int f = threadIdx.x; f < F; f += kBlock) {
     float acc = 0.f;
-    for (int s = s0; s < s0 + ns; ++s) acc += ws[(int64_t)s * ldw + f];
+    for (int s = s0; s < s0 + ns; s += 8) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ws[(int64_t)min(s + e, s0 + ns - 1) * ldw + f];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (s + e < s0 + ns) acc += v[e];
+    }
     if (divide_by_deg) acc = acc / deg;
     if (mask && !(mask[(int64_t)row * ldm + f] > 0.f)) acc = 0.f;
     out[(int64_t)row * ldo + f] = acc;
@@ -363,6 +369,7 @@ __global__ __launch_bounds__(kBlock) void sum_kernel(
     const int32_t* __restrict__ norm_ptr, const int4* __restrict__ items, int n_items,
     const float* __restrict__ X, int64_t ldx, int F, float* __restrict__ out, int64_t ldo,
     float* __restrict__ ws, int64_t ldw) {
+  constexpr int U = EdgeU<W, NC>::value;
   const int it = blockIdx.x * kWavesPerBlock + wave_id_uniform();
   if (it >= n_items) return;
   const int4 item = items[it];
@@ -374,52 +381,39 @@ __global__ __launch_bounds__(kBlock) void sum_kernel(
 #pragma unroll
     for (int i = 0; i < W; ++i) acc[c][i] = 0.f;
 
-  int k = k0;
-  for (; k + kUnroll <= k1; k += kUnroll) {
-    float v[kUnroll][NC][W];
+  for (int kw = k0; kw < k1; kw += kWave) {
+    const int nw = min(kWave, k1 - kw);
+    const int kl = kw + min(lane, nw - 1);
+    const int idxv = col[kl];
+    float wv = 1.f, dv = 1.f;
+    if constexpr (HAS_W) wv = ew[eslot ? eslot[kl] : kl];
+    if constexpr (NORM == 2) dv = (float)(norm_ptr[idxv + 1] - norm_ptr[idxv]);
+    for (int j = 0; j < nw; j += U) {
+      const int nv = min(U, nw - j);
+      float v[U][NC][W];
 #pragma unroll
-    for (int e = 0; e < kUnroll; ++e) {
-      const float* xr = X + (int64_t)col[k + e] * ldx;
+      for (int e = 0; e < U; ++e) {
+        const float* xr = X + (int64_t)bcast(idxv, j + min(e, nv - 1)) * ldx;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[e][c], 0.f);
-    }
-#pragma unroll
-    for (int e = 0; e < kUnroll; ++e) {
-      float w = 1.f, dc = 1.f;
-      if constexpr (HAS_W) w = ew[eslot ? eslot[k + e] : k + e];
-      if constexpr (NORM == 2) {
-        const int cc = col[k + e];
-        dc = (float)(norm_ptr[cc + 1] - norm_ptr[cc]);
+        for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[e][c], 0.f);
       }
 #pragma unroll
-      for (int c = 0; c < NC; ++c)
+      for (int e = 0; e < U; ++e) {
+        if (e < nv) {
+          float w = 1.f, dc = 1.f;
+          if constexpr (HAS_W) w = bcastf(wv, j + e);
+          if constexpr (NORM == 2) dc = bcastf(dv, j + e);
 #pragma unroll
-        for (int i = 0; i < W; ++i) {
-          float tv = HAS_W ? v[e][c][i] * w : v[e][c][i];
-          if constexpr (NORM == 2) tv = tv / dc;
-          acc[c][i] += tv;
+          for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int i = 0; i < W; ++i) {
+              float tv = HAS_W ? v[e][c][i] * w : v[e][c][i];
+              if constexpr (NORM == 2) tv = tv / dc;
+              acc[c][i] += tv;
+            }
         }
-    }
-  }
-  for (; k < k1; ++k) {
-    float v[NC][W];
-    const float* xr = X + (int64_t)col[k] * ldx;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[c], 0.f);
-    float w = 1.f, dc = 1.f;
-    if constexpr (HAS_W) w = ew[eslot ? eslot[k] : k];
-    if constexpr (NORM == 2) {
-      const int cc = col[k];
-      dc = (float)(norm_ptr[cc + 1] - norm_ptr[cc]);
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-      for (int i = 0; i < W; ++i) {
-        float tv = HAS_W ? v[c][i] * w : v[c][i];
-        if constexpr (NORM == 2) tv = tv / dc;
-        acc[c][i] += tv;
       }
+    }
   }
   if (slot < 0) {
     if constexpr (NORM == 1) {
@@ -594,7 +588,7 @@ int launch_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, fl
     }
     if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_max_fwd: unsupported feature tile");
     if (g->n_merges > 0) {
-      hipLaunchKernelGGL((max_merge_kernel<A>), dim3(grid_for(g->n_merges)), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL((max_merge_kernel<A>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
                          (const int4*)g->merges, (int)g->n_merges, Ft, ws_val + f0, ws_arg + f0,
                          ldw, out + f0, ldo, arg + f0, lda);
     }
@@ -618,7 +612,7 @@ int launch_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const A* arg, int64_t 
       constexpr int W = decltype(w_c)::value;
       constexpr bool HW = decltype(hw_c)::value;
       hipLaunchKernelGGL((max_bwd_kernel<W, NC, HW, A>), dim3(blocks), dim3(kBlock), 0, st,
-                         g->ptr, g->ew, gt->ptr, gt->col, gt->eslot, (const int4*)gt->items,
+                         g->ew, gt->col, gt->eslot, gt->epos, (const int4*)gt->items,
                          (int)gt->n_items, arg + f0, lda, dout + f0, ldd, Ft,
                          mask ? mask + f0 : nullptr, ldm, dx + f0, ldx, ws ? ws + f0 : nullptr,
                          ldw);
@@ -636,7 +630,7 @@ int launch_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const A* arg, int64_t 
     }
     if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_max_bwd: unsupported feature tile");
     if (gt->n_merges > 0) {
-      hipLaunchKernelGGL(sum_merge_kernel, dim3(grid_for(gt->n_merges)), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL(sum_merge_kernel, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
                          (const int4*)gt->merges, (int)gt->n_merges, Ft, ws + f0, ldw, gt->ptr, 0,
                          mask ? mask + f0 : nullptr, ldm, dx + f0, ldx);
     }
@@ -703,6 +697,8 @@ int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, i
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: bad arg_kind %d", arg_kind);
   if (gt->n_cols != g->n_rows || gt->nnz != g->nnz)
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: gt is not the transpose of g");
+  if (gt->nnz > 0 && (!gt->epos || (g->ew && !gt->eslot)))
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: gt needs epos (and eslot when weighted)");
   if (F < 0 || ldd < F || ldx < F || lda < F || (mask_src && ldm < F))
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: bad F/leading dims");
   if (F == 0 || gt->n_rows == 0) return pg::ok();
@@ -813,7 +809,7 @@ int pg_spmm_sum(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, int n
     }
     if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_sum: unsupported feature tile");
     if (g->n_merges > 0)
-      hipLaunchKernelGGL(sum_merge_kernel, dim3(grid_for(g->n_merges)), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL(sum_merge_kernel, dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
                          (const int4*)g->merges, (int)g->n_merges, Ft, w + f0, ldw, g->ptr,
                          norm_mode == 1 ? 1 : 0, nullptr, 0, out + f0, ldo);
   }

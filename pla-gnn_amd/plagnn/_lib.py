@@ -31,6 +31,7 @@ class PgCsr(ctypes.Structure):
         ("ptr", ctypes.c_void_p),
         ("col", ctypes.c_void_p),
         ("eslot", ctypes.c_void_p),
+        ("epos", ctypes.c_void_p),
         ("ew", ctypes.c_void_p),
         ("items", ctypes.c_void_p),
         ("n_items", ctypes.c_int64),
@@ -54,7 +55,7 @@ _csr = ctypes.POINTER(PgCsr)
 # name -> (restype, argtypes); every symbol of include/plagnn.h
 SIGNATURES = {
     "pg_csr_from_coo": (_i, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp]),
-    "pg_csr_transpose": (_i, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp]),
+    "pg_csr_transpose": (_i, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "pg_schedule_count": (_i, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
     "pg_schedule_build": (_i, [_vp, _i64, _i32, _vp, _vp]),
     "pg_spmm_max_fwd_workspace": (_sz, [_csr, _i64, _i]),

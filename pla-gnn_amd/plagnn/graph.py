@@ -45,8 +45,8 @@ def _schedule(ptr: np.ndarray, chunk: int):
 class HostCsr:
     """One CSR direction with its schedule, in host memory (numpy int32)."""
 
-    def __init__(self, ptr, col, eslot, n_cols: int, chunk: int):
-        self.ptr, self.col, self.eslot = ptr, col, eslot
+    def __init__(self, ptr, col, eslot, n_cols: int, chunk: int, epos=None):
+        self.ptr, self.col, self.eslot, self.epos = ptr, col, eslot, epos
         self.n_rows = len(ptr) - 1
         self.n_cols = int(n_cols)
         self.nnz = int(len(col))
@@ -63,7 +63,7 @@ class DeviceCsr:
             return None if a is None else torch.from_numpy(a).to(device)
 
         self.device = device
-        self.ptr, self.col, self.eslot = up(h.ptr), up(h.col), up(h.eslot)
+        self.ptr, self.col, self.eslot, self.epos = up(h.ptr), up(h.col), up(h.eslot), up(h.epos)
         self.items, self.merges = up(h.items), up(h.merges)
         self.n_rows, self.n_cols, self.nnz = h.n_rows, h.n_cols, h.nnz
         self.n_items, self.n_merges, self.n_slots = h.n_items, h.n_merges, h.n_slots
@@ -75,6 +75,7 @@ class DeviceCsr:
         s.ptr = _lib.ptr(self.ptr)
         s.col = _lib.ptr(self.col)
         s.eslot = _lib.ptr(self.eslot)
+        s.epos = _lib.ptr(self.epos)
         s.ew = _lib.ptr(ew)
         s.items = _lib.ptr(self.items)
         s.n_items = self.n_items
@@ -105,13 +106,14 @@ class CSRGraph:
         tptr = np.zeros(n + 1, np.int32)
         tcol = np.zeros(max(E, 1), np.int32)
         tslot = np.zeros(max(E, 1), np.int32)
+        tpos = np.zeros(max(E, 1), np.int32)
         call("pg_csr_transpose", _np_ptr(ptr), _np_ptr(col), n, n, E, _np_ptr(tptr), _np_ptr(tcol),
-             _np_ptr(tslot))
+             _np_ptr(tslot), _np_ptr(tpos))
         self.num_nodes = n
         self.num_edges = E
         self.eid = eid  # in-CSR slot -> edge id
         self.fwd = HostCsr(ptr, col, None, n, chunk)
-        self.bwd = HostCsr(tptr, tcol[:E], tslot[:E], n, chunk)
+        self.bwd = HostCsr(tptr, tcol[:E], tslot[:E], n, chunk, epos=tpos[:E])
         # argmax records hold positions inside in-CSR rows: u16 while every row is shorter
         # than 0xFFFF entries (0xFFFF = no winner)
         self.arg_kind = _lib.PG_ARG_U16 if self.fwd.max_deg < 0xFFFF else _lib.PG_ARG_I32

@@ -148,10 +148,12 @@ def argpos_to_src(dg: DeviceGraph, argpos: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------ dense
 def _split_k(M: int, N: int, K: int) -> int:
-    tiles = ((M + 127) // 128) * ((N + 63) // 64)
+    """K-split for long-K products (weight gradients): aim at ~512 workgroups of the
+    64 x 128 tile, each keeping >= 512 rows of K."""
+    tiles = ((M + 63) // 64) * ((N + 127) // 128)
     if K < 2048 or tiles >= 512:
         return 1
-    return int(max(1, min(64, 1024 // max(tiles, 1), K // 512)))
+    return int(max(1, min(32, -(-512 // tiles), K // 512)))
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = False,

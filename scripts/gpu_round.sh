@@ -10,6 +10,11 @@ timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -x ${PYTES
 rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -ge 2 ]; then echo "pytest crashed/timed out; stopping"; exit $rc; fi
+if [ "${GEMM_BENCH:-0}" = "1" ]; then
+  timeout -k 10 300 python scripts/gemm_bench.py > gpurun_out/gemm_bench.txt 2>&1
+  rcg=$?; echo "gemm_bench rc=$rcg"; cat gpurun_out/gemm_bench.txt | tail -25
+  if [ $rcg -ne 0 ]; then exit $rcg; fi
+fi
 if [ "${SKIP_BENCH:-0}" = "1" ]; then exit $rc; fi
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 5 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc2=$?

@@ -145,4 +145,5 @@ def test_full_size_s0_properties():
     dX = ops.spmm_max_backward(dg, argpos, dZ)
     torch.testing.assert_close(dX.double().sum(0), dZ.double().sum(0), rtol=1e-5, atol=1e-2)
     dXs = ops.spmm_max_backward_scatter(dg, argpos, dZ)
-    torch.testing.assert_close(dX, dXs, rtol=1e-5, atol=1e-5)
+    # atomics sum hub rows in arrival order: fp32 reassociation only
+    torch.testing.assert_close(dX, dXs, rtol=1e-4, atol=1e-4)
