@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <limits>
 
 #include "common.hpp"
@@ -336,6 +338,221 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
   }
 }
 
+// ---- max backward, grouped form (default for u16 records and F <= 1024) ---------------
+// Pass 1, one workgroup per destination row v: counting-sort v's features by their
+// winning in-row position p (LDS histogram + block scan; a bitonic sort of the keys
+// (p << 16 | f) for rows longer than kHistMax), giving
+//   gpos[ptr[v] + v + p] = start of p's feature list (p = 0..deg; the last = #winners),
+//   gfeat[v][i]          = the features in p order,
+//   dpack[v][i]          = dout[v][gfeat[v][i]]  (the upstream gradient in list order).
+// Pass 2, one wave per source row u: for each out-edge (u -> v) at position p, ascending
+// v, add dpack[v][gpos..gpos'] (* w) into an LDS row accumulator at gfeat[v][...]. A
+// list never repeats a feature, so one instruction's lanes hit distinct LDS words and
+// the per-feature summation order is ascending v, exactly as the sequential
+// scatter_add_. Traffic per edge is two short contiguous runs (~F/deg entries) instead
+// of v's whole argmax row.
+constexpr int kHistMax = 4096;
+constexpr int kGroupMaxF = 1024;
+
+__device__ int block_exclusive_scan(int* s, int n, int* wsum) {
+  const int per = (n + kBlock - 1) / kBlock;
+  const int b = threadIdx.x * per;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  int local = 0;
+  for (int i = 0; i < per; ++i)
+    if (b + i < n) local += s[b + i];
+  int x = local;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == kWave - 1) wsum[wave] = x;
+  __syncthreads();
+  int pre = 0;
+  for (int w = 0; w < wave; ++w) pre += wsum[w];
+  int run = pre + x - local;
+  for (int i = 0; i < per; ++i)
+    if (b + i < n) {
+      const int t = s[b + i];
+      s[b + i] = run;
+      run += t;
+    }
+  const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return total;
+}
+
+template <typename A>
+__global__ __launch_bounds__(kBlock) void group_pack_kernel(
+    const int32_t* __restrict__ ptr, const A* __restrict__ arg, int64_t lda, int F,
+    const float* __restrict__ dout, int64_t ldd, uint16_t* __restrict__ gfeat,
+    uint16_t* __restrict__ gpos, float* __restrict__ dpack) {
+  __shared__ int hist[kHistMax + 8];
+  __shared__ uint16_t feats[kGroupMaxF];
+  __shared__ int wsum[4];
+  const int v = blockIdx.x;
+  const int rs = ptr[v];
+  const int deg = ptr[v + 1] - rs;
+  uint16_t* gp = gpos + rs + v;  // deg + 1 entries
+  const A* ar = arg + (int64_t)v * lda;
+  int total;
+  if (deg <= kHistMax) {
+    for (int p = threadIdx.x; p < deg; p += kBlock) hist[p] = 0;
+    __syncthreads();
+    for (int f = threadIdx.x; f < F; f += kBlock) {
+      const int a = (int)ar[f];
+      if (a != arg_none<A>()) atomicAdd(&hist[a], 1);
+    }
+    __syncthreads();
+    total = block_exclusive_scan(hist, deg, wsum);
+    for (int p = threadIdx.x; p < deg; p += kBlock) gp[p] = (uint16_t)hist[p];
+    if (threadIdx.x == 0) gp[deg] = (uint16_t)total;
+    __syncthreads();
+    for (int f = threadIdx.x; f < F; f += kBlock) {
+      const int a = (int)ar[f];
+      if (a != arg_none<A>()) feats[atomicAdd(&hist[a], 1)] = (uint16_t)f;
+    }
+    __syncthreads();
+  } else {
+    // hub row: bitonic sort of (p << 16 | f) keys; "none" sorts last
+    uint32_t* keys = reinterpret_cast<uint32_t*>(hist);
+    int np = 1;
+    while (np < F) np <<= 1;
+    for (int i = threadIdx.x; i < np; i += kBlock) {
+      uint32_t key = 0xFFFFFFFFu;
+      if (i < F) {
+        const int a = (int)ar[i];
+        if (a != arg_none<A>()) key = ((uint32_t)a << 16) | (uint32_t)i;
+      }
+      keys[i] = key;
+    }
+    __syncthreads();
+    for (int k = 2; k <= np; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < np; i += kBlock) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const uint32_t a = keys[i], b = keys[ixj];
+            if ((a > b) == ((i & k) == 0)) {
+              keys[i] = b;
+              keys[ixj] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    // count winners = first index whose key is 0xFFFFFFFF
+    for (int p = threadIdx.x; p <= deg; p += kBlock) {
+      const uint32_t key = (uint32_t)p << 16;
+      int lo = 0, hi = np;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < key) lo = mid + 1; else hi = mid;
+      }
+      gp[p] = (uint16_t)lo;
+    }
+    if (threadIdx.x == 0) {
+      int lo = 0, hi = np;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] != 0xFFFFFFFFu) lo = mid + 1; else hi = mid;
+      }
+      wsum[0] = lo;
+    }
+    __syncthreads();
+    total = wsum[0];
+    gp[deg] = (uint16_t)total;  // (all threads write the same value)
+    for (int i = threadIdx.x; i < total; i += kBlock) feats[i] = (uint16_t)(keys[i] & 0xFFFFu);
+    __syncthreads();
+  }
+  const float* dr = dout + (int64_t)v * ldd;
+  for (int i = threadIdx.x; i < total; i += kBlock) {
+    const int f = feats[i];
+    gfeat[(int64_t)v * F + i] = (uint16_t)f;
+    dpack[(int64_t)v * F + i] = dr[f];
+  }
+}
+
+template <bool HAS_W>
+__global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
+    const float* __restrict__ ew, const int32_t* __restrict__ tcol,
+    const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
+    const uint16_t* __restrict__ gfeat, const uint16_t* __restrict__ gpos,
+    const float* __restrict__ dpack, int F, const float* __restrict__ mask, int64_t ldm,
+    float* __restrict__ dx, int64_t ldx, float* __restrict__ ws, int64_t ldw) {
+  constexpr int U = 8;
+  __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
+  const int wave = wave_id_uniform();
+  const int it = blockIdx.x * kWavesPerBlock + wave;
+  if (it >= n_items) return;
+  float* acc = accs[wave];
+  const int4 item = items[it];
+  const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
+  const int lane = lane_id();
+  for (int f = lane; f < F; f += kWave) acc[f] = 0.f;
+
+  for (int tw = t0; tw < t1; tw += kWave) {
+    const int nw = min(kWave, t1 - tw);
+    const int tl = tw + min(lane, nw - 1);
+    const int vv = tcol[tl];
+    const int jj = tslot[tl];
+    const int sv = gpos[jj + vv];
+    const int ev = gpos[jj + vv + 1];
+    float wv = 1.f;
+    if constexpr (HAS_W) wv = ew[jj];
+    for (int j = 0; j < nw; j += U) {
+      const int nv = min(U, nw - j);
+      int fe[U];
+      float de[U];
+#pragma unroll
+      for (int e = 0; e < U; ++e) {
+        const int je = j + min(e, nv - 1);
+        const int64_t base = (int64_t)bcast(vv, je) * F + bcast(sv, je);
+        const int n = bcast(ev, je) - bcast(sv, je);
+        const bool on = lane < n;
+        fe[e] = on ? (int)gfeat[base + lane] : 0;
+        de[e] = on ? dpack[base + lane] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < U; ++e) {
+        if (e < nv) {
+          const int je = j + e;
+          const int n = bcast(ev, je) - bcast(sv, je);
+          float w = 1.f;
+          if constexpr (HAS_W) w = bcastf(wv, je);
+          if (lane < n) acc[fe[e]] += HAS_W ? w * de[e] : de[e];
+          if (n > kWave) {  // long list (low in-degree v): remaining segments, in order
+            const int64_t base = (int64_t)bcast(vv, je) * F + bcast(sv, je);
+            for (int s = kWave; s < n; s += kWave) {
+              if (s + lane < n) {
+                const int f = gfeat[base + s + lane];
+                const float d = dpack[base + s + lane];
+                acc[f] += HAS_W ? w * d : d;
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (slot < 0) {
+    float* xr = dx + (int64_t)row * ldx;
+    const float* mr = mask ? mask + (int64_t)row * ldm : nullptr;
+    for (int f = lane; f < F; f += kWave) {
+      float a = acc[f];
+      if (mr && !(mr[f] > 0.f)) a = 0.f;
+      xr[f] = a;
+    }
+  } else {
+    float* wr = ws + (int64_t)slot * ldw;
+    for (int f = lane; f < F; f += kWave) wr[f] = acc[f];
+  }
+}
+
 // Sum partial slots in order; optional relu' mask (bwd) or 1/deg (mean fwd).
 // One workgroup per split row, one thread per feature.
 __global__ __launch_bounds__(kBlock) void sum_merge_kernel(
@@ -543,12 +760,25 @@ struct TilePlan {
   int64_t tile;
 };
 
+// Feature columns per launch on the vector path (tuning knob PLAGNN_SPMM_FTILE, a
+// multiple of 256 up to 1024): narrower tiles mean fewer registers per wave (higher
+// occupancy) at the price of re-reading the column ids once per tile.
+inline int64_t vec_ftile() {
+  static const int64_t t = [] {
+    const char* e = getenv("PLAGNN_SPMM_FTILE");
+    int64_t v = e ? atoll(e) : 1024;
+    if (v < 256 || v > kFTileVec || v % 256) v = kFTileVec;
+    return v;
+  }();
+  return t;
+}
+
 inline TilePlan plan_tiles(int64_t F, std::initializer_list<int64_t> lds,
                            std::initializer_list<const void*> ptrs) {
   bool vec = (F % 4) == 0;
   for (int64_t l : lds) vec = vec && (l % 4) == 0;
   for (const void* p : ptrs) vec = vec && (p == nullptr || aligned16(p));
-  return {vec, vec ? (int64_t)kFTileVec : (int64_t)kFTileScalar};
+  return {vec, vec ? vec_ftile() : (int64_t)kFTileScalar};
 }
 
 template <typename A>
@@ -682,9 +912,19 @@ int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, f
                                  (int32_t*)ws_arg, ldw, st);
 }
 
+// [split-row partials][grouped path: gfeat N x F u16 | gpos (nnz + N) u16 | dpack N x F f32]
+static size_t bwd_partials_bytes(const pg_csr_t* gt, int64_t F) {
+  return gt->n_slots > 0 ? round_up(gt->n_slots * ws_ld(F) * 4, 256) : 0;
+}
+
 size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
-  if (!gt || gt->n_slots <= 0 || F <= 0) return 0;
-  return round_up(gt->n_slots * ws_ld(F) * 4, 256);
+  if (!gt || F <= 0) return 0;
+  size_t b = bwd_partials_bytes(gt, F);
+  if (F <= kGroupMaxF) {
+    const int64_t N = gt->n_cols;
+    b += round_up(N * F * 2, 256) + round_up((gt->nnz + N) * 2, 256) + round_up(N * F * 4, 256);
+  }
+  return b;
 }
 
 int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
@@ -697,8 +937,8 @@ int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, i
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: bad arg_kind %d", arg_kind);
   if (gt->n_cols != g->n_rows || gt->nnz != g->nnz)
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: gt is not the transpose of g");
-  if (gt->nnz > 0 && (!gt->epos || (g->ew && !gt->eslot)))
-    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: gt needs epos (and eslot when weighted)");
+  if (gt->nnz > 0 && (!gt->epos || !gt->eslot))
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: gt needs eslot and epos");
   if (F < 0 || ldd < F || ldx < F || lda < F || (mask_src && ldm < F))
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: bad F/leading dims");
   if (F == 0 || gt->n_rows == 0) return pg::ok();
@@ -706,7 +946,37 @@ int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, i
   const size_t need = pg_spmm_max_bwd_workspace(gt, F);
   PG_TRY(check_ws(ws_bytes, need, "pg_spmm_max_bwd"));
   hipStream_t st = (hipStream_t)stream;
-  float* w = need ? (float*)ws : nullptr;
+  const size_t pbytes = bwd_partials_bytes(gt, F);
+  float* w = pbytes ? (float*)ws : nullptr;
+  static const bool force_direct = [] {
+    const char* e = getenv("PLAGNN_BWD_PATH");  // tuning knob: "direct" = argmax-row gather
+    return e && strcmp(e, "direct") == 0;
+  }();
+  if (arg_kind == PG_ARG_U16 && F <= kGroupMaxF && !force_direct) {
+    const int64_t N = g->n_rows;
+    char* p = (char*)ws + pbytes;
+    uint16_t* gfeat = (uint16_t*)p;
+    p += round_up(N * F * 2, 256);
+    uint16_t* gpos = (uint16_t*)p;
+    p += round_up((g->nnz + N) * 2, 256);
+    float* dpack = (float*)p;
+    hipLaunchKernelGGL((group_pack_kernel<uint16_t>), dim3((unsigned)N), dim3(kBlock), 0, st, g->ptr,
+                       (const uint16_t*)argpos, lda, (int)F, dout, ldd, gfeat, gpos, dpack);
+    const int blocks = grid_for(gt->n_items);
+    if (g->ew)
+      hipLaunchKernelGGL((max_bwd_pull_kernel<true>), dim3(blocks), dim3(kBlock), 0, st, g->ew, gt->col,
+                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, gfeat, gpos, dpack,
+                         (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F));
+    else
+      hipLaunchKernelGGL((max_bwd_pull_kernel<false>), dim3(blocks), dim3(kBlock), 0, st, g->ew, gt->col,
+                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, gfeat, gpos, dpack,
+                         (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F));
+    if (gt->n_merges > 0)
+      hipLaunchKernelGGL(sum_merge_kernel, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
+                         (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
+                         mask_src, ldm, dx, ldx);
+    return hip_status("pg_spmm_max_bwd");
+  }
   if (arg_kind == PG_ARG_U16)
     return launch_max_bwd<uint16_t>(g, gt, (const uint16_t*)argpos, lda, dout, ldd, F, mask_src,
                                     ldm, dx, ldx, w, ws_ld(F), st);

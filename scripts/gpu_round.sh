@@ -15,6 +15,13 @@ if [ "${GEMM_BENCH:-0}" = "1" ]; then
   rcg=$?; echo "gemm_bench rc=$rcg"; cat gpurun_out/gemm_bench.txt | tail -25
   if [ $rcg -ne 0 ]; then exit $rcg; fi
 fi
+if [ "${SPMM_BENCH:-0}" = "1" ]; then
+  for cfg in "" "PLAGNN_SPMM_FTILE=256" "PLAGNN_BWD_PATH=direct"; do
+    env $cfg timeout -k 10 300 python scripts/spmm_bench.py >> gpurun_out/spmm_bench.txt 2>&1
+    rcs=$?; if [ $rcs -ne 0 ]; then echo "spmm_bench rc=$rcs"; cat gpurun_out/spmm_bench.txt; exit $rcs; fi
+  done
+  cat gpurun_out/spmm_bench.txt | grep -v amdgpu.ids
+fi
 if [ "${SKIP_BENCH:-0}" = "1" ]; then exit $rc; fi
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 5 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc2=$?

@@ -129,7 +129,8 @@ def test_spmm_sum_fwd_bwd(oracle_mod, mean, weighted):
     Xd = torch.from_numpy(X).to(DEV).requires_grad_(True)
     out = ops.SumAggregate.apply(Xd, dg, ews, mean)
     ref = oracle_mod.spmm_sum(og, X, mean=mean, use_weight=weighted)
-    np.testing.assert_allclose(out.detach().cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    # hub rows are summed in 256-entry partials (fp32 reassociation)
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref, rtol=1e-4, atol=1e-4)
     # backward against the dense adjacency (float64)
     A = np.zeros((n, n))
     for k, (s, d) in enumerate(zip(src, dst)):
