@@ -522,14 +522,24 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
           float w = 1.f;
           if constexpr (HAS_W) w = bcastf(wv, je);
           if (lane < n) acc[fe[e]] += HAS_W ? w * de[e] : de[e];
-          if (n > kWave) {  // long list (low in-degree v): remaining segments, in order
+          if (n > kWave) {
+            // long list (one winner takes many features, or low in-degree v): the rest of
+            // the list in batches of 8 segments, all loads first; a list holds distinct
+            // features, so its segments may be added in any order
             const int64_t base = (int64_t)bcast(vv, je) * F + bcast(sv, je);
-            for (int s = kWave; s < n; s += kWave) {
-              if (s + lane < n) {
-                const int f = gfeat[base + s + lane];
-                const float d = dpack[base + s + lane];
-                acc[f] += HAS_W ? w * d : d;
+            for (int s0 = kWave; s0 < n; s0 += 8 * kWave) {
+              int fs[8];
+              float ds[8];
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                const int idx = s0 + q * kWave + lane;
+                const bool on = idx < n;
+                fs[q] = on ? (int)gfeat[base + idx] : 0;
+                ds[q] = on ? dpack[base + idx] : 0.f;
               }
+#pragma unroll
+              for (int q = 0; q < 8; ++q)
+                if (s0 + q * kWave + lane < n) acc[fs[q]] += HAS_W ? w * ds[q] : ds[q];
             }
           }
         }
@@ -766,7 +776,7 @@ struct TilePlan {
 inline int64_t vec_ftile() {
   static const int64_t t = [] {
     const char* e = getenv("PLAGNN_SPMM_FTILE");
-    int64_t v = e ? atoll(e) : 1024;
+    int64_t v = e ? atoll(e) : 256;
     if (v < 256 || v > kFTileVec || v % 256) v = kFTileVec;
     return v;
   }();

@@ -21,7 +21,8 @@ import torch
 from . import _lib
 from ._lib import PgCsr, call
 
-DEFAULT_CHUNK = 256  # entries per work item before a row is split across waves
+DEFAULT_CHUNK = 256      # in-CSR entries per forward work item before a row is split
+DEFAULT_CHUNK_BWD = 128  # out-CSR entries per backward work item (its work is data-dependent)
 
 
 def _np_ptr(a: np.ndarray) -> int:
@@ -90,7 +91,8 @@ class DeviceCsr:
 class CSRGraph:
     """In-CSR + out-CSR of a directed graph given as COO (src -> dst), host resident."""
 
-    def __init__(self, src, dst, num_nodes: int, chunk: int = DEFAULT_CHUNK):
+    def __init__(self, src, dst, num_nodes: int, chunk: int = DEFAULT_CHUNK,
+                 chunk_bwd: int = DEFAULT_CHUNK_BWD):
         src = np.ascontiguousarray(np.asarray(src, dtype=np.int64))
         dst = np.ascontiguousarray(np.asarray(dst, dtype=np.int64))
         if src.shape != dst.shape or src.ndim != 1:
@@ -113,7 +115,7 @@ class CSRGraph:
         self.num_edges = E
         self.eid = eid  # in-CSR slot -> edge id
         self.fwd = HostCsr(ptr, col, None, n, chunk)
-        self.bwd = HostCsr(tptr, tcol[:E], tslot[:E], n, chunk, epos=tpos[:E])
+        self.bwd = HostCsr(tptr, tcol[:E], tslot[:E], n, min(chunk, chunk_bwd), epos=tpos[:E])
         # argmax records hold positions inside in-CSR rows: u16 while every row is shorter
         # than 0xFFFF entries (0xFFFF = no winner)
         self.arg_kind = _lib.PG_ARG_U16 if self.fwd.max_deg < 0xFFFF else _lib.PG_ARG_I32
