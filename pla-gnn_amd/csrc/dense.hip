@@ -137,12 +137,15 @@ __global__ __launch_bounds__(kBlock) void sigmoid_zero_kernel(const float* __res
 // the pair's loss term into LDS and its gradient into dz; then thread c < C sums its
 // class over the block's rows in row order (deterministic), giving part[b][c].
 // Mirrors the autograd graph of code/train.py:103-104 operation by operation.
-constexpr int kLossRows = 64;  // rows per block; kLossRows * C <= 64 * 64 pairs
+constexpr int kLossTerms = 4096;  // (row, class) terms per block held in LDS
+// rows per block: as many as fit kLossTerms, at most 256
+inline __host__ __device__ int loss_rows(int C) { return C * 256 <= kLossTerms ? 256 : kLossTerms / C; }
 __global__ __launch_bounds__(kBlock) void multi_loss_kernel(
     const float* __restrict__ z, int64_t ldz, int C, const float* __restrict__ labels,
     int64_t ldl, const float* __restrict__ cw, const int32_t* __restrict__ index, int64_t n_index,
     float* __restrict__ part, float* __restrict__ dz, int64_t lddz) {
-  __shared__ float terms[kLossRows * 64];
+  __shared__ float terms[kLossTerms];
+  const int kLossRows = loss_rows(C);
   const int64_t r0 = (int64_t)blockIdx.x * kLossRows;
   const int nr = (int)min<int64_t>(kLossRows, n_index - r0);
   const float inv_n = 1.0f / (float)n_index;
@@ -297,7 +300,7 @@ int pg_col_sum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* o
 }
 
 size_t pg_sigmoid_multi_loss_workspace(int64_t n_index, int32_t C) {
-  const int64_t nb = std::max<int64_t>(1, (n_index + kLossRows - 1) / kLossRows);
+  const int64_t nb = std::max<int64_t>(1, (n_index + loss_rows(C) - 1) / loss_rows(C));
   return (size_t)(nb * std::max(C, 1) * 4 + 2 * 64 * 4);
 }
 
@@ -317,7 +320,7 @@ int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C
   if ((prob || dz) && n_rows > 0)
     hipLaunchKernelGGL(sigmoid_zero_kernel, dim3(grid_1d(n_rows * C)), dim3(kBlock), 0, st, z, ldz,
                        n_rows, (int)C, prob, ldp, dz, lddz);
-  const int nb = (int)std::max<int64_t>(1, (n_index + kLossRows - 1) / kLossRows);
+  const int nb = (int)std::max<int64_t>(1, (n_index + loss_rows(C) - 1) / loss_rows(C));
   float* part = (float*)ws;
   if (n_index > 0) {
     hipLaunchKernelGGL(multi_loss_kernel, dim3(nb), dim3(kBlock), 0, st, z, ldz, (int)C, labels, ldl,

@@ -33,10 +33,16 @@ constexpr int KPAD = BK + 4;  // [row][k] image row stride (floats)
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-template <int ACT>
-__device__ __forceinline__ float epi_act(float x, float slope) {
-  if constexpr (ACT == PG_ACT_RELU) return x > 0.f ? x : 0.f;
-  else if constexpr (ACT == PG_ACT_LEAKY) return x > 0.f ? x : x * slope;
+// Epilogue modes: activation of the result, or multiplication by the derivative of an
+// activation given its OUTPUT y (the fused backward of relu / leaky_relu), or split-K.
+enum Epi { EPI_NONE = 0, EPI_RELU = 1, EPI_LEAKY = 2, EPI_DRELU = 3, EPI_DLEAKY = 4, EPI_SPLIT = 5 };
+
+template <int EPI>
+__device__ __forceinline__ float epi_apply(float x, float y, float slope) {
+  if constexpr (EPI == EPI_RELU) return x > 0.f ? x : 0.f;
+  else if constexpr (EPI == EPI_LEAKY) return x > 0.f ? x : x * slope;
+  else if constexpr (EPI == EPI_DRELU) return y > 0.f ? x : 0.f;
+  else if constexpr (EPI == EPI_DLEAKY) return y > 0.f ? x : x * slope;
   else return x;
 }
 
@@ -133,11 +139,13 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ S, int rc, i
 }
 
 // TA: A stored K x M (use A^T). TB: B stored N x K (use B^T).
-template <int BM, int BN, bool TA, bool TB, bool VA, bool VB, int ACT, bool SPLIT>
+template <int BM, int BN, bool TA, bool TB, bool VA, bool VB, int EPI>
 __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
     int M, int N, int K, int k_per_split, float alpha, const float* __restrict__ A, int64_t lda,
     const float* __restrict__ B, int64_t ldb, float beta, float* __restrict__ C, int64_t ldc,
-    const float* __restrict__ bias, float slope, float* __restrict__ ws) {
+    const float* __restrict__ bias, float slope, const float* __restrict__ dact, int64_t lddact,
+    float* __restrict__ ws) {
+  constexpr bool SPLIT = EPI == EPI_SPLIT;
   constexpr bool AK = TA;    // A image k-major ([k][m]) when A is stored transposed
   constexpr bool BKM = !TB;  // B image k-major ([k][n]) when B is stored K x N
   constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
@@ -217,7 +225,9 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
           float v = alpha * acc[i][j][r];
           if (beta != 0.f) v = v + beta * C[(int64_t)row * ldc + col];
           if (bias) v = v + bv;
-          C[(int64_t)row * ldc + col] = epi_act<ACT>(v, slope);
+          float y = 0.f;
+          if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) y = dact[(int64_t)row * lddact + col];
+          C[(int64_t)row * ldc + col] = epi_apply<EPI>(v, y, slope);
         }
       }
     }
@@ -255,44 +265,45 @@ struct Args {
   int64_t ldc;
   const float* bias;
   float slope;
+  const float* dact;
+  int64_t lddact;
   float* ws;
 };
 
-template <int BM, int BN, bool TA, bool TB, bool VA, bool VB, bool SPLIT>
-int launch_act(int act, dim3 grid, hipStream_t st, const Args& a) {
-#define PG_L(ACT_)                                                                          \
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, VA, VB, ACT_, SPLIT>), grid,            \
-                     dim3(kThreads), 0, st, a.M, a.N, a.K, a.kps, a.alpha, a.A, a.lda, a.B,   \
-                     a.ldb, a.beta, a.C, a.ldc, a.bias, a.slope, a.ws)
-  if (SPLIT) {
-    PG_L(PG_ACT_NONE);
-    return PG_OK;
-  }
-  switch (act) {
-    case PG_ACT_NONE: PG_L(PG_ACT_NONE); break;
-    case PG_ACT_RELU: PG_L(PG_ACT_RELU); break;
-    case PG_ACT_LEAKY: PG_L(PG_ACT_LEAKY); break;
+template <int BM, int BN, bool TA, bool TB, bool VA, bool VB>
+int launch_epi(int epi, dim3 grid, hipStream_t st, const Args& a) {
+#define PG_L(EPI_)                                                                          \
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, VA, VB, EPI_>), grid, dim3(kThreads), 0, \
+                     st, a.M, a.N, a.K, a.kps, a.alpha, a.A, a.lda, a.B, a.ldb, a.beta, a.C,  \
+                     a.ldc, a.bias, a.slope, a.dact, a.lddact, a.ws)
+  switch (epi) {
+    case EPI_NONE: PG_L(EPI_NONE); break;
+    case EPI_RELU: PG_L(EPI_RELU); break;
+    case EPI_LEAKY: PG_L(EPI_LEAKY); break;
+    case EPI_DRELU: PG_L(EPI_DRELU); break;
+    case EPI_DLEAKY: PG_L(EPI_DLEAKY); break;
+    case EPI_SPLIT: PG_L(EPI_SPLIT); break;
     default: return PG_ERR_INVALID;
   }
 #undef PG_L
   return PG_OK;
 }
 
-template <int BM, int BN, bool TA, bool TB, bool SPLIT>
-int launch_vec(bool va, bool vb, int act, dim3 grid, hipStream_t st, const Args& a) {
-  if (va && vb) return launch_act<BM, BN, TA, TB, true, true, SPLIT>(act, grid, st, a);
-  if (va) return launch_act<BM, BN, TA, TB, true, false, SPLIT>(act, grid, st, a);
-  if (vb) return launch_act<BM, BN, TA, TB, false, true, SPLIT>(act, grid, st, a);
-  return launch_act<BM, BN, TA, TB, false, false, SPLIT>(act, grid, st, a);
+template <int BM, int BN, bool TA, bool TB>
+int launch_vec(bool va, bool vb, int epi, dim3 grid, hipStream_t st, const Args& a) {
+  if (va && vb) return launch_epi<BM, BN, TA, TB, true, true>(epi, grid, st, a);
+  if (va) return launch_epi<BM, BN, TA, TB, true, false>(epi, grid, st, a);
+  if (vb) return launch_epi<BM, BN, TA, TB, false, true>(epi, grid, st, a);
+  return launch_epi<BM, BN, TA, TB, false, false>(epi, grid, st, a);
 }
 
-template <int BM, int BN, bool SPLIT>
-int launch_trans(bool ta, bool tb, bool va, bool vb, int act, dim3 grid, hipStream_t st,
+template <int BM, int BN>
+int launch_trans(bool ta, bool tb, bool va, bool vb, int epi, dim3 grid, hipStream_t st,
                  const Args& a) {
-  if (!ta && !tb) return launch_vec<BM, BN, false, false, SPLIT>(va, vb, act, grid, st, a);
-  if (!ta && tb) return launch_vec<BM, BN, false, true, SPLIT>(va, vb, act, grid, st, a);
-  if (ta && !tb) return launch_vec<BM, BN, true, false, SPLIT>(va, vb, act, grid, st, a);
-  return launch_vec<BM, BN, true, true, SPLIT>(va, vb, act, grid, st, a);
+  if (!ta && !tb) return launch_vec<BM, BN, false, false>(va, vb, epi, grid, st, a);
+  if (!ta && tb) return launch_vec<BM, BN, false, true>(va, vb, epi, grid, st, a);
+  if (ta && !tb) return launch_vec<BM, BN, true, false>(va, vb, epi, grid, st, a);
+  return launch_vec<BM, BN, true, true>(va, vb, epi, grid, st, a);
 }
 
 // Tile choice: BN = 64 for narrow outputs, else 128; BM = 128 only when that still gives
@@ -315,8 +326,8 @@ size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k) {
 
 int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
-                int64_t ldc, const float* bias, int act, float slope, int split_k, void* ws,
-                size_t ws_bytes, pg_stream_t stream) {
+                int64_t ldc, const float* bias, int act, float slope, const float* dact,
+                int64_t lddact, int split_k, void* ws, size_t ws_bytes, pg_stream_t stream) {
   if (M < 0 || N < 0 || K < 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
     return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32: bad sizes");
   if (ldc < N || (!transa && lda < K) || (transa && lda < M) || (!transb && ldb < N) ||
@@ -325,8 +336,10 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   if (act != PG_ACT_NONE && act != PG_ACT_RELU && act != PG_ACT_LEAKY)
     return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32: bad act %d", act);
   if (split_k < 1) split_k = 1;
-  if (split_k > 1 && (bias || act != PG_ACT_NONE || (beta != 0.f && beta != 1.f)))
+  if (split_k > 1 && (bias || act != PG_ACT_NONE || dact || (beta != 0.f && beta != 1.f)))
     return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32: split_k > 1 takes no bias/act, beta 0|1");
+  if (dact && (act == PG_ACT_NONE || lddact < N))
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32: dact needs act relu|leaky and lddact >= N");
   if (M == 0 || N == 0) return pg::ok();
   if (split_k > 1 && ws_bytes < pg_gemm_f32_workspace(M, N, K, split_k))
     return pg::set_error(PG_ERR_WORKSPACE, "pg_gemm_f32: workspace too small");
@@ -347,21 +360,20 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   dim3 grid((unsigned)((N + bn - 1) / bn), (unsigned)((M + bm - 1) / bm), (unsigned)split_k);
   hipStream_t st = (hipStream_t)stream;
   const Args a{(int)M, (int)N, (int)K, kps, alpha, A, lda, B, ldb, beta, C, ldc, bias, slope,
-               split ? (float*)ws : nullptr};
+               dact, lddact, split ? (float*)ws : nullptr};
   const bool ta = transa != 0, tb = transb != 0;
+  const int epi = split ? EPI_SPLIT
+                        : dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
+                               : (act == PG_ACT_RELU ? EPI_RELU : act == PG_ACT_LEAKY ? EPI_LEAKY : EPI_NONE);
   int rc;
   if (bm == 128 && bn == 128)
-    rc = split ? launch_trans<128, 128, true>(ta, tb, va, vb, act, grid, st, a)
-               : launch_trans<128, 128, false>(ta, tb, va, vb, act, grid, st, a);
+    rc = launch_trans<128, 128>(ta, tb, va, vb, epi, grid, st, a);
   else if (bm == 64 && bn == 128)
-    rc = split ? launch_trans<64, 128, true>(ta, tb, va, vb, act, grid, st, a)
-               : launch_trans<64, 128, false>(ta, tb, va, vb, act, grid, st, a);
+    rc = launch_trans<64, 128>(ta, tb, va, vb, epi, grid, st, a);
   else if (bm == 128)
-    rc = split ? launch_trans<128, 64, true>(ta, tb, va, vb, act, grid, st, a)
-               : launch_trans<128, 64, false>(ta, tb, va, vb, act, grid, st, a);
+    rc = launch_trans<128, 64>(ta, tb, va, vb, epi, grid, st, a);
   else
-    rc = split ? launch_trans<64, 64, true>(ta, tb, va, vb, act, grid, st, a)
-               : launch_trans<64, 64, false>(ta, tb, va, vb, act, grid, st, a);
+    rc = launch_trans<64, 64>(ta, tb, va, vb, epi, grid, st, a);
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_f32: dispatch failed");
   if (split) {
     const int64_t n = M * N;

@@ -8,16 +8,24 @@ One step is exactly the reference's epoch body (code/train.py:197-207):
 computed without autograd: forward and backward are written out layer by layer and the
 whole step is captured once into a HIP graph (torch.cuda.CUDAGraph) and replayed.
 
-Layout in HBM (all fp32, row-major, every width padded to a multiple of 4 with zero pads
-that stay exactly zero through forward, backward and Adam):
-  * parameters: ONE flat buffer (Adam is one launch, a multi-GPU all-reduce is one
-    bucket). Per SAGE layer l (Fi -> Fo): Wpool[Fi][Fi], bpool[Fi],
-    Wcat[Fo][2Fi] = [Wself | Wneigh] (so Y = [H | M] @ Wcat^T is a single K = 2Fi GEMM),
-    b[Fo]; then liner1 W1/b1 and liner2 W2/b2.
-  * activations: HM_l[N][2Fi] = [H_l | M_l] — the layer's input H_l (the previous layer's
-    leaky_relu output, written there directly by that layer's GEMM epilogue) beside the
-    max-aggregated neighbourhood M_l (written there by the SpMM); P_l[N][Fi]
-    (relu(fc_pool)); argpos_l[N][Fi] (u16 winning in-row positions).
+Layout in HBM (fp32, row-major; every width padded to a multiple of 4 with zero pads that
+stay exactly zero through forward, backward and Adam):
+  * Bias as a column. Every layer input carries a constant block [1 0 0 0] after its
+    features, and every weight matrix carries its bias in the matching column, so
+    x @ W_ext^T = x @ W^T + b is one GEMM, and the weight-gradient GEMM dY^T @ [x | 1]
+    yields the bias gradient (sum of dY over nodes) as its extra column: no bias
+    epilogue and no separate column-sum kernel.
+  * SAGE layer l (Fi -> Fo): HM_l[N][2Fi + 4] = [H_l | 1 0 0 0 | M_l] — the layer input
+    H_l (written there by the previous layer's GEMM epilogue), the ones block, and the
+    max-aggregated neighbourhood M_l (written there by the SpMM). Parameters
+    Wpool_ext[Fi][Fi + 4] = [Wpool | bpool 0 0 0] (reads HM[:, :Fi + 4]) and
+    Wcat_ext[Fo][2Fi + 4] = [Wself | b 0 0 0 | Wneigh] (reads all of HM): fc_self +
+    fc_neigh + bias is ONE K = 2Fi + 4 GEMM. P_l[N][Fi] = relu(fc_pool), argpos_l[N][Fi]
+    (u16 winning in-row positions).
+  * All parameters live in ONE flat buffer (Adam is one launch; a multi-GPU all-reduce is
+    one bucket), gradients in a second one with the same layout.
+  * Activation backward (leaky_relu') is fused into the epilogue of the GEMM producing
+    the gradient (pg_gemm_f32 with dact), relu' of fc_pool into the SpMM backward.
 """
 from __future__ import annotations
 
@@ -34,22 +42,26 @@ from .graph import CSRGraph, DeviceGraph
 from .ops import LEAKY_SLOPE, round4
 
 RELU, LEAKY, NONE = _lib.PG_ACT_RELU, _lib.PG_ACT_LEAKY, _lib.PG_ACT_NONE
+ONE = 4  # width of the constant [1 0 0 0] block that carries the bias
 
 
 class _Flat:
-    """Named, padded views into one flat fp32 buffer."""
+    """Named views into one flat fp32 buffer (256-B aligned)."""
 
     def __init__(self):
-        self.layout: List = []  # (name, shape_padded, shape_true, offset)
+        self.layout: List = []  # (name, shape)
+        self.offsets: Dict[str, int] = {}
         self.size = 0
 
-    def add(self, name, shape_p, shape_t):
-        n = int(np.prod(shape_p))
-        self.layout.append((name, tuple(shape_p), tuple(shape_t), self.size))
-        self.size += (n + 63) // 64 * 64  # 256-B aligned views
+    def add(self, name, shape):
+        n = int(np.prod(shape))
+        self.layout.append((name, tuple(shape)))
+        self.offsets[name] = self.size
+        self.size += (n + 63) // 64 * 64
 
     def views(self, buf: torch.Tensor) -> Dict[str, torch.Tensor]:
-        return {name: buf[off:off + int(np.prod(sp))].view(*sp) for name, sp, _, off in self.layout}
+        return {name: buf[self.offsets[name]:self.offsets[name] + int(np.prod(sh))].view(*sh)
+                for name, sh in self.layout}
 
 
 class TrainEngine:
@@ -63,6 +75,8 @@ class TrainEngine:
             raise ValueError("TrainEngine runs on a HIP device; use the dgl shim for -d cpu")
         self.dims = list(dims)
         self.L = len(self.dims) - 3
+        if self.L < 1:
+            raise ValueError("dims = [in, h_1, ..., h_L, h_mlp, classes] with L >= 1")
         N = graph.num_nodes
         self.N = N
         self.dg: DeviceGraph = graph.on(self.device)
@@ -71,22 +85,17 @@ class TrainEngine:
         C = self.dims[-1]
         self.C = C
         dev = self.device
-
-        # ---- parameters (flat, padded) ----
-        fl = _Flat()
         pd = [round4(d) for d in self.dims]
         self.pd = pd
+
+        # ---- parameters (flat, padded, bias as a column) ----
+        fl = _Flat()
         for l in range(self.L):
             Fi, Fo = pd[l], pd[l + 1]
-            fi, fo = self.dims[l], self.dims[l + 1]
-            fl.add(f"conv{l + 1}.Wpool", (Fi, Fi), (fi, fi))
-            fl.add(f"conv{l + 1}.bpool", (Fi,), (fi,))
-            fl.add(f"conv{l + 1}.Wcat", (Fo, 2 * Fi), (fo, 2 * fi))
-            fl.add(f"conv{l + 1}.b", (Fo,), (fo,))
-        fl.add("liner1.W", (pd[-2], pd[-3]), (self.dims[-2], self.dims[-3]))
-        fl.add("liner1.b", (pd[-2],), (self.dims[-2],))
-        fl.add("liner2.W", (pd[-1], pd[-2]), (self.dims[-1], self.dims[-2]))
-        fl.add("liner2.b", (pd[-1],), (self.dims[-1],))
+            fl.add(f"conv{l + 1}.Wpool", (Fi, Fi + ONE))
+            fl.add(f"conv{l + 1}.Wcat", (Fo, 2 * Fi + ONE))
+        fl.add("liner1.W", (pd[-2], pd[-3] + ONE))
+        fl.add("liner2.W", (pd[-1], pd[-2] + ONE))
         self.flat_layout = fl
         self.flat = torch.zeros(fl.size, dtype=torch.float32, device=dev)
         self.gflat = torch.zeros_like(self.flat)
@@ -103,7 +112,7 @@ class TrainEngine:
         self.load_state_dict(params)
 
         # ---- inputs ----
-        if features.shape != (N, self.dims[0]):
+        if tuple(features.shape) != (N, self.dims[0]):
             raise ValueError(f"features must be ({N}, {self.dims[0]})")
         self.labels = torch.zeros(N, pd[-1], dtype=torch.float32, device=dev)
         self.labels[:, :C] = labels.to(dev, torch.float32)
@@ -118,17 +127,21 @@ class TrainEngine:
         self.val_index = None if val_index is None else torch.as_tensor(
             np.asarray(val_index, np.int32), device=dev)
 
-        # ---- activations ----
+        # ---- activations (ones blocks set once; nothing else ever writes them) ----
         f32 = dict(dtype=torch.float32, device=dev)
         self.HM, self.Pl, self.arg = [], [], []
         for l in range(self.L):
             Fi = pd[l]
-            self.HM.append(torch.zeros(N, 2 * Fi, **f32))
+            hm = torch.zeros(N, 2 * Fi + ONE, **f32)
+            hm[:, Fi] = 1.0
+            self.HM.append(hm)
             self.Pl.append(torch.zeros(N, Fi, **f32))
             self.arg.append(torch.zeros(N, Fi, dtype=self.dg.arg_dtype, device=dev))
         self.HM[0][:, :self.dims[0]] = features.to(dev, torch.float32)
-        self.A3 = torch.zeros(N, pd[-3], **f32)
-        self.A4 = torch.zeros(N, pd[-2], **f32)
+        self.A3 = torch.zeros(N, pd[-3] + ONE, **f32)
+        self.A3[:, pd[-3]] = 1.0
+        self.A4 = torch.zeros(N, pd[-2] + ONE, **f32)
+        self.A4[:, pd[-2]] = 1.0
         self.Z = torch.zeros(N, pd[-1], **f32)
         self.prob = torch.zeros(N, pd[-1], **f32)
         self.loss = torch.zeros(2, **f32)  # [train, val]
@@ -136,7 +149,7 @@ class TrainEngine:
         self.dZ = torch.zeros(N, pd[-1], **f32)
         self.dA4 = torch.zeros(N, pd[-2], **f32)
         self.dA3 = torch.zeros(N, pd[-3], **f32)
-        self.dHM = [torch.zeros(N, 2 * pd[l], **f32) for l in range(self.L)]
+        self.dHM = [torch.zeros(N, 2 * pd[l] + ONE, **f32) for l in range(self.L)]
         self.dP = [torch.zeros(N, pd[l], **f32) for l in range(self.L)]
 
         # ---- workspace (one buffer, sized for the largest call) ----
@@ -151,8 +164,6 @@ class TrainEngine:
             sk = ops._split_k(M_, N_, K_)
             self._gemm_plans[(M_, N_, K_)] = sk
             need = max(need, L.pg_gemm_f32_workspace(M_, N_, K_, sk))
-        for w in pd:
-            need = max(need, L.pg_col_sum_workspace(N, w))
         need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
         self.ws_bytes = self.ws.numel()
@@ -164,13 +175,12 @@ class TrainEngine:
 
     # ------------------------------------------------------------------ parameters
     def _wgrad_shapes(self):
-        pd = self.pd
-        N = self.N
+        pd, N = self.pd, self.N
         out = []
         for l in range(self.L):
             Fi, Fo = pd[l], pd[l + 1]
-            out += [(Fo, 2 * Fi, N), (Fi, Fi, N)]
-        out += [(pd[-2], pd[-3], N), (pd[-1], pd[-2], N)]
+            out += [(Fo, 2 * Fi + ONE, N), (Fi, Fi + ONE, N)]
+        out += [(pd[-2], pd[-3] + ONE, N), (pd[-1], pd[-2] + ONE, N)]
         return out
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
@@ -179,35 +189,36 @@ class TrainEngine:
             self.flat.zero_()
             for l in range(self.L):
                 p = f"conv{l + 1}."
-                fi, fo = self.dims[l], self.dims[l + 1]
-                self.P[p + "Wpool"][:fi, :fi] = sd[p + "fc_pool.weight"]
-                self.P[p + "bpool"][:fi] = sd[p + "fc_pool.bias"]
-                Fi = self.pd[l]
-                self.P[p + "Wcat"][:fo, :fi] = sd[p + "fc_self.weight"]
-                self.P[p + "Wcat"][:fo, Fi:Fi + fi] = sd[p + "fc_neigh.weight"]
-                if p + "bias" in sd and sd[p + "bias"] is not None:
-                    self.P[p + "b"][:fo] = sd[p + "bias"]
-            d = self.dims
+                fi, fo, Fi = self.dims[l], self.dims[l + 1], self.pd[l]
+                Wp, Wc = self.P[p + "Wpool"], self.P[p + "Wcat"]
+                Wp[:fi, :fi] = sd[p + "fc_pool.weight"]
+                Wp[:fi, Fi] = sd[p + "fc_pool.bias"]
+                Wc[:fo, :fi] = sd[p + "fc_self.weight"]
+                if sd.get(p + "bias") is not None:
+                    Wc[:fo, Fi] = sd[p + "bias"]
+                Wc[:fo, Fi + ONE:Fi + ONE + fi] = sd[p + "fc_neigh.weight"]
+            d, pd = self.dims, self.pd
             self.P["liner1.W"][:d[-2], :d[-3]] = sd["liner1.weight"]
-            self.P["liner1.b"][:d[-2]] = sd["liner1.bias"]
+            self.P["liner1.W"][:d[-2], pd[-3]] = sd["liner1.bias"]
             self.P["liner2.W"][:d[-1], :d[-2]] = sd["liner2.weight"]
-            self.P["liner2.b"][:d[-1]] = sd["liner2.bias"]
+            self.P["liner2.W"][:d[-1], pd[-2]] = sd["liner2.bias"]
 
     def _unpad(self, views: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         out = {}
         for l in range(self.L):
             p = f"conv{l + 1}."
             fi, fo, Fi = self.dims[l], self.dims[l + 1], self.pd[l]
-            out[p + "fc_pool.weight"] = views[p + "Wpool"][:fi, :fi].clone()
-            out[p + "fc_pool.bias"] = views[p + "bpool"][:fi].clone()
-            out[p + "fc_neigh.weight"] = views[p + "Wcat"][:fo, Fi:Fi + fi].clone()
-            out[p + "fc_self.weight"] = views[p + "Wcat"][:fo, :fi].clone()
-            out[p + "bias"] = views[p + "b"][:fo].clone()
-        d = self.dims
+            Wp, Wc = views[p + "Wpool"], views[p + "Wcat"]
+            out[p + "fc_pool.weight"] = Wp[:fi, :fi].clone()
+            out[p + "fc_pool.bias"] = Wp[:fi, Fi].clone()
+            out[p + "fc_neigh.weight"] = Wc[:fo, Fi + ONE:Fi + ONE + fi].clone()
+            out[p + "fc_self.weight"] = Wc[:fo, :fi].clone()
+            out[p + "bias"] = Wc[:fo, Fi].clone()
+        d, pd = self.dims, self.pd
         out["liner1.weight"] = views["liner1.W"][:d[-2], :d[-3]].clone()
-        out["liner1.bias"] = views["liner1.b"][:d[-2]].clone()
+        out["liner1.bias"] = views["liner1.W"][:d[-2], pd[-3]].clone()
         out["liner2.weight"] = views["liner2.W"][:d[-1], :d[-2]].clone()
-        out["liner2.bias"] = views["liner2.b"][:d[-1]].clone()
+        out["liner2.bias"] = views["liner2.W"][:d[-1], pd[-2]].clone()
         return out
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
@@ -218,7 +229,9 @@ class TrainEngine:
 
     @property
     def num_params(self) -> int:
-        return sum(int(np.prod(st)) for _, _, st, _ in self.flat_layout.layout)
+        d = self.dims
+        n = sum(d[l] * d[l] + d[l] + 2 * d[l] * d[l + 1] + d[l + 1] for l in range(self.L))
+        return n + d[-3] * d[-2] + d[-2] + d[-2] * d[-1] + d[-1]
 
     # ------------------------------------------------------------------ timing
     @contextlib.contextmanager
@@ -255,23 +268,15 @@ class TrainEngine:
     def _s(self):
         return _lib.stream_handle(self.device)
 
-    def _gemm(self, A, B, C, transa=False, transb=False, beta=0.0, bias=None, act=NONE, tag="gemm"):
+    def _gemm(self, A, B, C, transa=False, transb=False, beta=0.0, act=NONE, dact=None, tag="gemm"):
         M = A.shape[1] if transa else A.shape[0]
         K = A.shape[0] if transa else A.shape[1]
         N = B.shape[0] if transb else B.shape[1]
-        sk = self._gemm_plans.get((M, N, K), 1) if (bias is None and act == NONE) else 1
+        sk = self._gemm_plans.get((M, N, K), 1) if (act == NONE and dact is None) else 1
         with self._t(tag, 2.0 * M * N * K):
-            self._gemm_call(A, B, C, transa, transb, beta, bias, act, M, N, K, sk)
-
-    def _gemm_call(self, A, B, C, transa, transb, beta, bias, act, M, N, K, sk):
-        call("pg_gemm_f32", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
-             B.stride(0), beta, ptr(C), C.stride(0), ptr(bias), act, LEAKY_SLOPE, sk, ptr(self.ws),
-             self.ws_bytes, self._s())
-
-    def _colsum(self, x, out):
-        with self._t("col_sum", 4.0 * x.shape[0] * x.shape[1]):
-            call("pg_col_sum", ptr(x), x.stride(0), x.shape[0], x.shape[1], ptr(out), 0, ptr(self.ws),
-                 self.ws_bytes, self._s())
+            call("pg_gemm_f32", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
+                 B.stride(0), beta, ptr(C), C.stride(0), 0, act, LEAKY_SLOPE, ptr(dact),
+                 dact.stride(0) if dact is not None else 0, sk, ptr(self.ws), self.ws_bytes, self._s())
 
     def forward(self) -> None:
         """Logits (self.prob) and both losses; dZ = d train_loss / d z."""
@@ -281,25 +286,24 @@ class TrainEngine:
             p = f"conv{l + 1}."
             Fi = self.pd[l]
             HM = self.HM[l]
-            H = HM[:, :Fi]
-            # P = relu(H Wpool^T + bpool)
-            self._gemm(H, self.P[p + "Wpool"], self.Pl[l], transb=True, bias=self.P[p + "bpool"], act=RELU,
+            # P = relu([H | 1] Wpool_ext^T)
+            self._gemm(HM[:, :Fi + ONE], self.P[p + "Wpool"], self.Pl[l], transb=True, act=RELU,
                        tag=f"gemm.fwd.pool.l{l + 1}")
-            # M = max-aggregate(P) -> right half of HM
-            M = HM[:, Fi:]
+            # M = max-aggregate(P) -> right block of HM
+            M = HM[:, Fi + ONE:]
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
                 call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(M), HM.stride(0), ptr(self.arg[l]),
                      Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
-            # Y = [H | M] Wcat^T + b, leaky_relu -> next layer's input
-            out = self.HM[l + 1][:, :self.pd[l + 1]] if l + 1 < self.L else self.A3
-            self._gemm(HM, self.P[p + "Wcat"], out, transb=True, bias=self.P[p + "b"], act=LEAKY,
-                       tag=f"gemm.fwd.cat.l{l + 1}")
-        self._gemm(self.A3, self.P["liner1.W"], self.A4, transb=True, bias=self.P["liner1.b"], act=LEAKY,
+            # Y = [H | 1 | M] Wcat_ext^T (fc_self + fc_neigh + bias), leaky_relu -> next input
+            Fo = self.pd[l + 1]
+            out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3[:, :Fo]
+            self._gemm(HM, self.P[p + "Wcat"], out, transb=True, act=LEAKY, tag=f"gemm.fwd.cat.l{l + 1}")
+        pd = self.pd
+        self._gemm(self.A3, self.P["liner1.W"], self.A4[:, :pd[-2]], transb=True, act=LEAKY,
                    tag="gemm.fwd.liner1")
-        self._gemm(self.A4, self.P["liner2.W"], self.Z, transb=True, bias=self.P["liner2.b"], act=NONE,
-                   tag="gemm.fwd.liner2")
+        self._gemm(self.A4, self.P["liner2.W"], self.Z, transb=True, act=NONE, tag="gemm.fwd.liner2")
         C = self.C
-        cp = self.pd[-1]
+        cp = pd[-1]
         with self._t("loss"):
             call("pg_sigmoid_multi_loss", ptr(self.Z), cp, self.N, C, ptr(self.labels), cp, ptr(self.cw),
                  ptr(self.train_index), self.train_index.numel(), ptr(self.prob), cp, ptr(self.loss[0:1]),
@@ -309,51 +313,44 @@ class TrainEngine:
                      ptr(self.val_index), self.val_index.numel(), 0, cp, ptr(self.loss[1:2]), 0, cp,
                      ptr(self.ws), self.ws_bytes, st)
 
-    def _act_bwd(self, dy, y, cols, tag):
-        with self._t(tag, 12.0 * self.N * cols):
-            call("pg_act_bwd", ptr(dy), dy.stride(0), ptr(y), y.stride(0), self.N, cols, LEAKY,
-                 LEAKY_SLOPE, self._s())
-
     def backward(self) -> None:
         st = self._s()
-        G, P = self.G, self.P
+        G, P, pd = self.G, self.P, self.pd
         g = self.dg.fwd.struct(self.ews)
         gt = self.dg.bwd.struct(None)
-        # liner2
+        h4, f3 = pd[-2], pd[-3]
+        # liner2: dW2_ext = dZ^T [A4 | 1]; dA4 = (dZ W2) * leaky'(A4)
         self._gemm(self.dZ, self.A4, G["liner2.W"], transa=True, tag="gemm.wgrad.liner2")
-        self._colsum(self.dZ, G["liner2.b"])
-        self._gemm(self.dZ, P["liner2.W"], self.dA4, tag="gemm.dgrad.liner2")
-        self._act_bwd(self.dA4, self.A4, self.dA4.shape[1], "act_bwd")
+        self._gemm(self.dZ, P["liner2.W"][:, :h4], self.dA4, act=LEAKY, dact=self.A4[:, :h4],
+                   tag="gemm.dgrad.liner2")
         # liner1
         self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, tag="gemm.wgrad.liner1")
-        self._colsum(self.dA4, G["liner1.b"])
-        self._gemm(self.dA4, P["liner1.W"], self.dA3, tag="gemm.dgrad.liner1")
-        self._act_bwd(self.dA3, self.A3, self.dA3.shape[1], "act_bwd")
+        self._gemm(self.dA4, P["liner1.W"][:, :f3], self.dA3, act=LEAKY, dact=self.A3[:, :f3],
+                   tag="gemm.dgrad.liner1")
         dY = self.dA3
         for l in reversed(range(self.L)):
             p = f"conv{l + 1}."
-            Fi = self.pd[l]
+            Fi = pd[l]
             HM, dHM = self.HM[l], self.dHM[l]
-            # weight / bias grads of Y = [H | M] Wcat^T + b
+            # d Wcat_ext = dY^T [H | 1 | M]  (the ones column gives d bias)
             self._gemm(dY, HM, G[p + "Wcat"], transa=True, tag=f"gemm.wgrad.cat.l{l + 1}")
-            self._colsum(dY, G[p + "b"])
-            # d[H | M] = dY Wcat   (layer 1: only dM is needed)
+            # d[H | . | M] = dY Wcat_ext   (layer 1: only dM is needed)
             if l > 0:
                 self._gemm(dY, P[p + "Wcat"], dHM, tag=f"gemm.dgrad.cat.l{l + 1}")
             else:
-                self._gemm(dY, P[p + "Wcat"][:, Fi:], dHM[:, Fi:], tag=f"gemm.dgrad.cat.l{l + 1}")
-            # max backward + relu' of fc_pool, fused
+                self._gemm(dY, P[p + "Wcat"][:, Fi + ONE:], dHM[:, Fi + ONE:], tag=f"gemm.dgrad.cat.l{l + 1}")
+            # max backward with relu' of fc_pool fused
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
+                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi + ONE:]),
                      dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(self.dP[l]), Fi, ptr(self.ws),
                      self.ws_bytes, st)
-            self._gemm(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, tag=f"gemm.wgrad.pool.l{l + 1}")
-            self._colsum(self.dP[l], G[p + "bpool"])
+            # d Wpool_ext = dP^T [H | 1]
+            self._gemm(self.dP[l], HM[:, :Fi + ONE], G[p + "Wpool"], transa=True, tag=f"gemm.wgrad.pool.l{l + 1}")
             if l > 0:
+                # dH = (dH_self + dP Wpool) * leaky'(H): H is the previous layer's output
                 dH = dHM[:, :Fi]
-                self._gemm(self.dP[l], P[p + "Wpool"], dH, beta=1.0, tag=f"gemm.dgrad.pool.l{l + 1}")
-                # through the previous layer's leaky_relu (its output is H = HM[:, :Fi])
-                self._act_bwd(dH, HM, Fi, "act_bwd")
+                self._gemm(self.dP[l], P[p + "Wpool"][:, :Fi], dH, beta=1.0, act=LEAKY, dact=HM[:, :Fi],
+                           tag=f"gemm.dgrad.pool.l{l + 1}")
                 dY = dH
 
     def adam(self) -> None:
@@ -401,7 +398,7 @@ class TrainEngine:
 
     def step(self) -> None:
         if self.graph is None:
-            self.step_eager(getattr(self, "allreduce", None))
+            self.step_eager(self.allreduce)
             return
         self.graph.replay()
         if self.graph_adam is not None:
@@ -430,16 +427,16 @@ class TrainEngine:
         return 4 * (N + 1) + 4 * E + 4 * F * E + 4 * F * N + a * F * N
 
     def spmm_bwd_bytes(self, layer: int) -> int:
-        """Algorithmic bytes of one deterministic max backward (gather form): transposed
-        CSR (4(N+1) + 8E': column + slot), the argmax row of each out-neighbour
-        (a*F*E'), the upstream gradient and the relu mask read once (8*F*N), dX written
-        once (4*F*N). The dout rows of non-matching features are not needed."""
+        """Algorithmic bytes of one max backward: the upstream gradient
+        and the argmax record read once (s*F*N + a*F*N), dX written once (s*F*N), plus
+        the fused relu mask (s*F*N) and the transposed CSR (4(N+1) + 8E')."""
         N, E, F = self.N, self.dg.num_edges, self.pd[layer]
         a = 2 if self.dg.arg_kind == _lib.PG_ARG_U16 else 4
-        return 4 * (N + 1) + 8 * E + a * F * E + 12 * F * N
+        return 4 * (N + 1) + 8 * E + (12 + a) * F * N
 
     def flops_per_step(self) -> int:
-        """Dense GEMM flops of one step (forward + backward, layer-1 input grad skipped)."""
+        """Dense GEMM flops of one step at the true (unpadded) dims, forward + backward
+        (layer-1 input gradient skipped, as autograd does for the constant features)."""
         N, d = self.N, self.dims
         f = 0
         for l in range(self.L):

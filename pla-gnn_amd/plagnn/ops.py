@@ -159,9 +159,11 @@ def _split_k(M: int, N: int, K: int) -> int:
 def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = False,
          out: Optional[torch.Tensor] = None, alpha: float = 1.0, beta: float = 0.0,
          bias: Optional[torch.Tensor] = None, act: int = _lib.PG_ACT_NONE,
-         slope: float = LEAKY_SLOPE, split_k: Optional[int] = None) -> torch.Tensor:
+         slope: float = LEAKY_SLOPE, split_k: Optional[int] = None,
+         dact: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = alpha*op(A)@op(B) + beta*C (+bias, act) on the fp32 MFMA kernel (GPU) or
-    torch-CPU (CPU device)."""
+    torch-CPU (CPU device). With `dact` (an activation output) the result is instead
+    multiplied by act'(dact): the fused activation backward."""
     M = A.shape[1] if transa else A.shape[0]
     K = A.shape[0] if transa else A.shape[1]
     Kb = B.shape[1] if transb else B.shape[0]
@@ -180,19 +182,22 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
             r = r + beta * out
         if bias is not None:
             r = r + bias
-        if act == _lib.PG_ACT_RELU:
+        if dact is not None:
+            r = torch.where(dact > 0, r, r * slope if act == _lib.PG_ACT_LEAKY else r * 0)
+        elif act == _lib.PG_ACT_RELU:
             r = torch.relu(r)
         elif act == _lib.PG_ACT_LEAKY:
             r = torch.nn.functional.leaky_relu(r, slope)
         out.copy_(r)
         return out
     if split_k is None:
-        split_k = 1 if (bias is not None or act != _lib.PG_ACT_NONE or beta not in (0.0, 1.0)) \
-            else _split_k(M, N, K)
+        split_k = 1 if (bias is not None or act != _lib.PG_ACT_NONE or dact is not None
+                        or beta not in (0.0, 1.0)) else _split_k(M, N, K)
     ws_n = _lib.lib().pg_gemm_f32_workspace(M, N, K, split_k)
     ws = _workspace(ws_n, A.device)
     call("pg_gemm_f32", int(transa), int(transb), M, N, K, alpha, ptr(A), _ld(A), ptr(B), _ld(B),
-         beta, ptr(out), _ld(out), ptr(bias), act, slope, split_k, ptr(ws), ws_n, _stream(A))
+         beta, ptr(out), _ld(out), ptr(bias), act, slope, ptr(dact),
+         _ld(dact) if dact is not None else 0, split_k, ptr(ws), ws_n, _stream(A))
     return out
 
 

@@ -11,8 +11,8 @@ from collections import defaultdict
 
 
 def short(name):
-    n = name.split("(")[0]
-    return n.replace("void ", "").replace("(anonymous namespace)::", "")
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0]
 
 
 def main():

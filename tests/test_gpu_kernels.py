@@ -252,3 +252,20 @@ def test_adam_matches_oracle_and_torch(oracle_mod):
         oracle_mod.adam_step_torch110([p_ref], [g], [m_ref], [v_ref], step, 5e-5)
     torch.testing.assert_close(pd.cpu(), p_ref, rtol=1e-6, atol=1e-9)
     assert st[0].item() == 7.0
+
+
+def test_gemm_fused_activation_backward():
+    """dact epilogue: (A @ B + beta*C) * act'(Y) with Y an activation output."""
+    from plagnn import _lib, ops
+
+    torch.manual_seed(1)
+    A = torch.randn(300, 96)
+    B = torch.randn(96, 40)
+    Y = torch.randn(300, 40)
+    C0 = torch.randn(300, 40)
+    for act, slope in ((_lib.PG_ACT_LEAKY, 0.01), (_lib.PG_ACT_RELU, 0.0)):
+        Cd = C0.to(DEV)
+        ops.gemm(A.to(DEV), B.to(DEV), out=Cd, beta=1.0, act=act, dact=Y.to(DEV))
+        full = A.double() @ B.double() + C0.double()
+        ref = torch.where(Y > 0, full, full * slope)
+        torch.testing.assert_close(Cd.cpu().double(), ref, rtol=1e-5, atol=1e-5)
