@@ -23,6 +23,9 @@
 // slabs summed in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
@@ -309,6 +312,19 @@ int launch_trans(bool ta, bool tb, bool va, bool vb, int epi, dim3 grid, hipStre
 // Tile choice: BN = 64 for narrow outputs, else 128; BM = 128 only when that still gives
 // at least ~3 workgroups per CU (256 CUs), so skinny-N products keep the chip filled.
 inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
+  // tuning knob PLAGNN_GEMM_TILE = "BMxBN" (64|128 each) forces a tile
+  static const int forced = [] {
+    const char* e = getenv("PLAGNN_GEMM_TILE");
+    if (!e) return 0;
+    int a = 0, b = 0;
+    if (sscanf(e, "%dx%d", &a, &b) != 2 || (a != 64 && a != 128) || (b != 64 && b != 128)) return 0;
+    return a * 1000 + b;
+  }();
+  if (forced) {
+    bm = forced / 1000;
+    bn = forced % 1000;
+    return;
+  }
   bn = N <= 64 ? 64 : 128;
   const int64_t tiles128 = ((M + 127) / 128) * ((N + bn - 1) / bn) * split;
   bm = tiles128 >= 3 * 256 ? 128 : 64;
