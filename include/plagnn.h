@@ -204,19 +204,29 @@ int pg_adam_apply(float* param, const float* grad, float* exp_avg, float* exp_av
                   const float* state, double beta1, double beta2, double eps,
                   double weight_decay, pg_stream_t stream);
 
-/* C[M,N] = alpha * op(A) * op(B) + beta * C, then epilogue: + bias[N] (row vector), act.
+/* Epilogue of pg_gemm_f32 (NULL = plain C = alpha * op(A) op(B) + beta * C). */
+typedef struct pg_gemm_epilogue {
+  const float* bias; /* [N] row vector added after alpha*AB + beta*C, or NULL */
+  int act;           /* PG_ACT_*: applied to the result, unless dact is given */
+  float slope;       /* negative slope of PG_ACT_LEAKY */
+  const float* dact; /* if not NULL: multiply the result by act'(dact[m][n]) instead, dact being
+                        the activation OUTPUT (relu: dact > 0 ? 1 : 0; leaky: dact > 0 ? 1 : slope)
+                        = the fused backward of relu / leaky_relu */
+  int64_t lddact;
+  float* rowsum;     /* if not NULL: rowsum[m] = sum_k op(A)[m][k] (overwritten). For a weight
+                        gradient dY^T X (transa) these are the bias gradients sum_nodes dY. */
+} pg_gemm_epilogue_t;
+
+/* C[M,N] = alpha * op(A) * op(B) + beta * C, then the epilogue.
  * op(A) = A (M x K, lda) or A^T when transa (A stored K x M); op(B) = B (K x N) or B^T when
- * transb (B stored N x K). fp32 in, fp32 accumulate on MFMA.
- * With dact != NULL the activation is not applied; instead the result is multiplied by the
- * derivative of `act` taken from the activation OUTPUT dact[M][N] (lddact): the fused
- * backward of relu / leaky_relu (relu: dact > 0 ? 1 : 0; leaky: dact > 0 ? 1 : slope).
- * When split_k > 1, beta must be 0 or 1 and no bias/act/dact is applied (partials are
- * combined in the workspace, in slice order). */
+ * transb (B stored N x K). fp32 in, fp32 accumulate on MFMA (v_mfma_f32_32x32x2_f32).
+ * When split_k > 1, beta must be 0 or 1 and the epilogue may only carry rowsum (partials
+ * are combined in the workspace, in slice order: deterministic). */
 size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k);
 int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
-                int64_t ldc, const float* bias, int act, float slope, const float* dact,
-                int64_t lddact, int split_k, void* ws, size_t ws_bytes, pg_stream_t stream);
+                int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
+                size_t ws_bytes, pg_stream_t stream);
 
 /* ---------------- host (_cpu): the same operations on host pointers ---------------- */
 int pg_spmm_max_fwd_cpu(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,

@@ -1,21 +1,29 @@
 // fp32 GEMM on the gfx950 matrix cores (v_mfma_f32_32x32x2_f32: exact f32 products,
-// f32 accumulate; gfx950 has no xf32 shortcut) with a fused epilogue
-// (alpha/beta, + bias row vector, relu / leaky_relu). Serves every nn.Linear of the
-// PLA-GNN step: SAGEConv's fc_pool / fc_self / fc_neigh (code/model.py:13-15) and
-// liner1 / liner2 (code/model.py:16-17), forward and backward.
+// f32 accumulate; gfx950 has no xf32 shortcut) with a fused epilogue. Serves every
+// nn.Linear of the PLA-GNN step: SAGEConv's fc_pool / fc_self / fc_neigh
+// (code/model.py:13-15) and liner1 / liner2 (code/model.py:16-17), forward and backward.
 //
-// Tiling: BM x BN per 256-thread workgroup (BM, BN in {64, 128}), K step 32; the four
+// Epilogue (pg_gemm_epilogue_t): + bias row vector, relu / leaky_relu, or the fused
+// activation backward (multiply by act'(y) of a given activation output y), and the row
+// sums of op(A) (for a weight-gradient GEMM dY^T X these are the bias gradients
+// sum_nodes dY, computed from the A tiles already staged in LDS).
+//
+// Tiling: BM x BN per 256-thread workgroup (BM, BN in {64, 128}), K step 64; the four
 // waves form a 2 x 2 grid, each owning (BM/2) x (BN/2) = TM x TN MFMA tiles of 32 x 32.
-// Global -> register prefetch of the next K tile overlaps the MFMAs of the current one.
+// Global -> register prefetch of the next K tile overlaps the MFMAs of the current one
+// (4096 MFMA cycles per wave per K step cover an HBM miss). Workgroups are ordered so the
+// column tiles of one row tile are consecutive on one XCD (`blockIdx % 8` group, the
+// bijective remap of cdna_hip_programming.md §5): the A rows they share stay in that
+// XCD's L2.
 // LDS layout follows the global layout so every staging store is a ds_write_b128:
-//   A not transposed (A[m][k]) -> As[m][k] (k contiguous, row stride 36 floats: the
-//   16-lane groups of ds_read_b128 hit 16 distinct 4-bank slots since 9 is odd);
+//   A not transposed (A[m][k]) -> As[m][k] (k contiguous, row stride BK+4 floats: the
+//   16-lane groups of ds_read_b128 hit 16 distinct 4-bank slots since 17 is odd);
 //   A transposed (A[k][m])     -> As[k][m] (m contiguous, read by ds_read_b32);
 //   the same for B with n in place of m.
 // K is consumed in a permuted order: at MFMA step s a lane of half h supplies
-// k = 16 h + s (not 2 s + h) for A and B alike, so one lane's 16 k-values are contiguous
-// in a [row][k] image (four ds_read_b128). Each MFMA still pairs A and B at equal k, so
-// the product is exact f32 with a fixed (permuted) summation order.
+// k = 32 h + s (not 2 s + h) for A and B alike, so one lane's k-values are contiguous in
+// a [row][k] image (ds_read_b128). Each MFMA still pairs A and B at equal k, so the
+// product is exact f32 with a fixed (permuted) summation order.
 // MFMA 32x32x2 f32 operand map (cdna_hip_programming.md §3): lane l holds
 // A[i = l & 31][kk = l >> 5] and B[kk = l >> 5][j = l & 31]; the accumulator holds
 // C[row = (r & 3) + 8 (r >> 2) + 4 (l >> 5)][col = l & 31] in register r.
@@ -30,7 +38,8 @@
 
 namespace {
 
-constexpr int BK = 32;
+constexpr int BK = 64;
+constexpr int HK = BK / 2;  // k-values per lane half per K step
 constexpr int kThreads = 256;
 constexpr int KPAD = BK + 4;  // [row][k] image row stride (floats)
 
@@ -53,8 +62,9 @@ __device__ __forceinline__ float epi_apply(float x, float y, float slope) {
 // rows [r0, r0+ROWS) x k [k0, k0+BK), zero outside [0,R) x [0,kz1). 4 floats per unit.
 template <int ROWS, bool KMAJ, bool VEC>
 struct TileLoader {
-  static constexpr int UNITS = ROWS * BK / 4;          // float4 units per tile
-  static constexpr int PER = UNITS / kThreads;         // per thread (1, 2 or 4)
+  static constexpr int UNITS = ROWS * BK / 4;   // float4 units per tile
+  static constexpr int PER = UNITS / kThreads;  // per thread
+  static constexpr int UPR = BK / 4;            // units per [row][k] row
   float r[PER][4];
 
   __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int r0, int R,
@@ -63,10 +73,10 @@ struct TileLoader {
     for (int i = 0; i < PER; ++i) {
       const int q = tid + i * kThreads;
       int row, k;
-      if constexpr (!KMAJ) {  // [row][k]: 8 units per row
-        row = q >> 3;
-        k = (q & 7) << 2;
-      } else {  // [k][row]: ROWS/4 units per k
+      if constexpr (!KMAJ) {
+        row = q / UPR;
+        k = (q % UPR) << 2;
+      } else {
         k = q / (ROWS / 4);
         row = (q % (ROWS / 4)) << 2;
       }
@@ -110,7 +120,7 @@ struct TileLoader {
       const int q = tid + i * kThreads;
       float* d;
       if constexpr (!KMAJ) {
-        d = S + (q >> 3) * KPAD + ((q & 7) << 2);
+        d = S + (q / UPR) * KPAD + ((q % UPR) << 2);
       } else {
         d = S + (q / (ROWS / 4)) * (ROWS + 4) + ((q % (ROWS / 4)) << 2);
       }
@@ -124,12 +134,13 @@ constexpr int image_floats() {
   return KMAJ ? BK * (ROWS + 4) : ROWS * KPAD;
 }
 
-// Fragment of 16 k-values for MFMA row/col `rc` of lane half h from an LDS image.
+// 16 k-values (chunk c of lane half h) for MFMA row/col `rc` from an LDS image.
 template <int ROWS, bool KMAJ>
-__device__ __forceinline__ void read_frag(const float* __restrict__ S, int rc, int h,
+__device__ __forceinline__ void read_frag(const float* __restrict__ S, int rc, int h, int c,
                                           float (&f)[16]) {
+  const int kb = h * HK + c * 16;
   if constexpr (!KMAJ) {
-    const float4* p = reinterpret_cast<const float4*>(S + rc * KPAD + h * 16);
+    const float4* p = reinterpret_cast<const float4*>(S + rc * KPAD + kb);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float4 t = p[q];
@@ -137,34 +148,60 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ S, int rc, i
     }
   } else {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) f[s] = S[(h * 16 + s) * (ROWS + 4) + rc];
+    for (int s = 0; s < 16; ++s) f[s] = S[(kb + s) * (ROWS + 4) + rc];
   }
+}
+
+// Row sums of the A tile in LDS over its BK k-values: thread t owns row t % BM and the
+// k-values k = t / BM, t / BM + G, ... (G = 256 / BM groups).
+template <int BM, bool AK>
+__device__ __forceinline__ float tile_rowsum(const float* __restrict__ As, int tid) {
+  constexpr int G = kThreads / BM;
+  const int m = tid % BM, g = tid / BM;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < BK / G; ++i) {
+    const int k = g + i * G;
+    s += AK ? As[k * (BM + 4) + m] : As[m * KPAD + k];
+  }
+  return s;
 }
 
 // TA: A stored K x M (use A^T). TB: B stored N x K (use B^T).
 template <int BM, int BN, bool TA, bool TB, bool VA, bool VB, int EPI>
 __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
-    int M, int N, int K, int k_per_split, float alpha, const float* __restrict__ A, int64_t lda,
-    const float* __restrict__ B, int64_t ldb, float beta, float* __restrict__ C, int64_t ldc,
-    const float* __restrict__ bias, float slope, const float* __restrict__ dact, int64_t lddact,
-    float* __restrict__ ws) {
+    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
+    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
+    const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
+    float* __restrict__ ws, float* __restrict__ ws_rowsum) {
   constexpr bool SPLIT = EPI == EPI_SPLIT;
   constexpr bool AK = TA;    // A image k-major ([k][m]) when A is stored transposed
   constexpr bool BKM = !TB;  // B image k-major ([k][n]) when B is stored K x N
   constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
   __shared__ __attribute__((aligned(16))) float As[image_floats<BM, AK>()];
   __shared__ __attribute__((aligned(16))) float Bs[image_floats<BN, BKM>()];
+  __shared__ float rsred[kThreads];
+
+  // XCD-aware tile order: blocks b, b+8, ... share an XCD; give each such group a
+  // contiguous run of tile ids (row-major over [tile_m][tile_n]).
+  const int b = blockIdx.x;
+  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
+  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * BM;
-  const int n0 = blockIdx.x * BN;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
   const int kz0 = blockIdx.z * k_per_split;
   const int kz1 = min(K, kz0 + k_per_split);
   const int h = lane >> 5;
   const int l32 = lane & 31;
+  const bool do_rs = rowsum != nullptr && tn == 0;
+  float rs = 0.f;
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -189,24 +226,40 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
         la.load(A, lda, m0, M, k0 + BK, kz1, tid);
         lb.load(B, ldb, n0, N, k0 + BK, kz1, tid);
       }
-      float fa[TM][16], fb[TN][16];
+      if (do_rs) rs += tile_rowsum<BM, AK>(As, tid);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) read_frag<BM, AK>(As, wm * (BM / 2) + i * 32 + l32, h, fa[i]);
+      for (int c = 0; c < HK / 16; ++c) {
+        float fa[TM][16], fb[TN][16];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) read_frag<BN, BKM>(Bs, wn * (BN / 2) + j * 32 + l32, h, fb[j]);
+        for (int i = 0; i < TM; ++i) read_frag<BM, AK>(As, wm * (BM / 2) + i * 32 + l32, h, c, fa[i]);
 #pragma unroll
-      for (int s = 0; s < 16; ++s)
+        for (int j = 0; j < TN; ++j) read_frag<BN, BKM>(Bs, wn * (BN / 2) + j * 32 + l32, h, c, fb[j]);
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int s = 0; s < 16; ++s)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+      }
       __syncthreads();
       if (more) {
         la.store(As, tid);
         lb.store(Bs, tid);
         __syncthreads();
       }
+    }
+  }
+
+  // row sums of op(A): combine the k-groups in order, one value per row of the tile
+  if (do_rs) {
+    rsred[tid] = rs;
+    __syncthreads();
+    if (tid < BM && m0 + tid < M) {
+      float t = 0.f;
+      for (int g = 0; g < kThreads / BM; ++g) t += rsred[g * BM + tid];
+      if constexpr (SPLIT) ws_rowsum[(int64_t)blockIdx.z * M + m0 + tid] = t;
+      else rowsum[m0 + tid] = t;
     }
   }
 
@@ -237,13 +290,23 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
   }
 }
 
-// Split-K combine: C = alpha * sum_z ws[z] (+ beta * C), slices summed in order.
+// Split-K combine: C = alpha * sum_z ws[z] (+ beta * C), slices summed in order; the row
+// sums likewise (their slices follow the partial slabs in the workspace).
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws,
                                                             int splits, int M, int N, float alpha,
                                                             float beta, float* __restrict__ C,
-                                                            int64_t ldc) {
+                                                            int64_t ldc, const float* __restrict__ ws_rowsum,
+                                                            float* __restrict__ rowsum) {
   const int64_t n = (int64_t)M * N;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n + (rowsum ? M : 0);
+       i += (int64_t)gridDim.x * 256) {
+    if (i >= n) {
+      const int m = (int)(i - n);
+      float s = 0.f;
+      for (int z = 0; z < splits; ++z) s += ws_rowsum[(int64_t)z * M + m];
+      rowsum[m] = s;
+      continue;
+    }
     float s = 0.f;
     for (int z = 0; z < splits; ++z) s += ws[(int64_t)z * n + i];
     const int64_t r = i / N;
@@ -257,7 +320,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 struct Args {
-  int M, N, K, kps;
+  int M, N, K, kps, tiles_n, tiles;
   float alpha;
   const float* A;
   int64_t lda;
@@ -270,15 +333,18 @@ struct Args {
   float slope;
   const float* dact;
   int64_t lddact;
+  float* rowsum;
   float* ws;
+  float* ws_rowsum;
 };
 
 template <int BM, int BN, bool TA, bool TB, bool VA, bool VB>
 int launch_epi(int epi, dim3 grid, hipStream_t st, const Args& a) {
 #define PG_L(EPI_)                                                                          \
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, VA, VB, EPI_>), grid, dim3(kThreads), 0, \
-                     st, a.M, a.N, a.K, a.kps, a.alpha, a.A, a.lda, a.B, a.ldb, a.beta, a.C,  \
-                     a.ldc, a.bias, a.slope, a.dact, a.lddact, a.ws)
+                     st, a.M, a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B,  \
+                     a.ldb, a.beta, a.C, a.ldc, a.bias, a.slope, a.dact, a.lddact, a.rowsum,  \
+                     a.ws, a.ws_rowsum)
   switch (epi) {
     case EPI_NONE: PG_L(EPI_NONE); break;
     case EPI_RELU: PG_L(EPI_RELU); break;
@@ -309,8 +375,9 @@ int launch_trans(bool ta, bool tb, bool va, bool vb, int epi, dim3 grid, hipStre
   return launch_vec<BM, BN, true, true>(va, vb, epi, grid, st, a);
 }
 
-// Tile choice: BN = 64 for narrow outputs, else 128; BM = 128 only when that still gives
-// at least ~3 workgroups per CU (256 CUs), so skinny-N products keep the chip filled.
+// Tile choice: BN = 64 for outputs up to 128 columns wide, else 128; BM = 128 only when
+// that still gives at least ~3 workgroups per CU (256 CUs), so skinny-N products keep the
+// chip filled.
 inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
   // tuning knob PLAGNN_GEMM_TILE = "BMxBN" (64|128 each) forces a tile
   static const int forced = [] {
@@ -325,7 +392,7 @@ inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
     bn = forced % 1000;
     return;
   }
-  bn = N <= 64 ? 64 : 128;
+  bn = N <= 128 ? 64 : 128;
   const int64_t tiles128 = ((M + 127) / 128) * ((N + bn - 1) / bn) * split;
   bm = tiles128 >= 3 * 256 ? 128 : 64;
 }
@@ -337,13 +404,16 @@ extern "C" {
 size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k) {
   (void)K;
   if (split_k <= 1 || M <= 0 || N <= 0) return 0;
-  return (size_t)split_k * (size_t)M * (size_t)N * 4;
+  return (size_t)split_k * (size_t)M * (size_t)(N + 1) * 4;
 }
 
 int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
-                int64_t ldc, const float* bias, int act, float slope, const float* dact,
-                int64_t lddact, int split_k, void* ws, size_t ws_bytes, pg_stream_t stream) {
+                int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
+                size_t ws_bytes, pg_stream_t stream) {
+  const pg_gemm_epilogue_t none{nullptr, PG_ACT_NONE, 0.f, nullptr, 0, nullptr};
+  if (!ep) ep = &none;
+  const int act = ep->act;
   if (M < 0 || N < 0 || K < 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
     return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32: bad sizes");
   if (ldc < N || (!transa && lda < K) || (transa && lda < M) || (!transb && ldb < N) ||
@@ -352,9 +422,9 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   if (act != PG_ACT_NONE && act != PG_ACT_RELU && act != PG_ACT_LEAKY)
     return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32: bad act %d", act);
   if (split_k < 1) split_k = 1;
-  if (split_k > 1 && (bias || act != PG_ACT_NONE || dact || (beta != 0.f && beta != 1.f)))
+  if (split_k > 1 && (ep->bias || act != PG_ACT_NONE || ep->dact || (beta != 0.f && beta != 1.f)))
     return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32: split_k > 1 takes no bias/act, beta 0|1");
-  if (dact && (act == PG_ACT_NONE || lddact < N))
+  if (ep->dact && (act == PG_ACT_NONE || ep->lddact < N))
     return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32: dact needs act relu|leaky and lddact >= N");
   if (M == 0 || N == 0) return pg::ok();
   if (split_k > 1 && ws_bytes < pg_gemm_f32_workspace(M, N, K, split_k))
@@ -373,14 +443,18 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   const bool split = split_k > 1;
   int bm, bn;
   pick_tile(M, N, split_k, bm, bn);
-  dim3 grid((unsigned)((N + bn - 1) / bn), (unsigned)((M + bm - 1) / bm), (unsigned)split_k);
+  const int tiles_n = (int)((N + bn - 1) / bn);
+  const int tiles = tiles_n * (int)((M + bm - 1) / bm);
+  dim3 grid((unsigned)tiles, 1, (unsigned)split_k);
   hipStream_t st = (hipStream_t)stream;
-  const Args a{(int)M, (int)N, (int)K, kps, alpha, A, lda, B, ldb, beta, C, ldc, bias, slope,
-               dact, lddact, split ? (float*)ws : nullptr};
+  float* wsf = split ? (float*)ws : nullptr;
+  const Args a{(int)M, (int)N, (int)K, kps, tiles_n, tiles, alpha, A, lda, B, ldb, beta, C, ldc,
+               ep->bias, ep->slope, ep->dact, ep->lddact, ep->rowsum, wsf,
+               split ? wsf + (int64_t)split_k * M * N : nullptr};
   const bool ta = transa != 0, tb = transb != 0;
   const int epi = split ? EPI_SPLIT
-                        : dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
-                               : (act == PG_ACT_RELU ? EPI_RELU : act == PG_ACT_LEAKY ? EPI_LEAKY : EPI_NONE);
+                        : ep->dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
+                                   : (act == PG_ACT_RELU ? EPI_RELU : act == PG_ACT_LEAKY ? EPI_LEAKY : EPI_NONE);
   int rc;
   if (bm == 128 && bn == 128)
     rc = launch_trans<128, 128>(ta, tb, va, vb, epi, grid, st, a);
@@ -392,10 +466,11 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
     rc = launch_trans<64, 64>(ta, tb, va, vb, epi, grid, st, a);
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_f32: dispatch failed");
   if (split) {
-    const int64_t n = M * N;
+    const int64_t n = M * N + (ep->rowsum ? M : 0);
     const int blocks = (int)std::min<int64_t>(4096, (n + 255) / 256);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws,
-                       split_k, (int)M, (int)N, alpha, beta, C, ldc);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)wsf,
+                       split_k, (int)M, (int)N, alpha, beta, C, ldc, (const float*)a.ws_rowsum,
+                       ep->rowsum);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess)

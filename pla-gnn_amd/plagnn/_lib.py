@@ -43,6 +43,19 @@ class PgCsr(ctypes.Structure):
     ]
 
 
+class PgGemmEpilogue(ctypes.Structure):
+    """pg_gemm_epilogue_t (include/plagnn.h)."""
+
+    _fields_ = [
+        ("bias", ctypes.c_void_p),
+        ("act", ctypes.c_int),
+        ("slope", ctypes.c_float),
+        ("dact", ctypes.c_void_p),
+        ("lddact", ctypes.c_int64),
+        ("rowsum", ctypes.c_void_p),
+    ]
+
+
 _i = ctypes.c_int
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
@@ -51,6 +64,7 @@ _d = ctypes.c_double
 _sz = ctypes.c_size_t
 _vp = ctypes.c_void_p
 _csr = ctypes.POINTER(PgCsr)
+_ep = ctypes.POINTER(PgGemmEpilogue)
 
 # name -> (restype, argtypes); every symbol of include/plagnn.h
 SIGNATURES = {
@@ -77,8 +91,8 @@ SIGNATURES = {
     "pg_adam_prepare": (_i, [_vp, _d, _d, _d, _vp]),
     "pg_adam_apply": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _d, _d, _d, _d, _vp]),
     "pg_gemm_f32_workspace": (_sz, [_i64, _i64, _i64, _i]),
-    "pg_gemm_f32": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _vp,
-                         _i, _f, _vp, _i64, _i, _vp, _sz, _vp]),
+    "pg_gemm_f32": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _ep,
+                         _i, _vp, _sz, _vp]),
     "pg_spmm_max_fwd_cpu": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i]),
     "pg_spmm_max_bwd_cpu": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64]),
     "pg_spmm_sum_cpu": (_i, [_csr, _vp, _i64, _i64, _i, _vp, _vp, _i64]),
@@ -124,6 +138,18 @@ def call(name: str, *args) -> None:
 def stream_handle(device: torch.device):
     """hipStream_t of torch's current stream on `device` (as an int for ctypes)."""
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def epilogue(bias=None, act: int = PG_ACT_NONE, slope: float = 0.01, dact=None, rowsum=None):
+    """pg_gemm_epilogue_t from tensors (or None)."""
+    e = PgGemmEpilogue()
+    e.bias = ptr(bias)
+    e.act = act
+    e.slope = slope
+    e.dact = ptr(dact)
+    e.lddact = dact.stride(0) if dact is not None else 0
+    e.rowsum = ptr(rowsum)
+    return e
 
 
 def ptr(t) -> int:

@@ -10,22 +10,17 @@ whole step is captured once into a HIP graph (torch.cuda.CUDAGraph) and replayed
 
 Layout in HBM (fp32, row-major; every width padded to a multiple of 4 with zero pads that
 stay exactly zero through forward, backward and Adam):
-  * Bias as a column. Every layer input carries a constant block [1 0 0 0] after its
-    features, and every weight matrix carries its bias in the matching column, so
-    x @ W_ext^T = x @ W^T + b is one GEMM, and the weight-gradient GEMM dY^T @ [x | 1]
-    yields the bias gradient (sum of dY over nodes) as its extra column: no bias
-    epilogue and no separate column-sum kernel.
-  * SAGE layer l (Fi -> Fo): HM_l[N][2Fi + 4] = [H_l | 1 0 0 0 | M_l] — the layer input
-    H_l (written there by the previous layer's GEMM epilogue), the ones block, and the
-    max-aggregated neighbourhood M_l (written there by the SpMM). Parameters
-    Wpool_ext[Fi][Fi + 4] = [Wpool | bpool 0 0 0] (reads HM[:, :Fi + 4]) and
-    Wcat_ext[Fo][2Fi + 4] = [Wself | b 0 0 0 | Wneigh] (reads all of HM): fc_self +
-    fc_neigh + bias is ONE K = 2Fi + 4 GEMM. P_l[N][Fi] = relu(fc_pool), argpos_l[N][Fi]
-    (u16 winning in-row positions).
+  * SAGE layer l (Fi -> Fo): HM_l[N][2Fi] = [H_l | M_l] — the layer input H_l (written
+    there by the previous layer's GEMM epilogue) beside the max-aggregated neighbourhood
+    M_l (written there by the SpMM); parameters Wpool[Fi][Fi], bpool[Fi],
+    Wcat[Fo][2Fi] = [Wself | Wneigh], b[Fo]: fc_self + fc_neigh + bias is ONE K = 2Fi GEMM
+    over HM. P_l[N][Fi] = relu(fc_pool), argpos_l[N][Fi] (u16 winning in-row positions).
   * All parameters live in ONE flat buffer (Adam is one launch; a multi-GPU all-reduce is
     one bucket), gradients in a second one with the same layout.
-  * Activation backward (leaky_relu') is fused into the epilogue of the GEMM producing
-    the gradient (pg_gemm_f32 with dact), relu' of fc_pool into the SpMM backward.
+  * Fusions: bias + relu / leaky_relu in the forward GEMM epilogues; leaky_relu' in the
+    epilogue of the GEMM producing each activation gradient; the bias gradients
+    (sum of dY over nodes) as row sums of the weight-gradient GEMM's A operand; relu' of
+    fc_pool inside the SpMM backward.
 """
 from __future__ import annotations
 
@@ -42,7 +37,6 @@ from .graph import CSRGraph, DeviceGraph
 from .ops import LEAKY_SLOPE, round4
 
 RELU, LEAKY, NONE = _lib.PG_ACT_RELU, _lib.PG_ACT_LEAKY, _lib.PG_ACT_NONE
-ONE = 4  # width of the constant [1 0 0 0] block that carries the bias
 
 
 class _Flat:
@@ -88,14 +82,18 @@ class TrainEngine:
         pd = [round4(d) for d in self.dims]
         self.pd = pd
 
-        # ---- parameters (flat, padded, bias as a column) ----
+        # ---- parameters (flat, padded) ----
         fl = _Flat()
         for l in range(self.L):
             Fi, Fo = pd[l], pd[l + 1]
-            fl.add(f"conv{l + 1}.Wpool", (Fi, Fi + ONE))
-            fl.add(f"conv{l + 1}.Wcat", (Fo, 2 * Fi + ONE))
-        fl.add("liner1.W", (pd[-2], pd[-3] + ONE))
-        fl.add("liner2.W", (pd[-1], pd[-2] + ONE))
+            fl.add(f"conv{l + 1}.Wpool", (Fi, Fi))
+            fl.add(f"conv{l + 1}.bpool", (Fi,))
+            fl.add(f"conv{l + 1}.Wcat", (Fo, 2 * Fi))
+            fl.add(f"conv{l + 1}.b", (Fo,))
+        fl.add("liner1.W", (pd[-2], pd[-3]))
+        fl.add("liner1.b", (pd[-2],))
+        fl.add("liner2.W", (pd[-1], pd[-2]))
+        fl.add("liner2.b", (pd[-1],))
         self.flat_layout = fl
         self.flat = torch.zeros(fl.size, dtype=torch.float32, device=dev)
         self.gflat = torch.zeros_like(self.flat)
@@ -127,21 +125,17 @@ class TrainEngine:
         self.val_index = None if val_index is None else torch.as_tensor(
             np.asarray(val_index, np.int32), device=dev)
 
-        # ---- activations (ones blocks set once; nothing else ever writes them) ----
+        # ---- activations ----
         f32 = dict(dtype=torch.float32, device=dev)
         self.HM, self.Pl, self.arg = [], [], []
         for l in range(self.L):
             Fi = pd[l]
-            hm = torch.zeros(N, 2 * Fi + ONE, **f32)
-            hm[:, Fi] = 1.0
-            self.HM.append(hm)
+            self.HM.append(torch.zeros(N, 2 * Fi, **f32))
             self.Pl.append(torch.zeros(N, Fi, **f32))
             self.arg.append(torch.zeros(N, Fi, dtype=self.dg.arg_dtype, device=dev))
         self.HM[0][:, :self.dims[0]] = features.to(dev, torch.float32)
-        self.A3 = torch.zeros(N, pd[-3] + ONE, **f32)
-        self.A3[:, pd[-3]] = 1.0
-        self.A4 = torch.zeros(N, pd[-2] + ONE, **f32)
-        self.A4[:, pd[-2]] = 1.0
+        self.A3 = torch.zeros(N, pd[-3], **f32)
+        self.A4 = torch.zeros(N, pd[-2], **f32)
         self.Z = torch.zeros(N, pd[-1], **f32)
         self.prob = torch.zeros(N, pd[-1], **f32)
         self.loss = torch.zeros(2, **f32)  # [train, val]
@@ -149,7 +143,7 @@ class TrainEngine:
         self.dZ = torch.zeros(N, pd[-1], **f32)
         self.dA4 = torch.zeros(N, pd[-2], **f32)
         self.dA3 = torch.zeros(N, pd[-3], **f32)
-        self.dHM = [torch.zeros(N, 2 * pd[l] + ONE, **f32) for l in range(self.L)]
+        self.dHM = [torch.zeros(N, 2 * pd[l], **f32) for l in range(self.L)]
         self.dP = [torch.zeros(N, pd[l], **f32) for l in range(self.L)]
 
         # ---- workspace (one buffer, sized for the largest call) ----
@@ -179,8 +173,8 @@ class TrainEngine:
         out = []
         for l in range(self.L):
             Fi, Fo = pd[l], pd[l + 1]
-            out += [(Fo, 2 * Fi + ONE, N), (Fi, Fi + ONE, N)]
-        out += [(pd[-2], pd[-3] + ONE, N), (pd[-1], pd[-2] + ONE, N)]
+            out += [(Fo, 2 * Fi, N), (Fi, Fi, N)]
+        out += [(pd[-2], pd[-3], N), (pd[-1], pd[-2], N)]
         return out
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
@@ -190,35 +184,33 @@ class TrainEngine:
             for l in range(self.L):
                 p = f"conv{l + 1}."
                 fi, fo, Fi = self.dims[l], self.dims[l + 1], self.pd[l]
-                Wp, Wc = self.P[p + "Wpool"], self.P[p + "Wcat"]
-                Wp[:fi, :fi] = sd[p + "fc_pool.weight"]
-                Wp[:fi, Fi] = sd[p + "fc_pool.bias"]
-                Wc[:fo, :fi] = sd[p + "fc_self.weight"]
+                self.P[p + "Wpool"][:fi, :fi] = sd[p + "fc_pool.weight"]
+                self.P[p + "bpool"][:fi] = sd[p + "fc_pool.bias"]
+                self.P[p + "Wcat"][:fo, :fi] = sd[p + "fc_self.weight"]
+                self.P[p + "Wcat"][:fo, Fi:Fi + fi] = sd[p + "fc_neigh.weight"]
                 if sd.get(p + "bias") is not None:
-                    Wc[:fo, Fi] = sd[p + "bias"]
-                Wc[:fo, Fi + ONE:Fi + ONE + fi] = sd[p + "fc_neigh.weight"]
-            d, pd = self.dims, self.pd
+                    self.P[p + "b"][:fo] = sd[p + "bias"]
+            d = self.dims
             self.P["liner1.W"][:d[-2], :d[-3]] = sd["liner1.weight"]
-            self.P["liner1.W"][:d[-2], pd[-3]] = sd["liner1.bias"]
+            self.P["liner1.b"][:d[-2]] = sd["liner1.bias"]
             self.P["liner2.W"][:d[-1], :d[-2]] = sd["liner2.weight"]
-            self.P["liner2.W"][:d[-1], pd[-2]] = sd["liner2.bias"]
+            self.P["liner2.b"][:d[-1]] = sd["liner2.bias"]
 
     def _unpad(self, views: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         out = {}
         for l in range(self.L):
             p = f"conv{l + 1}."
             fi, fo, Fi = self.dims[l], self.dims[l + 1], self.pd[l]
-            Wp, Wc = views[p + "Wpool"], views[p + "Wcat"]
-            out[p + "fc_pool.weight"] = Wp[:fi, :fi].clone()
-            out[p + "fc_pool.bias"] = Wp[:fi, Fi].clone()
-            out[p + "fc_neigh.weight"] = Wc[:fo, Fi + ONE:Fi + ONE + fi].clone()
-            out[p + "fc_self.weight"] = Wc[:fo, :fi].clone()
-            out[p + "bias"] = Wc[:fo, Fi].clone()
-        d, pd = self.dims, self.pd
+            out[p + "fc_pool.weight"] = views[p + "Wpool"][:fi, :fi].clone()
+            out[p + "fc_pool.bias"] = views[p + "bpool"][:fi].clone()
+            out[p + "fc_neigh.weight"] = views[p + "Wcat"][:fo, Fi:Fi + fi].clone()
+            out[p + "fc_self.weight"] = views[p + "Wcat"][:fo, :fi].clone()
+            out[p + "bias"] = views[p + "b"][:fo].clone()
+        d = self.dims
         out["liner1.weight"] = views["liner1.W"][:d[-2], :d[-3]].clone()
-        out["liner1.bias"] = views["liner1.W"][:d[-2], pd[-3]].clone()
+        out["liner1.bias"] = views["liner1.b"][:d[-2]].clone()
         out["liner2.weight"] = views["liner2.W"][:d[-1], :d[-2]].clone()
-        out["liner2.bias"] = views["liner2.W"][:d[-1], pd[-2]].clone()
+        out["liner2.bias"] = views["liner2.b"][:d[-1]].clone()
         return out
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
@@ -268,40 +260,42 @@ class TrainEngine:
     def _s(self):
         return _lib.stream_handle(self.device)
 
-    def _gemm(self, A, B, C, transa=False, transb=False, beta=0.0, act=NONE, dact=None, tag="gemm"):
+    def _gemm(self, A, B, C, transa=False, transb=False, beta=0.0, bias=None, act=NONE, dact=None,
+              rowsum=None, tag="gemm"):
         M = A.shape[1] if transa else A.shape[0]
         K = A.shape[0] if transa else A.shape[1]
         N = B.shape[0] if transb else B.shape[1]
-        sk = self._gemm_plans.get((M, N, K), 1) if (act == NONE and dact is None) else 1
+        sk = self._gemm_plans.get((M, N, K), 1) if (bias is None and act == NONE and dact is None) else 1
+        ep = _lib.epilogue(bias, act, LEAKY_SLOPE, dact, rowsum)
         with self._t(tag, 2.0 * M * N * K):
             call("pg_gemm_f32", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
-                 B.stride(0), beta, ptr(C), C.stride(0), 0, act, LEAKY_SLOPE, ptr(dact),
-                 dact.stride(0) if dact is not None else 0, sk, ptr(self.ws), self.ws_bytes, self._s())
+                 B.stride(0), beta, ptr(C), C.stride(0), ep, sk, ptr(self.ws), self.ws_bytes, self._s())
 
     def forward(self) -> None:
         """Logits (self.prob) and both losses; dZ = d train_loss / d z."""
         st = self._s()
         g = self.dg.fwd.struct(self.ews)
+        P, pd = self.P, self.pd
         for l in range(self.L):
             p = f"conv{l + 1}."
-            Fi = self.pd[l]
+            Fi = pd[l]
             HM = self.HM[l]
-            # P = relu([H | 1] Wpool_ext^T)
-            self._gemm(HM[:, :Fi + ONE], self.P[p + "Wpool"], self.Pl[l], transb=True, act=RELU,
+            # P = relu(H Wpool^T + bpool)
+            self._gemm(HM[:, :Fi], P[p + "Wpool"], self.Pl[l], transb=True, bias=P[p + "bpool"], act=RELU,
                        tag=f"gemm.fwd.pool.l{l + 1}")
-            # M = max-aggregate(P) -> right block of HM
-            M = HM[:, Fi + ONE:]
+            # M = max-aggregate(P) -> right half of HM
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
-                call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(M), HM.stride(0), ptr(self.arg[l]),
-                     Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
-            # Y = [H | 1 | M] Wcat_ext^T (fc_self + fc_neigh + bias), leaky_relu -> next input
-            Fo = self.pd[l + 1]
-            out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3[:, :Fo]
-            self._gemm(HM, self.P[p + "Wcat"], out, transb=True, act=LEAKY, tag=f"gemm.fwd.cat.l{l + 1}")
-        pd = self.pd
-        self._gemm(self.A3, self.P["liner1.W"], self.A4[:, :pd[-2]], transb=True, act=LEAKY,
+                call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
+                     ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
+            # Y = [H | M] Wcat^T + b (fc_self + fc_neigh + bias), leaky_relu -> next input
+            Fo = pd[l + 1]
+            out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
+            self._gemm(HM, P[p + "Wcat"], out, transb=True, bias=P[p + "b"], act=LEAKY,
+                       tag=f"gemm.fwd.cat.l{l + 1}")
+        self._gemm(self.A3, P["liner1.W"], self.A4, transb=True, bias=P["liner1.b"], act=LEAKY,
                    tag="gemm.fwd.liner1")
-        self._gemm(self.A4, self.P["liner2.W"], self.Z, transb=True, act=NONE, tag="gemm.fwd.liner2")
+        self._gemm(self.A4, P["liner2.W"], self.Z, transb=True, bias=P["liner2.b"], act=NONE,
+                   tag="gemm.fwd.liner2")
         C = self.C
         cp = pd[-1]
         with self._t("loss"):
@@ -318,38 +312,36 @@ class TrainEngine:
         G, P, pd = self.G, self.P, self.pd
         g = self.dg.fwd.struct(self.ews)
         gt = self.dg.bwd.struct(None)
-        h4, f3 = pd[-2], pd[-3]
-        # liner2: dW2_ext = dZ^T [A4 | 1]; dA4 = (dZ W2) * leaky'(A4)
-        self._gemm(self.dZ, self.A4, G["liner2.W"], transa=True, tag="gemm.wgrad.liner2")
-        self._gemm(self.dZ, P["liner2.W"][:, :h4], self.dA4, act=LEAKY, dact=self.A4[:, :h4],
-                   tag="gemm.dgrad.liner2")
+        # liner2: dW2 = dZ^T A4 (+ db2 = row sums of dZ^T); dA4 = (dZ W2) * leaky'(A4)
+        self._gemm(self.dZ, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
+        self._gemm(self.dZ, P["liner2.W"], self.dA4, act=LEAKY, dact=self.A4, tag="gemm.dgrad.liner2")
         # liner1
-        self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, tag="gemm.wgrad.liner1")
-        self._gemm(self.dA4, P["liner1.W"][:, :f3], self.dA3, act=LEAKY, dact=self.A3[:, :f3],
-                   tag="gemm.dgrad.liner1")
+        self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
+        self._gemm(self.dA4, P["liner1.W"], self.dA3, act=LEAKY, dact=self.A3, tag="gemm.dgrad.liner1")
         dY = self.dA3
         for l in reversed(range(self.L)):
             p = f"conv{l + 1}."
             Fi = pd[l]
             HM, dHM = self.HM[l], self.dHM[l]
-            # d Wcat_ext = dY^T [H | 1 | M]  (the ones column gives d bias)
-            self._gemm(dY, HM, G[p + "Wcat"], transa=True, tag=f"gemm.wgrad.cat.l{l + 1}")
-            # d[H | . | M] = dY Wcat_ext   (layer 1: only dM is needed)
+            # d Wcat = dY^T [H | M], d b = sum_nodes dY
+            self._gemm(dY, HM, G[p + "Wcat"], transa=True, rowsum=G[p + "b"], tag=f"gemm.wgrad.cat.l{l + 1}")
+            # d[H | M] = dY Wcat   (layer 1: only dM is needed)
             if l > 0:
                 self._gemm(dY, P[p + "Wcat"], dHM, tag=f"gemm.dgrad.cat.l{l + 1}")
             else:
-                self._gemm(dY, P[p + "Wcat"][:, Fi + ONE:], dHM[:, Fi + ONE:], tag=f"gemm.dgrad.cat.l{l + 1}")
+                self._gemm(dY, P[p + "Wcat"][:, Fi:], dHM[:, Fi:], tag=f"gemm.dgrad.cat.l{l + 1}")
             # max backward with relu' of fc_pool fused
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi + ONE:]),
+                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
                      dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(self.dP[l]), Fi, ptr(self.ws),
                      self.ws_bytes, st)
-            # d Wpool_ext = dP^T [H | 1]
-            self._gemm(self.dP[l], HM[:, :Fi + ONE], G[p + "Wpool"], transa=True, tag=f"gemm.wgrad.pool.l{l + 1}")
+            # d Wpool = dP^T H, d bpool = sum_nodes dP
+            self._gemm(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
+                       tag=f"gemm.wgrad.pool.l{l + 1}")
             if l > 0:
                 # dH = (dH_self + dP Wpool) * leaky'(H): H is the previous layer's output
                 dH = dHM[:, :Fi]
-                self._gemm(self.dP[l], P[p + "Wpool"][:, :Fi], dH, beta=1.0, act=LEAKY, dact=HM[:, :Fi],
+                self._gemm(self.dP[l], P[p + "Wpool"], dH, beta=1.0, act=LEAKY, dact=HM[:, :Fi],
                            tag=f"gemm.dgrad.pool.l{l + 1}")
                 dY = dH
 

@@ -160,10 +160,12 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
          out: Optional[torch.Tensor] = None, alpha: float = 1.0, beta: float = 0.0,
          bias: Optional[torch.Tensor] = None, act: int = _lib.PG_ACT_NONE,
          slope: float = LEAKY_SLOPE, split_k: Optional[int] = None,
-         dact: Optional[torch.Tensor] = None) -> torch.Tensor:
+         dact: Optional[torch.Tensor] = None, rowsum: Optional[torch.Tensor] = None
+         ) -> torch.Tensor:
     """C = alpha*op(A)@op(B) + beta*C (+bias, act) on the fp32 MFMA kernel (GPU) or
     torch-CPU (CPU device). With `dact` (an activation output) the result is instead
-    multiplied by act'(dact): the fused activation backward."""
+    multiplied by act'(dact): the fused activation backward. With `rowsum`, also
+    rowsum[m] = sum_k op(A)[m][k] (bias gradients of a weight-gradient product)."""
     M = A.shape[1] if transa else A.shape[0]
     K = A.shape[0] if transa else A.shape[1]
     Kb = B.shape[1] if transb else B.shape[0]
@@ -189,15 +191,17 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
         elif act == _lib.PG_ACT_LEAKY:
             r = torch.nn.functional.leaky_relu(r, slope)
         out.copy_(r)
+        if rowsum is not None:
+            rowsum.copy_((A.t() if transa else A).sum(1))
         return out
     if split_k is None:
         split_k = 1 if (bias is not None or act != _lib.PG_ACT_NONE or dact is not None
                         or beta not in (0.0, 1.0)) else _split_k(M, N, K)
     ws_n = _lib.lib().pg_gemm_f32_workspace(M, N, K, split_k)
     ws = _workspace(ws_n, A.device)
+    ep = _lib.epilogue(bias, act, slope, dact, rowsum)
     call("pg_gemm_f32", int(transa), int(transb), M, N, K, alpha, ptr(A), _ld(A), ptr(B), _ld(B),
-         beta, ptr(out), _ld(out), ptr(bias), act, slope, ptr(dact),
-         _ld(dact) if dact is not None else 0, split_k, ptr(ws), ws_n, _stream(A))
+         beta, ptr(out), _ld(out), ep, split_k, ptr(ws), ws_n, _stream(A))
     return out
 
 
@@ -295,16 +299,21 @@ class SagePool(torch.autograd.Function):
         dY = dY.contiguous()
         N, Fin = h.shape
         need_h, need_wp, need_bp, need_ws, need_wn, need_b = ctx.needs_input_grad[:6]
-        d_ws = gemm(dY, h, transa=True) if need_ws else None
+        d_b = torch.empty(dY.shape[1], dtype=torch.float32, device=dY.device) \
+            if (need_b and ctx.has_bias) else None
+        d_ws = gemm(dY, h, transa=True, rowsum=d_b) if need_ws else None
         d_wn = gemm(dY, Mb[:, :Fin], transa=True) if need_wn else None
-        d_b = col_sum(dY) if (need_b and ctx.has_bias) else None
+        if d_b is not None and not need_ws:
+            d_b = col_sum(dY)
         dMb = _padded(N, Fin, h.device)
         gemm(dY, w_neigh, out=dMb[:, :Fin])
         dPb = torch.empty_like(Pb)
         spmm_max_backward(dg, argpos, dMb, ew_slots, mask=Pb, dx=dPb)
         dP = dPb[:, :Fin]
-        d_wp = gemm(dP, h, transa=True) if need_wp else None
-        d_bp = col_sum(dP) if need_bp else None
+        d_bp = torch.empty(Fin, dtype=torch.float32, device=dY.device) if need_bp else None
+        d_wp = gemm(dP, h, transa=True, rowsum=d_bp) if need_wp else None
+        if d_bp is not None and not need_wp:
+            d_bp = col_sum(dP)
         d_h = None
         if need_h:
             d_h = gemm(dY, w_self)
