@@ -124,8 +124,7 @@ def main():
                                 seed=rank)
     allreduce = None
     if dist is not None:
-        def allreduce(t):
-            dist.all_reduce(t, op=dist.ReduceOp.AVG)
+        from plagnn.dist import allreduce_mean as allreduce
 
     n_cap_warm = min(2, args.warmup)
     engine.capture(warmup=n_cap_warm, allreduce=allreduce)

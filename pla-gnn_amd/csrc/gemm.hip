@@ -8,20 +8,20 @@
 // sums of op(A) (for a weight-gradient GEMM dY^T X these are the bias gradients
 // sum_nodes dY, computed from the A tiles already staged in LDS).
 //
-// Tiling: BM x BN per 256-thread workgroup (BM, BN in {64, 128}), K step 64; the four
+// Tiling: BM x BN per 256-thread workgroup (BM, BN in {64, 128}), K step 32; the four
 // waves form a 2 x 2 grid, each owning (BM/2) x (BN/2) = TM x TN MFMA tiles of 32 x 32.
 // Global -> register prefetch of the next K tile overlaps the MFMAs of the current one
-// (4096 MFMA cycles per wave per K step cover an HBM miss). Workgroups are ordered so the
+// (a K step of 64 proved slower: the doubled staging registers halve occupancy). Workgroups are ordered so the
 // column tiles of one row tile are consecutive on one XCD (`blockIdx % 8` group, the
 // bijective remap of cdna_hip_programming.md §5): the A rows they share stay in that
 // XCD's L2.
 // LDS layout follows the global layout so every staging store is a ds_write_b128:
 //   A not transposed (A[m][k]) -> As[m][k] (k contiguous, row stride BK+4 floats: the
-//   16-lane groups of ds_read_b128 hit 16 distinct 4-bank slots since 17 is odd);
+//   16-lane groups of ds_read_b128 hit 16 distinct 4-bank slots since 9 is odd);
 //   A transposed (A[k][m])     -> As[k][m] (m contiguous, read by ds_read_b32);
 //   the same for B with n in place of m.
 // K is consumed in a permuted order: at MFMA step s a lane of half h supplies
-// k = 32 h + s (not 2 s + h) for A and B alike, so one lane's k-values are contiguous in
+// k = 16 h + s (not 2 s + h) for A and B alike, so one lane's k-values are contiguous in
 // a [row][k] image (ds_read_b128). Each MFMA still pairs A and B at equal k, so the
 // product is exact f32 with a fixed (permuted) summation order.
 // MFMA 32x32x2 f32 operand map (cdna_hip_programming.md §3): lane l holds
@@ -38,7 +38,7 @@
 
 namespace {
 
-constexpr int BK = 64;
+constexpr int BK = 32;
 constexpr int HK = BK / 2;  // k-values per lane half per K step
 constexpr int kThreads = 256;
 constexpr int KPAD = BK + 4;  // [row][k] image row stride (floats)
