@@ -42,6 +42,29 @@ constexpr int BK = 32;
 constexpr int HK = BK / 2;  // k-values per lane half per K step
 constexpr int kThreads = 256;
 constexpr int KPAD = BK + 4;  // [row][k] image row stride (floats)
+#ifndef PG_GEMM_DB
+#define PG_GEMM_DB 0
+#endif
+#ifndef PG_GEMM_PIPE
+#define PG_GEMM_PIPE 0
+#endif
+constexpr int kBufs = (PG_GEMM_DB || PG_GEMM_PIPE) ? 2 : 1;  // LDS images per operand
+#ifndef PG_GEMM_X
+#define PG_GEMM_X 0  // experiment only: 1 = no in-loop staging (wrong results; timing ceiling)
+#endif
+#ifndef PG_GEMM_STAMP
+#define PG_GEMM_STAMP 0  // probe builds only: per-workgroup clock stamps (scripts/probes)
+#endif
+#if PG_GEMM_STAMP
+__device__ unsigned long long pg_gemm_stamp[65536][4];
+__device__ unsigned long long pg_gemm_kstamp[64][64];  // shader clock at each K-step barrier
+#endif
+#ifndef PG_GEMM_SCHED
+#define PG_GEMM_SCHED 0
+#endif
+#ifndef PG_GEMM_PRIO
+#define PG_GEMM_PRIO 0  // 1 = s_setprio(1) around each MFMA cluster
+#endif
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
@@ -152,6 +175,20 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ S, int rc, i
   }
 }
 
+// 4 k-values (chunk q of lane half h: k = 16 h + 4 q + 0..3) for row/col `rc`.
+template <int ROWS, bool KMAJ>
+__device__ __forceinline__ void read_chunk(const float* __restrict__ S, int rc, int h, int q,
+                                           float (&f)[4]) {
+  const int kb = h * HK + 4 * q;
+  if constexpr (!KMAJ) {
+    const float4 t = *reinterpret_cast<const float4*>(S + rc * KPAD + kb);
+    f[0] = t.x; f[1] = t.y; f[2] = t.z; f[3] = t.w;
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) f[s] = S[(kb + s) * (ROWS + 4) + rc];
+  }
+}
+
 // Row sums of the A tile in LDS over its BK k-values: thread t owns row t % BM and the
 // k-values k = t / BM, t / BM + G, ... (G = 256 / BM groups).
 template <int BM, bool AK>
@@ -167,92 +204,19 @@ __device__ __forceinline__ float tile_rowsum(const float* __restrict__ As, int t
   return s;
 }
 
-// TA: A stored K x M (use A^T). TB: B stored N x K (use B^T).
-template <int BM, int BN, bool TA, bool TB, bool VA, bool VB, int EPI>
-__global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
-    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
-    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
-    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
-    const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
-    float* __restrict__ ws, float* __restrict__ ws_rowsum) {
+// Row sums of op(A) (combined over the k-groups in order) and the epilogue of one tile.
+template <int BM, int BN, int EPI>
+__device__ __forceinline__ void finish_tile(
+    const f32x16 (&acc)[BM / 64][BN / 64], float rs, bool do_rs, float* __restrict__ rsred, int tid,
+    int m0, int n0, int M, int N, float alpha, float beta, float* __restrict__ C, int64_t ldc,
+    const float* __restrict__ bias, float slope, const float* __restrict__ dact, int64_t lddact,
+    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum) {
   constexpr bool SPLIT = EPI == EPI_SPLIT;
-  constexpr bool AK = TA;    // A image k-major ([k][m]) when A is stored transposed
-  constexpr bool BKM = !TB;  // B image k-major ([k][n]) when B is stored K x N
-  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
-  __shared__ __attribute__((aligned(16))) float As[image_floats<BM, AK>()];
-  __shared__ __attribute__((aligned(16))) float Bs[image_floats<BN, BKM>()];
-  __shared__ float rsred[kThreads];
-
-  // XCD-aware tile order: blocks b, b+8, ... share an XCD; give each such group a
-  // contiguous run of tile ids (row-major over [tile_m][tile_n]).
-  const int b = blockIdx.x;
-  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
-  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = tm * BM;
-  const int n0 = tn * BN;
-  const int kz0 = blockIdx.z * k_per_split;
-  const int kz1 = min(K, kz0 + k_per_split);
-  const int h = lane >> 5;
-  const int l32 = lane & 31;
-  const bool do_rs = rowsum != nullptr && tn == 0;
-  float rs = 0.f;
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  TileLoader<BM, AK, VA> la;
-  TileLoader<BN, BKM, VB> lb;
-
-  if (kz0 < kz1) {
-    la.load(A, lda, m0, M, kz0, kz1, tid);
-    lb.load(B, ldb, n0, N, kz0, kz1, tid);
-    la.store(As, tid);
-    lb.store(Bs, tid);
-    __syncthreads();
-    for (int k0 = kz0; k0 < kz1; k0 += BK) {
-      const bool more = k0 + BK < kz1;
-      if (more) {
-        la.load(A, lda, m0, M, k0 + BK, kz1, tid);
-        lb.load(B, ldb, n0, N, k0 + BK, kz1, tid);
-      }
-      if (do_rs) rs += tile_rowsum<BM, AK>(As, tid);
-#pragma unroll
-      for (int c = 0; c < HK / 16; ++c) {
-        float fa[TM][16], fb[TN][16];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) read_frag<BM, AK>(As, wm * (BM / 2) + i * 32 + l32, h, c, fa[i]);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) read_frag<BN, BKM>(Bs, wn * (BN / 2) + j * 32 + l32, h, c, fb[j]);
-#pragma unroll
-        for (int s = 0; s < 16; ++s)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
-      }
-      __syncthreads();
-      if (more) {
-        la.store(As, tid);
-        lb.store(Bs, tid);
-        __syncthreads();
-      }
-    }
-  }
-
-  // row sums of op(A): combine the k-groups in order, one value per row of the tile
+  constexpr int TM = BM / 64, TN = BN / 64;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
   if (do_rs) {
+    __syncthreads();
     rsred[tid] = rs;
     __syncthreads();
     if (tid < BM && m0 + tid < M) {
@@ -288,6 +252,445 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
       }
     }
   }
+}
+
+// The same through LDS: the accumulator tile is transposed into a [BM][BN] LDS image
+// (the staging images are free by now) and written out row-major with 16-B loads/stores,
+// instead of one 4-B store per lane and accumulator register. Needs N % 4 == 0 and 16-B
+// aligned C / ldc (and dact / bias when present).
+template <int BM, int BN, int EPI>
+__device__ __forceinline__ void finish_tile_lds(
+    const f32x16 (&acc)[BM / 64][BN / 64], float rs, bool do_rs, float* __restrict__ lds, int tid,
+    int m0, int n0, int M, int N, float alpha, float beta, float* __restrict__ C, int64_t ldc,
+    const float* __restrict__ bias, float slope, const float* __restrict__ dact, int64_t lddact,
+    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum) {
+  constexpr bool SPLIT = EPI == EPI_SPLIT;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+  if (do_rs) {
+    lds[tid] = rs;
+    __syncthreads();
+    if (tid < BM && m0 + tid < M) {
+      float t = 0.f;
+      for (int g = 0; g < kThreads / BM; ++g) t += lds[g * BM + tid];
+      if constexpr (SPLIT) ws_rowsum[(int64_t)blockIdx.z * M + m0 + tid] = t;
+      else rowsum[m0 + tid] = t;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        lds[row * BN + wn * (BN / 2) + j * 32 + l32] = acc[i][j][r];
+      }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < BM * BN / 4 / kThreads; ++it) {
+    const int u = it * kThreads + tid;
+    const int row = u / (BN / 4), c = (u % (BN / 4)) * 4;
+    const int gr = m0 + row, gc = n0 + c;
+    if (gr >= M || gc >= N) continue;
+    float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
+    if constexpr (SPLIT) {
+      *reinterpret_cast<float4*>(ws + ((int64_t)blockIdx.z * M + gr) * N + gc) = v;
+    } else {
+      float* cp = C + (int64_t)gr * ldc + gc;
+      float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
+      if (beta != 0.f) {
+        const float4 c4 = *reinterpret_cast<const float4*>(cp);
+        o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
+        o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
+      }
+      if (bias) {
+        const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
+        o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
+      }
+      float y[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
+        const float4 d4 = *reinterpret_cast<const float4*>(dact + (int64_t)gr * lddact + gc);
+        y[0] = d4.x; y[1] = d4.y; y[2] = d4.z; y[3] = d4.w;
+      }
+      *reinterpret_cast<float4*>(cp) = make_float4(epi_apply<EPI>(o[0], y[0], slope), epi_apply<EPI>(o[1], y[1], slope),
+                                                   epi_apply<EPI>(o[2], y[2], slope), epi_apply<EPI>(o[3], y[3], slope));
+    }
+  }
+}
+
+#if PG_GEMM_STAMP
+__device__ __forceinline__ void stamp(unsigned long long st_rt, unsigned long long st_ck, int tid) {
+  if (tid == 0 && blockIdx.x < 65536) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    pg_gemm_stamp[blockIdx.x][0] = st_rt;
+    pg_gemm_stamp[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+    pg_gemm_stamp[blockIdx.x][2] = __builtin_amdgcn_s_memtime() - st_ck;
+    pg_gemm_stamp[blockIdx.x][3] = ((unsigned long long)xcc << 32) | hw;
+  }
+}
+#endif
+
+// TA: A stored K x M (use A^T). TB: B stored N x K (use B^T).
+template <int BM, int BN, bool TA, bool TB, bool VA, bool VB, int EPI>
+__global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
+    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
+    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
+    const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
+    float* __restrict__ ws, float* __restrict__ ws_rowsum) {
+  constexpr bool AK = TA;    // A image k-major ([k][m]) when A is stored transposed
+  constexpr bool BKM = !TB;  // B image k-major ([k][n]) when B is stored K x N
+  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
+  __shared__ __attribute__((aligned(16))) float As_[kBufs][image_floats<BM, AK>()];
+  __shared__ __attribute__((aligned(16))) float Bs_[kBufs][image_floats<BN, BKM>()];
+  __shared__ float rsred[kThreads];
+
+  // XCD-aware tile order: blocks b, b+8, ... share an XCD; give each such group a
+  // contiguous run of tile ids (row-major over [tile_m][tile_n]).
+  const int b = blockIdx.x;
+  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
+  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+#if PG_GEMM_STAMP
+  unsigned long long st_rt = __builtin_amdgcn_s_memrealtime(), st_ck = __builtin_amdgcn_s_memtime();
+#endif
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+  const int kz0 = blockIdx.z * k_per_split;
+  const int kz1 = min(K, kz0 + k_per_split);
+  const int h = lane >> 5;
+  const int l32 = lane & 31;
+  const bool do_rs = rowsum != nullptr && tn == 0;
+  float rs = 0.f;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  TileLoader<BM, AK, VA> la;
+  TileLoader<BN, BKM, VB> lb;
+
+#if PG_GEMM_PIPE
+  // Software pipeline: fragments are read in chunks of 4 k-values (one ds_read_b128 per
+  // 32-row tile) one chunk ahead of the MFMAs that use them, across K steps as well; the
+  // next K tile is staged into the other LDS image behind the third chunk's MFMAs, so one
+  // barrier per K step and the next step's first chunk read is covered by chunk 3.
+  if (kz0 < kz1) {
+    la.load(A, lda, m0, M, kz0, kz1, tid);
+    lb.load(B, ldb, n0, N, kz0, kz1, tid);
+    la.store(As_[0], tid);
+    lb.store(Bs_[0], tid);
+    __syncthreads();
+    float fa[2][TM][4], fb[2][TN][4];
+    const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) read_chunk<BM, AK>(As_[0], ra + i * 32, h, 0, fa[0][i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) read_chunk<BN, BKM>(Bs_[0], rb + j * 32, h, 0, fb[0][j]);
+    int cur = 0;
+    for (int k0 = kz0; k0 < kz1; k0 += BK) {
+      const bool more = k0 + BK < kz1;
+      if (more) {
+        la.load(A, lda, m0, M, k0 + BK, kz1, tid);
+        lb.load(B, ldb, n0, N, k0 + BK, kz1, tid);
+      }
+      const float* As = As_[cur];
+      const float* Bs = Bs_[cur];
+      if (do_rs) rs += tile_rowsum<BM, AK>(As, tid);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = q & 1;
+        if (q < 3) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) read_chunk<BM, AK>(As, ra + i * 32, h, q + 1, fa[u ^ 1][i]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) read_chunk<BN, BKM>(Bs, rb + j * 32, h, q + 1, fb[u ^ 1][j]);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][i][s], fb[u][j][s], acc[i][j], 0, 0, 0);
+        if (q == 2) {
+          if (more) {
+            la.store(As_[cur ^ 1], tid);
+            lb.store(Bs_[cur ^ 1], tid);
+          }
+          __syncthreads();
+          if (more) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) read_chunk<BM, AK>(As_[cur ^ 1], ra + i * 32, h, 0, fa[0][i]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) read_chunk<BN, BKM>(Bs_[cur ^ 1], rb + j * 32, h, 0, fb[0][j]);
+          }
+        }
+      }
+      cur ^= 1;
+    }
+  }
+#else
+  if (kz0 < kz1) {
+    la.load(A, lda, m0, M, kz0, kz1, tid);
+    lb.load(B, ldb, n0, N, kz0, kz1, tid);
+    la.store(As_[0], tid);
+    lb.store(Bs_[0], tid);
+    __syncthreads();
+    int cur = 0;
+    for (int k0 = kz0; k0 < kz1; k0 += BK) {
+      const bool more = !PG_GEMM_X && k0 + BK < kz1;
+      if (more) {
+        la.load(A, lda, m0, M, k0 + BK, kz1, tid);
+        lb.load(B, ldb, n0, N, k0 + BK, kz1, tid);
+      }
+      const float* As = As_[cur];
+      const float* Bs = Bs_[cur];
+      if (do_rs) rs += tile_rowsum<BM, AK>(As, tid);
+#pragma unroll
+      for (int c = 0; c < HK / 16; ++c) {
+        float fa[TM][16], fb[TN][16];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) read_frag<BM, AK>(As, wm * (BM / 2) + i * 32 + l32, h, c, fa[i]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) read_frag<BN, BKM>(Bs, wn * (BN / 2) + j * 32 + l32, h, c, fb[j]);
+        if (PG_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+        if (PG_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
+      }
+      if constexpr (kBufs == 2) {
+        // double buffer: stage into the other image, one barrier per K step (every wave
+        // finished reading that image before the previous barrier)
+        if (more) {
+          la.store(As_[cur ^ 1], tid);
+          lb.store(Bs_[cur ^ 1], tid);
+        }
+        __syncthreads();
+        cur ^= 1;
+      } else {
+        __syncthreads();
+        if (more) {
+          la.store(As_[0], tid);
+          lb.store(Bs_[0], tid);
+          __syncthreads();
+        }
+      }
+    }
+  }
+
+#endif
+
+  finish_tile<BM, BN, EPI>(acc, rs, do_rs, rsred, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
+                           slope, dact, lddact, rowsum, ws, ws_rowsum);
+#if PG_GEMM_STAMP
+  stamp(st_rt, st_ck, tid);
+#endif
+}
+
+// ---------------------------------------------------------------------------------------
+// Main kernel (16-B aligned operands with extents that are multiples of 4): LDS-DMA staging.
+//
+// K tiles go global -> LDS by global_load_lds_dwordx4 (no register round trip, no ds_write)
+// into two LDS images per operand; the tile for step t+1 is issued at the top of step t and
+// waited for by the single barrier of step t. Fragments are read in chunks of 4 k-values
+// (one ds_read_b128, or 4 ds_read_b32 for a k-major image) one chunk ahead of the MFMAs
+// that consume them, across K steps too: the barrier sits after chunk 2's MFMAs and the
+// next tile's chunk 0 is read under chunk 3's, so the LDS traffic of a wave overlaps its
+// own MFMAs instead of waiting for other waves to fill the matrix pipe.
+//
+// LDS images (no padding; one DMA wave-instruction fills 1 KiB contiguously):
+//   [row][k] (operand stored k-contiguous): row r = 128 B = 8 chunks of 4 k-values; chunk c
+//     is stored at chunk c ^ ((r >> 1) & 7): the 16-lane groups of ds_read_b128 (16
+//     consecutive rows, same chunk) hit 16 distinct 16-B bank slots. The XOR is applied
+//     to the DMA's per-lane SOURCE address (the destination is lane-linear).
+//   [k][row] (operand stored row-contiguous): plain; ds_read_b32 over 32 consecutive rows.
+// Rows past the matrix edge are loaded from a clamped (valid) row: they only feed output
+// rows / columns that are never stored. In a partial last K tile the units past K are
+// zero-filled by ds_write instead of loaded.
+template <int ROWS, bool KMAJ>
+__device__ __forceinline__ int img_off(int row, int k) {  // float offset of (row, k)
+  if constexpr (KMAJ) return k * ROWS + row;
+  else return row * BK + ((((k >> 2) ^ ((row >> 1) & 7))) << 2) + (k & 3);
+}
+
+template <int ROWS, bool KMAJ, bool FULL>
+__device__ __forceinline__ void dma_tile(const float* __restrict__ P, int64_t ld, int r0, int R,
+                                         int k0, int kvalid, float* S, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < ROWS / 32; ++j) {
+    const int piece = j * 4 + wave;  // 1-KiB piece of the image
+    const int u = piece * 64 + lane;  // 16-B unit
+    const float* src;
+    bool valid;
+    if constexpr (!KMAJ) {
+      const int row = u >> 3, c = (u & 7) ^ ((row >> 1) & 7);
+      valid = 4 * c < kvalid;
+      src = P + (int64_t)min(r0 + row, R - 1) * ld + k0 + 4 * c;
+    } else {
+      const int k = u / (ROWS / 4), c4 = u % (ROWS / 4);
+      valid = k < kvalid;
+      src = P + (int64_t)(k0 + k) * ld + min(r0 + 4 * c4, R - 4);
+    }
+    // units past K (partial last tile) are zero-filled by the lane that owns them instead
+    // (a DMA lane masked off by EXEC writes nothing)
+    if (FULL || valid) __builtin_amdgcn_global_load_lds(src, S + piece * 256, 16, 0, 0);
+    else *reinterpret_cast<float4*>(S + u * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int ROWS, bool KMAJ>
+__device__ __forceinline__ void frag_chunk(const float* __restrict__ S, int rc, int h, int q,
+                                           float (&f)[4]) {
+  const int kb = h * HK + 4 * q;
+  if constexpr (!KMAJ) {
+    const float4 t = *reinterpret_cast<const float4*>(S + img_off<ROWS, false>(rc, kb));
+    f[0] = t.x; f[1] = t.y; f[2] = t.z; f[3] = t.w;
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) f[s] = S[(kb + s) * ROWS + rc];
+  }
+}
+
+template <int BM, bool AK>
+__device__ __forceinline__ float img_rowsum(const float* __restrict__ As, int tid) {
+  constexpr int G = kThreads / BM;
+  const int m = tid % BM, g = tid / BM;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < BK / G; ++i) s += As[img_off<BM, AK>(m, g + i * G)];
+  return s;
+}
+
+template <int BM, int BN, bool TA, bool TB, int EPI>
+__global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
+    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
+    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
+    const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
+    float* __restrict__ ws, float* __restrict__ ws_rowsum, int vec_out) {
+  constexpr bool AK = TA, BKM = !TB;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int IA = BM * BK, IB = BN * BK;  // image sizes (floats)
+  // one LDS array: [A0 | A1 | B0 | B1] (a second __shared__ object can make hipcc drain
+  // the DMA at every LDS read)
+  __shared__ __attribute__((aligned(16))) float lds[2 * (IA + IB)];
+
+  const int b = blockIdx.x;
+  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
+  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kz0 = blockIdx.z * k_per_split;
+  const int kz1 = min(K, kz0 + k_per_split);
+  const bool do_rs = rowsum != nullptr && tn == 0;
+#if PG_GEMM_STAMP
+  unsigned long long st_rt = __builtin_amdgcn_s_memrealtime(), st_ck = __builtin_amdgcn_s_memtime();
+#endif
+  float rs = 0.f;
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = kz1 > kz0 ? (kz1 - kz0 + BK - 1) / BK : 0;
+  // issue the DMA of K tile t into LDS image `buf`
+  auto issue = [&](int t, int buf) {
+    const int k0 = kz0 + t * BK;
+    if (kz1 - k0 >= BK) {
+      dma_tile<BM, AK, true>(A, lda, m0, M, k0, BK, lds + buf * IA, wave, lane);
+      dma_tile<BN, BKM, true>(B, ldb, n0, N, k0, BK, lds + 2 * IA + buf * IB, wave, lane);
+    } else {
+      dma_tile<BM, AK, false>(A, lda, m0, M, k0, kz1 - k0, lds + buf * IA, wave, lane);
+      dma_tile<BN, BKM, false>(B, ldb, n0, N, k0, kz1 - k0, lds + 2 * IA + buf * IB, wave, lane);
+    }
+  };
+
+  if (nk > 0) {
+    issue(0, 0);
+    __syncthreads();
+    float fa[2][TM][4], fb[2][TN][4];
+    const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) frag_chunk<BM, AK>(lds, ra + i * 32, h, 0, fa[0][i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) frag_chunk<BN, BKM>(lds + 2 * IA, rb + j * 32, h, 0, fb[0][j]);
+    for (int t = 0; t < nk; ++t) {
+      const int cur = t & 1;
+      const bool more = t + 1 < nk;
+      if (more) issue(t + 1, cur ^ 1);
+      const float* As = lds + cur * IA;
+      const float* Bs = lds + 2 * IA + cur * IB;
+      if (do_rs) rs += img_rowsum<BM, AK>(As, tid);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = q & 1;
+        if (q < 3) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) frag_chunk<BM, AK>(As, ra + i * 32, h, q + 1, fa[u ^ 1][i]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) frag_chunk<BN, BKM>(Bs, rb + j * 32, h, q + 1, fb[u ^ 1][j]);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][i][s], fb[u][j][s], acc[i][j], 0, 0, 0);
+        if (q == 2) {
+#if PG_GEMM_SCHED
+          __builtin_amdgcn_sched_barrier(0);  // keep chunk 2's MFMAs ahead of the barrier
+#endif
+          __syncthreads();  // tile t+1 landed (vmcnt) and every wave is past its reads of tile t-1
+#if PG_GEMM_STAMP
+          if (tid == 0 && blockIdx.x < 64 && t < 64) pg_gemm_kstamp[blockIdx.x][t] = __builtin_amdgcn_s_memtime();
+#endif
+          if (more) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+              frag_chunk<BM, AK>(lds + (cur ^ 1) * IA, ra + i * 32, h, 0, fa[0][i]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              frag_chunk<BN, BKM>(lds + 2 * IA + (cur ^ 1) * IB, rb + j * 32, h, 0, fb[0][j]);
+          }
+        }
+      }
+    }
+    __syncthreads();  // the row-sum scratch below reuses the staging array
+  }
+  if (vec_out)
+    finish_tile_lds<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
+                                 slope, dact, lddact, rowsum, ws, ws_rowsum);
+  else
+    finish_tile<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
+                             slope, dact, lddact, rowsum, ws, ws_rowsum);
+#if PG_GEMM_STAMP
+  stamp(st_rt, st_ck, tid);
+#endif
 }
 
 // Split-K combine: C = alpha * sum_z ws[z] (+ beta * C), slices summed in order; the row
@@ -336,6 +739,7 @@ struct Args {
   float* rowsum;
   float* ws;
   float* ws_rowsum;
+  int vec_out;
 };
 
 template <int BM, int BN, bool TA, bool TB, bool VA, bool VB>
@@ -359,7 +763,29 @@ int launch_epi(int epi, dim3 grid, hipStream_t st, const Args& a) {
 }
 
 template <int BM, int BN, bool TA, bool TB>
+int launch_dma(int epi, dim3 grid, hipStream_t st, const Args& a) {
+#define PG_L(EPI_)                                                                          \
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, EPI_>), grid, dim3(kThreads), 0, st, a.M, \
+                     a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb,     \
+                     a.beta, a.C, a.ldc, a.bias, a.slope, a.dact, a.lddact, a.rowsum, a.ws,    \
+                     a.ws_rowsum, a.vec_out)
+  switch (epi) {
+    case EPI_NONE: PG_L(EPI_NONE); break;
+    case EPI_RELU: PG_L(EPI_RELU); break;
+    case EPI_LEAKY: PG_L(EPI_LEAKY); break;
+    case EPI_DRELU: PG_L(EPI_DRELU); break;
+    case EPI_DLEAKY: PG_L(EPI_DLEAKY); break;
+    case EPI_SPLIT: PG_L(EPI_SPLIT); break;
+    default: return PG_ERR_INVALID;
+  }
+#undef PG_L
+  return PG_OK;
+}
+
+template <int BM, int BN, bool TA, bool TB>
 int launch_vec(bool va, bool vb, int epi, dim3 grid, hipStream_t st, const Args& a) {
+  static const bool legacy = getenv("PLAGNN_GEMM_LEGACY") != nullptr;  // A/B knob
+  if (va && vb && !legacy) return launch_dma<BM, BN, TA, TB>(epi, grid, st, a);
   if (va && vb) return launch_epi<BM, BN, TA, TB, true, true>(epi, grid, st, a);
   if (va) return launch_epi<BM, BN, TA, TB, true, false>(epi, grid, st, a);
   if (vb) return launch_epi<BM, BN, TA, TB, false, true>(epi, grid, st, a);
@@ -448,9 +874,14 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   dim3 grid((unsigned)tiles, 1, (unsigned)split_k);
   hipStream_t st = (hipStream_t)stream;
   float* wsf = split ? (float*)ws : nullptr;
+  // 16-B epilogue stores (finish_tile_lds) when every output-side operand allows them
+  const bool vec_out = (N % 4) == 0 &&
+                       (split ? al16(wsf) : (al16(C) && (ldc % 4) == 0)) &&
+                       (!ep->bias || al16(ep->bias)) &&
+                       (!ep->dact || (al16(ep->dact) && (ep->lddact % 4) == 0));
   const Args a{(int)M, (int)N, (int)K, kps, tiles_n, tiles, alpha, A, lda, B, ldb, beta, C, ldc,
                ep->bias, ep->slope, ep->dact, ep->lddact, ep->rowsum, wsf,
-               split ? wsf + (int64_t)split_k * M * N : nullptr};
+               split ? wsf + (int64_t)split_k * M * N : nullptr, vec_out ? 1 : 0};
   const bool ta = transa != 0, tb = transb != 0;
   const int epi = split ? EPI_SPLIT
                         : ep->dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)

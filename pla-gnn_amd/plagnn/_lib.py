@@ -12,7 +12,8 @@ import os
 import torch  # noqa: F401  (load order: see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libplagnn.so")
+# PLAGNN_LIB overrides the library path (A/B builds of tuning variants)
+LIB_PATH = os.environ.get("PLAGNN_LIB") or os.path.join(_HERE, "libplagnn.so")
 
 PG_ARG_U16 = 16
 PG_ARG_I32 = 32

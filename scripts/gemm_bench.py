@@ -43,12 +43,15 @@ def timeit(fn, reps=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dims", default="503,256,256,256,100,12")
+    ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--square", type=int, default=4096, help="also time an NxNxN NN GEMM (0: skip)")
     args = ap.parse_args()
     dims = [int(x) for x in args.dims.split(",")]
+    extra = [("square", False, False, args.square, args.square, args.square)] if args.square else []
     tot_m = tot_t = 0.0
     print(f"{'op':14} {'ta':>2} {'tb':>2} {'M':>6} {'N':>5} {'K':>6} {'mine_us':>8} {'TF':>6} {'torch_us':>8} {'TF':>6}")
     seen = set()
-    for name, ta, tb, M, N, K in shapes(dims):
+    for name, ta, tb, M, N, K in shapes(dims) + extra:
         key = (ta, tb, M, N, K)
         if key in seen:
             continue
@@ -59,10 +62,11 @@ def main():
         tm = timeit(lambda: ops.gemm(A, B, transa=ta, transb=tb, out=C))
         a_ = A.t() if ta else A
         b_ = B.t() if tb else B
-        tt = timeit(lambda: torch.mm(a_, b_, out=C))
+        tt = float("nan") if args.no_torch else timeit(lambda: torch.mm(a_, b_, out=C))
         fl = 2.0 * M * N * K
-        tot_m += tm
-        tot_t += tt
+        if name != "square":
+            tot_m += tm
+            tot_t += tt
         print(f"{name:14} {int(ta):>2} {int(tb):>2} {M:>6} {N:>5} {K:>6} {tm*1e3:8.1f} {fl/tm/1e9:6.1f} {tt*1e3:8.1f} {fl/tt/1e9:6.1f}")
     print(f"total (unique shapes): mine {tot_m*1e3:.1f} us, torch {tot_t*1e3:.1f} us")
 

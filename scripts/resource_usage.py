@@ -1,5 +1,6 @@
 """Per-kernel VGPR/AGPR/occupancy/scratch/LDS from hipcc -Rpass-analysis (gfx950).
-Usage: python scripts/resource_usage.py pla-gnn_amd/csrc/spmm.hip [filter]"""
+Usage: [RU_FLAGS=-DX=1] python scripts/resource_usage.py pla-gnn_amd/csrc/spmm.hip [filter]"""
+import os
 import re
 import subprocess
 import sys
@@ -8,7 +9,7 @@ src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
 out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
                       "-ffp-contract=off", "-c", src, "-o", "/dev/null",
-                      "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
+                      "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("RU_FLAGS", "").split(), capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
     m = re.search(r"remark: (.*?) \[-Rpass", line)

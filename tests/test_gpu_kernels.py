@@ -70,9 +70,9 @@ def test_spmm_max_bwd(oracle_mod, F, weighted):
     mask = torch.from_numpy(X).to(DEV)
     dXm = ops.spmm_max_backward(dg, argpos, torch.from_numpy(dZ).to(DEV), ews, mask=mask).cpu().numpy()
     np.testing.assert_array_equal(dXm, np.where(X > 0, dX, 0.0))
-    # DGL scatter form (atomics)
+    # DGL scatter form (atomics: the fp32 summation order varies run to run, as in DGL)
     dXs = ops.spmm_max_backward_scatter(dg, argpos, torch.from_numpy(dZ).to(DEV), ews).cpu().numpy()
-    np.testing.assert_allclose(dXs, dX_ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(dXs, dX_ref, rtol=1e-4, atol=1e-4)
 
 
 def test_spmm_max_int32_positions(oracle_mod):
