@@ -102,6 +102,8 @@ typedef struct pg_csr {
   int64_t n_slots;
   int32_t max_deg;
   int32_t chunk;
+  const int32_t* einv;   /* [nnz] in-CSR only, optional: index of every in-CSR slot in the
+                            transposed CSR (the inverse permutation of its eslot) */
 } pg_csr_t;
 
 /* ---------------- host: graph construction (code/utils.py:74-75) ---------------- */
@@ -241,7 +243,7 @@ int pg_argpos_to_src_cpu(const pg_csr_t* g, const void* argpos, int64_t lda, int
 
 /* ---------------- misc ---------------- */
 const char* pg_last_error_string(void);
-int pg_version(void);
+int pg_version(void); /* 2: pg_csr_t.einv */
 
 #ifdef __cplusplus
 }

@@ -58,6 +58,7 @@ constexpr int kBufs = (PG_GEMM_DB || PG_GEMM_PIPE) ? 2 : 1;  // LDS images per o
 #if PG_GEMM_STAMP
 __device__ unsigned long long pg_gemm_stamp[65536][4];
 __device__ unsigned long long pg_gemm_kstamp[64][64];  // shader clock at each K-step barrier
+__device__ unsigned long long pg_gemm_kphase[64][4];   // start, prologue done, loop done, end
 #endif
 #ifndef PG_GEMM_SCHED
 #define PG_GEMM_SCHED 0
@@ -329,6 +330,7 @@ __device__ __forceinline__ void stamp(unsigned long long st_rt, unsigned long lo
     pg_gemm_stamp[blockIdx.x][0] = st_rt;
     pg_gemm_stamp[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
     pg_gemm_stamp[blockIdx.x][2] = __builtin_amdgcn_s_memtime() - st_ck;
+    if (blockIdx.x < 64) pg_gemm_kphase[blockIdx.x][3] = st_ck + pg_gemm_stamp[blockIdx.x][2];
     pg_gemm_stamp[blockIdx.x][3] = ((unsigned long long)xcc << 32) | hw;
   }
 }
@@ -632,6 +634,9 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
   if (nk > 0) {
     issue(0, 0);
     __syncthreads();
+#if PG_GEMM_STAMP
+    if (tid == 0 && blockIdx.x < 64) pg_gemm_kphase[blockIdx.x][1] = __builtin_amdgcn_s_memtime();
+#endif
     float fa[2][TM][4], fb[2][TN][4];
     const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
 #pragma unroll
@@ -682,6 +687,12 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     }
     __syncthreads();  // the row-sum scratch below reuses the staging array
   }
+#if PG_GEMM_STAMP
+  if (tid == 0 && blockIdx.x < 64) {
+    pg_gemm_kphase[blockIdx.x][0] = st_ck;
+    pg_gemm_kphase[blockIdx.x][2] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   if (vec_out)
     finish_tile_lds<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
                                  slope, dact, lddact, rowsum, ws, ws_rowsum);

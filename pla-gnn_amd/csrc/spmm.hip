@@ -339,20 +339,31 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
 }
 
 // ---- max backward, grouped form (default for u16 records and F <= 1024) ---------------
-// Pass 1, one workgroup per destination row v: counting-sort v's features by their
-// winning in-row position p (LDS histogram + block scan; a bitonic sort of the keys
-// (p << 16 | f) for rows longer than kHistMax), giving
-//   gpos[ptr[v] + v + p] = start of p's feature list (p = 0..deg; the last = #winners),
-//   gfeat[v][i]          = the features in p order,
-//   dpack[v][i]          = dout[v][gfeat[v][i]]  (the upstream gradient in list order).
-// Pass 2, one wave per source row u: for each out-edge (u -> v) at position p, ascending
-// v, add dpack[v][gpos..gpos'] (* w) into an LDS row accumulator at gfeat[v][...]. A
-// list never repeats a feature, so one instruction's lanes hit distinct LDS words and
-// the per-feature summation order is ascending v, exactly as the sequential
-// scatter_add_. Traffic per edge is two short contiguous runs (~F/deg entries) instead
-// of v's whole argmax row.
+// Pass 1 (pack), per destination row v: group v's features by their winning in-row
+// position p, giving
+//   gfeat[v F + i]  the features, grouped by p (any order inside a group),
+//   dpack[v F + i]  = dout[v][gfeat[v F + i]]   (the upstream gradient in list order),
+//   glist[t]        = {v F + start_p, count_p} for the edge at in-CSR slot ptr[v] + p,
+//                     stored at that edge's index t = einv[slot] in the transposed CSR.
+// Rows of in-degree <= kPackWaveMax: one wave per row (wave-private LDS histogram, wave
+// scan, LDS-atomic placement); longer rows: one workgroup per row (block histogram, or a
+// bitonic sort of (p << 16 | f) keys past kHistMax entries).
+// Pass 2 (pull), one wave per source row u: for each out-edge of u, ascending destination
+// v (the transposed CSR order), read its descriptor glist[t] (coalesced over the window)
+// and add dpack[list] (* w) into an LDS row accumulator at gfeat[list]. A list never
+// repeats a feature, so one instruction's lanes hit distinct LDS words and every
+// feature's terms are summed in ascending v, the order of the sequential scatter_add_:
+// the order inside a list does not matter. Traffic per edge: one 8-B descriptor and two
+// short contiguous runs (~F/deg entries).
 constexpr int kHistMax = 4096;
 constexpr int kGroupMaxF = 1024;
+constexpr int kPackWaveMax = 256;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   const int per = (n + kBlock - 1) / kBlock;
@@ -384,18 +395,88 @@ __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
 }
 
 template <typename A>
-__global__ __launch_bounds__(kBlock) void group_pack_kernel(
-    const int32_t* __restrict__ ptr, const A* __restrict__ arg, int64_t lda, int F,
-    const float* __restrict__ dout, int64_t ldd, uint16_t* __restrict__ gfeat,
-    uint16_t* __restrict__ gpos, float* __restrict__ dpack) {
-  __shared__ int hist[kHistMax + 8];
-  __shared__ uint16_t feats[kGroupMaxF];
-  __shared__ int wsum[4];
-  const int v = blockIdx.x;
+__device__ __forceinline__ void pack_short_row(
+    int v, int wave, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
+    const A* __restrict__ arg, int64_t lda, int F, const float* __restrict__ dout, int64_t ldd,
+    uint16_t* __restrict__ gfeat, int2* __restrict__ glist, float* __restrict__ dpack,
+    int* __restrict__ lds) {
+  constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
+  const int lane = lane_id();
   const int rs = ptr[v];
   const int deg = ptr[v + 1] - rs;
-  uint16_t* gp = gpos + rs + v;  // deg + 1 entries
+  if (deg > kPackWaveMax || deg == 0) return;
+  int* hist = lds + wave * (kPackWaveMax + 4 + kGroupMaxF / 2);
+  uint16_t* feats = reinterpret_cast<uint16_t*>(hist + kPackWaveMax + 4);
+  for (int p = lane; p < deg; p += kWave) hist[p] = 0;
+  wave_lds_sync();
   const A* ar = arg + (int64_t)v * lda;
+  int a[MAXW];
+#pragma unroll
+  for (int i = 0; i < MAXW; ++i) {
+    const int f = lane + i * kWave;
+    a[i] = f < F ? (int)ar[f] : arg_none<A>();
+  }
+#pragma unroll
+  for (int i = 0; i < MAXW; ++i)
+    if (a[i] != arg_none<A>()) atomicAdd(&hist[a[i]], 1);
+  wave_lds_sync();
+  // exclusive scan over the deg bins: lane owns bins [lane B, lane B + B)
+  const int B = (deg + kWave - 1) / kWave;  // <= 4
+  int c[4], local = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = lane * B + q;
+    c[q] = (q < B && p < deg) ? hist[p] : 0;
+    local += c[q];
+  }
+  int x = local;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  const int total = __shfl(x, kWave - 1);
+  int run = x - local;
+  const int vF = v * F;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = lane * B + q;
+    if (q < B && p < deg) {
+      hist[p] = run;
+      glist[einv[rs + p]] = make_int2(vF + run, c[q]);
+      run += c[q];
+    }
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int i = 0; i < MAXW; ++i)
+    if (a[i] != arg_none<A>()) feats[atomicAdd(&hist[a[i]], 1)] = (uint16_t)(lane + i * kWave);
+  wave_lds_sync();
+  const float* dr = dout + (int64_t)v * ldd;
+  for (int i = lane; i < total; i += kWave) {
+    const int f = feats[i];
+    gfeat[(int64_t)vF + i] = (uint16_t)f;
+    dpack[(int64_t)vF + i] = dr[f];
+  }
+}
+
+// Rows longer than kPackWaveMax, one workgroup each: `rows` lists them ({row, ...} int4,
+// the split-row merges of a schedule whose chunk <= kPackWaveMax), or NULL = every row
+// (short ones exit at once).
+template <typename A>
+__device__ __forceinline__ void pack_long_row(
+    int v, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
+    const A* __restrict__ arg, int64_t lda, int F, const float* __restrict__ dout, int64_t ldd,
+    uint16_t* __restrict__ gfeat, int2* __restrict__ glist, float* __restrict__ dpack,
+    int* __restrict__ lds) {
+  int* hist = lds;
+  uint16_t* feats = reinterpret_cast<uint16_t*>(lds + kHistMax + 8);
+  int* wsum = lds + kHistMax + 8 + kGroupMaxF / 2;
+  const int rs = ptr[v];
+  const int deg = ptr[v + 1] - rs;
+  if (deg <= kPackWaveMax) return;
+  const A* ar = arg + (int64_t)v * lda;
+  const int vF = v * F;
   int total;
   if (deg <= kHistMax) {
     for (int p = threadIdx.x; p < deg; p += kBlock) hist[p] = 0;
@@ -406,8 +487,11 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
     }
     __syncthreads();
     total = block_exclusive_scan(hist, deg, wsum);
-    for (int p = threadIdx.x; p < deg; p += kBlock) gp[p] = (uint16_t)hist[p];
-    if (threadIdx.x == 0) gp[deg] = (uint16_t)total;
+    for (int p = threadIdx.x; p < deg; p += kBlock) {
+      const int st = hist[p];
+      const int en = p + 1 < deg ? hist[p + 1] : total;
+      glist[einv[rs + p]] = make_int2(vF + st, en - st);
+    }
     __syncthreads();
     for (int f = threadIdx.x; f < F; f += kBlock) {
       const int a = (int)ar[f];
@@ -442,46 +526,71 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
         }
         __syncthreads();
       }
-    // count winners = first index whose key is 0xFFFFFFFF
-    for (int p = threadIdx.x; p <= deg; p += kBlock) {
-      const uint32_t key = (uint32_t)p << 16;
+    auto lower = [&](uint32_t key) {
       int lo = 0, hi = np;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if (keys[mid] < key) lo = mid + 1; else hi = mid;
       }
-      gp[p] = (uint16_t)lo;
+      return lo;
+    };
+    for (int p = threadIdx.x; p < deg; p += kBlock) {
+      const int st = lower((uint32_t)p << 16);
+      const int en = lower((uint32_t)(p + 1) << 16);
+      glist[einv[rs + p]] = make_int2(vF + st, en - st);
     }
-    if (threadIdx.x == 0) {
-      int lo = 0, hi = np;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (keys[mid] != 0xFFFFFFFFu) lo = mid + 1; else hi = mid;
-      }
-      wsum[0] = lo;
-    }
+    if (threadIdx.x == 0) wsum[0] = lower(0xFFFFFFFFu);
     __syncthreads();
     total = wsum[0];
-    gp[deg] = (uint16_t)total;  // (all threads write the same value)
     for (int i = threadIdx.x; i < total; i += kBlock) feats[i] = (uint16_t)(keys[i] & 0xFFFFu);
     __syncthreads();
   }
   const float* dr = dout + (int64_t)v * ldd;
   for (int i = threadIdx.x; i < total; i += kBlock) {
     const int f = feats[i];
-    gfeat[(int64_t)v * F + i] = (uint16_t)f;
-    dpack[(int64_t)v * F + i] = dr[f];
+    gfeat[(int64_t)vF + i] = (uint16_t)f;
+    dpack[(int64_t)vF + i] = dr[f];
   }
+}
+
+// One launch for both: blocks [0, n_long) take the rows past kPackWaveMax (`rows` lists
+// them, as {row, ...} int4 = the split-row merges of a schedule whose chunk is <=
+// kPackWaveMax; NULL = every row, short ones exit at once) so the long rows start first;
+// the remaining blocks take 4 rows each, one wave per row.
+constexpr int kPackLds = kHistMax + 8 + kGroupMaxF / 2 + 4;
+static_assert(kPackLds >= kWavesPerBlock * (kPackWaveMax + 4 + kGroupMaxF / 2), "pack LDS");
+
+template <typename A>
+__global__ __launch_bounds__(kBlock) void group_pack_kernel(
+    const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
+    const int32_t* __restrict__ einv, const A* __restrict__ arg, int64_t lda, int F,
+    const float* __restrict__ dout, int64_t ldd, uint16_t* __restrict__ gfeat,
+    int2* __restrict__ glist, float* __restrict__ dpack) {
+  __shared__ __attribute__((aligned(16))) int lds[kPackLds];
+  const int b = blockIdx.x;
+  if (b < n_long) {
+    pack_long_row<A>(rows ? rows[b].x : b, ptr, einv, arg, lda, F, dout, ldd, gfeat, glist, dpack, lds);
+  } else {
+    const int wave = wave_id_uniform();
+    const int v = (b - n_long) * kWavesPerBlock + wave;
+    if (v < n_rows) pack_short_row<A>(v, wave, ptr, einv, arg, lda, F, dout, ldd, gfeat, glist, dpack, lds);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void invert_slots_kernel(const int32_t* __restrict__ tslot,
+                                                              int64_t nnz, int32_t* __restrict__ einv) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < nnz; t += (int64_t)gridDim.x * kBlock)
+    einv[tslot[t]] = (int32_t)t;
 }
 
 template <bool HAS_W>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
-    const float* __restrict__ ew, const int32_t* __restrict__ tcol,
-    const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
-    const uint16_t* __restrict__ gfeat, const uint16_t* __restrict__ gpos,
-    const float* __restrict__ dpack, int F, const float* __restrict__ mask, int64_t ldm,
-    float* __restrict__ dx, int64_t ldx, float* __restrict__ ws, int64_t ldw) {
-  constexpr int U = 8;
+    const float* __restrict__ ew, const int32_t* __restrict__ tslot,
+    const int4* __restrict__ items, int n_items, const int2* __restrict__ glist,
+    const uint16_t* __restrict__ gfeat, const float* __restrict__ dpack, int F,
+    const float* __restrict__ mask, int64_t ldm, float* __restrict__ dx, int64_t ldx,
+    float* __restrict__ ws, int64_t ldw) {
+  constexpr int U = 16;
   __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
   const int wave = wave_id_uniform();
   const int it = blockIdx.x * kWavesPerBlock + wave;
@@ -495,12 +604,9 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   for (int tw = t0; tw < t1; tw += kWave) {
     const int nw = min(kWave, t1 - tw);
     const int tl = tw + min(lane, nw - 1);
-    const int vv = tcol[tl];
-    const int jj = tslot[tl];
-    const int sv = gpos[jj + vv];
-    const int ev = gpos[jj + vv + 1];
+    const int2 gl = glist[tl];
     float wv = 1.f;
-    if constexpr (HAS_W) wv = ew[jj];
+    if constexpr (HAS_W) wv = ew[tslot[tl]];
     for (int j = 0; j < nw; j += U) {
       const int nv = min(U, nw - j);
       int fe[U];
@@ -508,8 +614,8 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
 #pragma unroll
       for (int e = 0; e < U; ++e) {
         const int je = j + min(e, nv - 1);
-        const int64_t base = (int64_t)bcast(vv, je) * F + bcast(sv, je);
-        const int n = bcast(ev, je) - bcast(sv, je);
+        const int base = bcast(gl.x, je);
+        const int n = bcast(gl.y, je);
         const bool on = lane < n;
         fe[e] = on ? (int)gfeat[base + lane] : 0;
         de[e] = on ? dpack[base + lane] : 0.f;
@@ -518,7 +624,7 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
       for (int e = 0; e < U; ++e) {
         if (e < nv) {
           const int je = j + e;
-          const int n = bcast(ev, je) - bcast(sv, je);
+          const int n = bcast(gl.y, je);
           float w = 1.f;
           if constexpr (HAS_W) w = bcastf(wv, je);
           if (lane < n) acc[fe[e]] += HAS_W ? w * de[e] : de[e];
@@ -526,7 +632,7 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
             // long list (one winner takes many features, or low in-degree v): the rest of
             // the list in batches of 8 segments, all loads first; a list holds distinct
             // features, so its segments may be added in any order
-            const int64_t base = (int64_t)bcast(vv, je) * F + bcast(sv, je);
+            const int base = bcast(gl.x, je);
             for (int s0 = kWave; s0 < n; s0 += 8 * kWave) {
               int fs[8];
               float ds[8];
@@ -546,9 +652,7 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
       }
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  wave_lds_sync();
   if (slot < 0) {
     float* xr = dx + (int64_t)row * ldx;
     const float* mr = mask ? mask + (int64_t)row * ldm : nullptr;
@@ -922,7 +1026,8 @@ int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, f
                                  (int32_t*)ws_arg, ldw, st);
 }
 
-// [split-row partials][grouped path: gfeat N x F u16 | gpos (nnz + N) u16 | dpack N x F f32]
+// [split-row partials][grouped path: gfeat N x F u16 | glist nnz x int2 | dpack N x F f32 |
+//  einv nnz x int32 (used when g->einv is NULL)]
 static size_t bwd_partials_bytes(const pg_csr_t* gt, int64_t F) {
   return gt->n_slots > 0 ? round_up(gt->n_slots * ws_ld(F) * 4, 256) : 0;
 }
@@ -932,7 +1037,8 @@ size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
   size_t b = bwd_partials_bytes(gt, F);
   if (F <= kGroupMaxF) {
     const int64_t N = gt->n_cols;
-    b += round_up(N * F * 2, 256) + round_up((gt->nnz + N) * 2, 256) + round_up(N * F * 4, 256);
+    b += round_up(N * F * 2, 256) + round_up(gt->nnz * 8, 256) + round_up(N * F * 4, 256) +
+         round_up(gt->nnz * 4, 256);
   }
   return b;
 }
@@ -962,24 +1068,40 @@ int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, i
     const char* e = getenv("PLAGNN_BWD_PATH");  // tuning knob: "direct" = argmax-row gather
     return e && strcmp(e, "direct") == 0;
   }();
-  if (arg_kind == PG_ARG_U16 && F <= kGroupMaxF && !force_direct) {
-    const int64_t N = g->n_rows;
+  const int64_t N = g->n_rows;
+  if (arg_kind == PG_ARG_U16 && F <= kGroupMaxF && N * F < INT32_MAX && !force_direct) {
     char* p = (char*)ws + pbytes;
     uint16_t* gfeat = (uint16_t*)p;
     p += round_up(N * F * 2, 256);
-    uint16_t* gpos = (uint16_t*)p;
-    p += round_up((g->nnz + N) * 2, 256);
+    int2* glist = (int2*)p;
+    p += round_up(g->nnz * 8, 256);
     float* dpack = (float*)p;
-    hipLaunchKernelGGL((group_pack_kernel<uint16_t>), dim3((unsigned)N), dim3(kBlock), 0, st, g->ptr,
-                       (const uint16_t*)argpos, lda, (int)F, dout, ldd, gfeat, gpos, dpack);
+    p += round_up(N * F * 4, 256);
+    const int32_t* einv = g->einv;
+    if (!einv) {
+      int32_t* e = (int32_t*)p;
+      const int blocks = (int)std::min<int64_t>(4096, (g->nnz + kBlock - 1) / kBlock);
+      if (blocks > 0)
+        hipLaunchKernelGGL(invert_slots_kernel, dim3(blocks), dim3(kBlock), 0, st, gt->eslot, g->nnz, e);
+      einv = e;
+    }
+    const auto* arg16 = (const uint16_t*)argpos;
+    // rows past kPackWaveMax: the schedule's split rows when its chunk guarantees they are
+    // a superset, else every row
+    const bool listed = g->merges != nullptr && g->chunk > 0 && g->chunk <= kPackWaveMax;
+    const int n_long = (int)(listed ? g->n_merges : N);
+    const int n_short_blocks = (int)((N + kWavesPerBlock - 1) / kWavesPerBlock);
+    hipLaunchKernelGGL((group_pack_kernel<uint16_t>), dim3((unsigned)(n_long + n_short_blocks)),
+                       dim3(kBlock), 0, st, listed ? (const int4*)g->merges : nullptr, n_long,
+                       (int)N, g->ptr, einv, arg16, lda, (int)F, dout, ldd, gfeat, glist, dpack);
     const int blocks = grid_for(gt->n_items);
     if (g->ew)
-      hipLaunchKernelGGL((max_bwd_pull_kernel<true>), dim3(blocks), dim3(kBlock), 0, st, g->ew, gt->col,
-                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, gfeat, gpos, dpack,
+      hipLaunchKernelGGL((max_bwd_pull_kernel<true>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
+                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, glist, gfeat, dpack,
                          (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F));
     else
-      hipLaunchKernelGGL((max_bwd_pull_kernel<false>), dim3(blocks), dim3(kBlock), 0, st, g->ew, gt->col,
-                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, gfeat, gpos, dpack,
+      hipLaunchKernelGGL((max_bwd_pull_kernel<false>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
+                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, glist, gfeat, dpack,
                          (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F));
     if (gt->n_merges > 0)
       hipLaunchKernelGGL(sum_merge_kernel, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,

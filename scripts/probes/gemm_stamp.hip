@@ -76,6 +76,19 @@ int main(int argc, char** argv) {
     }
     fclose(g);
   }
+  {
+    std::vector<unsigned long long> ph(64 * 4);
+    (void)hipMemcpyFromSymbol(ph.data(), HIP_SYMBOL(pg_gemm_kphase), ph.size() * 8);
+    std::vector<double> pro, loop, epi;
+    for (int b = 0; b < 64 && b < tiles; ++b) {
+      pro.push_back((double)(ph[b * 4 + 1] - ph[b * 4]));
+      loop.push_back((double)(ph[b * 4 + 2] - ph[b * 4 + 1]));
+      epi.push_back((double)(ph[b * 4 + 3] - ph[b * 4 + 2]));
+    }
+    auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+    printf("   phases (median clocks, first 64 blocks): prologue %.0f  loop %.0f  epilogue %.0f\n",
+           med(pro), med(loop), med(epi));
+  }
   FILE* f = fopen(csv, "w");
   fprintf(f, "block,start_ns,end_ns,clocks,xcc,hw_id\n");
   for (int b = 0; b < tiles && b < 65536; ++b)

@@ -49,8 +49,10 @@ def main():
                              dg.arg_kind, dZ.data_ptr(), F, F, P.data_ptr(), F, dX.data_ptr(), F,
                              ws.data_ptr(), ws.numel(), plagnn._lib.stream_handle(P.device))
         tb = timeit(bwd)
+        ts = timeit(lambda: ops.spmm_max_backward_scatter(dg, arg, dZ, None))
         fb = 4 * (N + 1) + 4 * E + 4 * F * E + 4 * F * N + 2 * F * N
-        print(f"F={F:4d} fwd {tf*1e3:8.1f} us {fb/tf/1e6:8.1f} GB/s | bwd {tb*1e3:8.1f} us")
+        print(f"F={F:4d} fwd {tf*1e3:8.1f} us {fb/tf/1e6:8.1f} GB/s | bwd {tb*1e3:8.1f} us | "
+              f"scatter(atomics, incl. zero-fill) {ts*1e3:8.1f} us")
 
 
 if __name__ == "__main__":
