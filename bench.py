@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown-reps", type=int, default=5)
+    ap.add_argument("--dump-breakdown", default="", help="write the per-launch-site breakdown (JSON)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -160,6 +161,9 @@ def main():
 
     # per-kernel HIP-event breakdown (eager diagnostic steps, after the timed region)
     bd = engine.kernel_breakdown(args.breakdown_reps)
+    if args.dump_breakdown:
+        with open(args.dump_breakdown, "w") as f:
+            json.dump(bd, f, indent=1)
     groups = {}
     for name, r in bd.items():
         gname = _group(name)

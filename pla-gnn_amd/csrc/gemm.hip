@@ -704,30 +704,53 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
 #endif
 }
 
-// Split-K combine: C = alpha * sum_z ws[z] (+ beta * C), slices summed in order; the row
-// sums likewise (their slices follow the partial slabs in the workspace).
+// Split-K combine: C = alpha * sum_z ws[z] (+ beta * C); the row sums likewise (their
+// slices follow the partial slabs in the workspace). G threads per output: thread group g
+// sums slices [S g / G, S (g+1) / G) in order, then one thread adds the G group sums in
+// order (a fixed order: deterministic). Consecutive threads take consecutive outputs, so
+// every slab read is coalesced.
+template <int G>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws,
                                                             int splits, int M, int N, float alpha,
                                                             float beta, float* __restrict__ C,
                                                             int64_t ldc, const float* __restrict__ ws_rowsum,
                                                             float* __restrict__ rowsum) {
+  constexpr int OPB = 256 / G;  // outputs per block
+  __shared__ float part[256];
   const int64_t n = (int64_t)M * N;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n + (rowsum ? M : 0);
-       i += (int64_t)gridDim.x * 256) {
-    if (i >= n) {
-      const int m = (int)(i - n);
-      float s = 0.f;
-      for (int z = 0; z < splits; ++z) s += ws_rowsum[(int64_t)z * M + m];
-      rowsum[m] = s;
-      continue;
-    }
+  const int64_t total = n + (rowsum ? M : 0);
+  const int ol = threadIdx.x % OPB, g = threadIdx.x / OPB;
+  const int z0 = (int)((int64_t)splits * g / G), z1 = (int)((int64_t)splits * (g + 1) / G);
+  for (int64_t base = (int64_t)blockIdx.x * OPB; base < total; base += (int64_t)gridDim.x * OPB) {
+    const int64_t i = base + ol;
     float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += ws[(int64_t)z * n + i];
-    const int64_t r = i / N;
-    const int c = (int)(i - r * N);
-    float v = alpha * s;
-    if (beta != 0.f) v = v + beta * C[r * ldc + c];
-    C[r * ldc + c] = v;
+    if (i < total) {
+      if (i < n) {
+        for (int z = z0; z < z1; ++z) s += ws[(int64_t)z * n + i];
+      } else {
+        for (int z = z0; z < z1; ++z) s += ws_rowsum[(int64_t)z * M + (i - n)];
+      }
+    }
+    if constexpr (G > 1) {
+      part[threadIdx.x] = s;
+      __syncthreads();
+      if (g == 0) {
+#pragma unroll
+        for (int q = 1; q < G; ++q) s += part[q * OPB + ol];
+      }
+      __syncthreads();
+    }
+    if (g == 0 && i < total) {
+      if (i >= n) {
+        rowsum[i - n] = s;
+      } else {
+        const int64_t r = i / N;
+        const int c = (int)(i - r * N);
+        float v = alpha * s;
+        if (beta != 0.f) v = v + beta * C[r * ldc + c];
+        C[r * ldc + c] = v;
+      }
+    }
   }
 }
 
@@ -838,6 +861,18 @@ inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
 
 extern "C" {
 
+int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K < 1024) return 1;
+  int bm, bn;
+  pick_tile(M, N, 1, bm, bn);
+  const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  if (tiles >= 768) return 1;
+  // ~3 workgroups per CU (256 CUs), each slice >= 3 K steps, at most 256 slices
+  const int64_t target = (768 + tiles - 1) / tiles;
+  const int64_t by_k = K / (3 * BK);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, by_k), 256));
+}
+
 size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k) {
   (void)K;
   if (split_k <= 1 || M <= 0 || N <= 0) return 0;
@@ -909,10 +944,18 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_f32: dispatch failed");
   if (split) {
     const int64_t n = M * N + (ep->rowsum ? M : 0);
-    const int blocks = (int)std::min<int64_t>(4096, (n + 255) / 256);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)wsf,
-                       split_k, (int)M, (int)N, alpha, beta, C, ldc, (const float*)a.ws_rowsum,
-                       ep->rowsum);
+    // threads per output: enough slice groups that each thread sums <= ~8 slices
+    const int G = split_k <= 8 ? 1 : split_k <= 32 ? 4 : 16;
+    const int opb = 256 / G;
+    const int blocks = (int)std::min<int64_t>(8192, (n + opb - 1) / opb);
+#define PG_R(G_)                                                                              \
+  hipLaunchKernelGGL(splitk_reduce_kernel<G_>, dim3(blocks), dim3(256), 0, st, (const float*)wsf, \
+                     split_k, (int)M, (int)N, alpha, beta, C, ldc, (const float*)a.ws_rowsum,    \
+                     ep->rowsum)
+    if (G == 1) PG_R(1);
+    else if (G == 4) PG_R(4);
+    else PG_R(16);
+#undef PG_R
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess)

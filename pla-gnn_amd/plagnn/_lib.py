@@ -92,6 +92,7 @@ SIGNATURES = {
                                    _vp, _vp, _i64, _vp, _sz, _vp]),
     "pg_adam_prepare": (_i, [_vp, _d, _d, _d, _vp]),
     "pg_adam_apply": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _d, _d, _d, _d, _vp]),
+    "pg_gemm_f32_split_k": (_i, [_i64, _i64, _i64]),
     "pg_gemm_f32_workspace": (_sz, [_i64, _i64, _i64, _i]),
     "pg_gemm_f32": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _ep,
                          _i, _vp, _sz, _vp]),

@@ -148,12 +148,9 @@ def argpos_to_src(dg: DeviceGraph, argpos: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------ dense
 def _split_k(M: int, N: int, K: int) -> int:
-    """K-split for long-K products (weight gradients): aim at ~512 workgroups of the
-    64 x 128 tile, each keeping >= 512 rows of K."""
-    tiles = ((M + 63) // 64) * ((N + 127) // 128)
-    if K < 2048 or tiles >= 512:
-        return 1
-    return int(max(1, min(32, -(-512 // tiles), K // 512)))
+    """K-split for long-K products (weight gradients): the library's recommendation
+    (pg_gemm_f32_split_k: ~3 workgroups per CU, slices of >= 96 K entries)."""
+    return int(_lib.lib().pg_gemm_f32_split_k(M, N, K))
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = False,
