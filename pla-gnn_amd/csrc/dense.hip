@@ -133,23 +133,22 @@ __global__ __launch_bounds__(kBlock) void sigmoid_zero_kernel(const float* __res
   }
 }
 
-// pass 2: block b owns indexed rows [b*R, b*R+R); one thread per (row, class) pair writes
-// the pair's loss term into LDS and its gradient into dz; then thread c < C sums its
-// class over the block's rows in row order (deterministic), giving part[b][c].
+// pass 2: block b owns indexed rows [b*R, b*R+R), R = 256 / C; one thread per (row, class)
+// pair writes the pair's loss term into LDS and its gradient into dz; then thread c < C
+// sums its class over the block's rows in row order (deterministic), giving part[b][c].
 // Mirrors the autograd graph of code/train.py:103-104 operation by operation.
-constexpr int kLossTerms = 4096;  // (row, class) terms per block held in LDS
-// rows per block: as many as fit kLossTerms, at most 256
-inline __host__ __device__ int loss_rows(int C) { return C * 256 <= kLossTerms ? 256 : kLossTerms / C; }
+inline __host__ __device__ int loss_rows(int C) { return C >= kBlock ? 1 : kBlock / C; }
 __global__ __launch_bounds__(kBlock) void multi_loss_kernel(
     const float* __restrict__ z, int64_t ldz, int C, const float* __restrict__ labels,
     int64_t ldl, const float* __restrict__ cw, const int32_t* __restrict__ index, int64_t n_index,
     float* __restrict__ part, float* __restrict__ dz, int64_t lddz) {
-  __shared__ float terms[kLossTerms];
-  const int kLossRows = loss_rows(C);
-  const int64_t r0 = (int64_t)blockIdx.x * kLossRows;
-  const int nr = (int)min<int64_t>(kLossRows, n_index - r0);
+  __shared__ float terms[kBlock];
+  const int R = loss_rows(C);
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int nr = (int)min<int64_t>(R, n_index - r0);
   const float inv_n = 1.0f / (float)n_index;
-  for (int p = threadIdx.x; p < nr * C; p += kBlock) {
+  const int p = threadIdx.x;
+  if (p < nr * C) {
     const int ri = p / C;
     const int c = p - ri * C;
     const int64_t r = index[r0 + ri];
@@ -186,19 +185,30 @@ __global__ __launch_bounds__(kBlock) void multi_loss_kernel(
   }
 }
 
-// pass 3: one wave; lane c sums class c over the blocks in order, lane 0 adds classes.
-__global__ __launch_bounds__(64) void multi_loss_final_kernel(const float* __restrict__ part,
-                                                              int nb, int C, int64_t n_index,
-                                                              float* __restrict__ loss) {
+// pass 3, one workgroup: G = 256 / C thread groups per class; group g sums blocks
+// [nb g / G, nb (g+1) / G) in order, then thread c adds the G group sums in order and
+// thread 0 the classes in order.
+__global__ __launch_bounds__(kBlock) void multi_loss_final_kernel(const float* __restrict__ part,
+                                                                  int nb, int C, int64_t n_index,
+                                                                  float* __restrict__ loss) {
+  __shared__ float gs[kBlock];
   __shared__ float cls[64];
-  const int c = threadIdx.x;
-  if (c < C) {
-    float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += part[(int64_t)b * C + c];
-    cls[c] = -s / (float)n_index;
+  const int G = kBlock / C;
+  const int c = threadIdx.x % C, g = threadIdx.x / C;
+  float s = 0.f;
+  if (g < G) {
+    const int b0 = (int)((int64_t)nb * g / G), b1 = (int)((int64_t)nb * (g + 1) / G);
+    for (int b = b0; b < b1; ++b) s += part[(int64_t)b * C + c];
+  }
+  gs[threadIdx.x] = s;
+  __syncthreads();
+  if ((int)threadIdx.x < C) {
+    float t = 0.f;
+    for (int q = 0; q < G; ++q) t += gs[q * C + threadIdx.x];
+    cls[threadIdx.x] = -t / (float)n_index;
   }
   __syncthreads();
-  if (c == 0) {
+  if (threadIdx.x == 0) {
     float total = 0.f;
     for (int k = 0; k < C; ++k) total += cls[k];
     loss[0] = total;
@@ -326,7 +336,7 @@ int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C
     hipLaunchKernelGGL(multi_loss_kernel, dim3(nb), dim3(kBlock), 0, st, z, ldz, (int)C, labels, ldl,
                        class_w, index, n_index, part, dz, lddz);
     if (loss)
-      hipLaunchKernelGGL(multi_loss_final_kernel, dim3(1), dim3(64), 0, st, (const float*)part, nb,
+      hipLaunchKernelGGL(multi_loss_final_kernel, dim3(1), dim3(kBlock), 0, st, (const float*)part, nb,
                          (int)C, n_index, loss);
   }
   return hip_status("pg_sigmoid_multi_loss");

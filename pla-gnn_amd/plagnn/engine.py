@@ -80,6 +80,12 @@ class TrainEngine:
         self.C = C
         dev = self.device
         pd = [round4(d) for d in self.dims]
+        # SAGE layer inputs: a multiple of 64 when that costs <= 2 % more columns (503 -> 512):
+        # whole feature tiles for the SpMM kernels; pads are zero and stay zero
+        for l in range(self.L):
+            r64 = -(-self.dims[l] // 64) * 64
+            if r64 <= 1.02 * self.dims[l]:
+                pd[l] = r64
         self.pd = pd
 
         # ---- parameters (flat, padded) ----
@@ -413,16 +419,17 @@ class TrainEngine:
 
     def spmm_bytes(self, layer: int) -> int:
         """Algorithmic HBM bytes of one max-aggregation forward:
-        4(N+1) + 4E' + s*F*E' + s*F*N + a*F*N, s = 4 (f32), a = argpos bytes."""
-        N, E, F = self.N, self.dg.num_edges, self.pd[layer]
+        4(N+1) + 4E' + s*F*E' + s*F*N + a*F*N, s = 4 (f32), a = argpos bytes, at the true
+        (unpadded) width F."""
+        N, E, F = self.N, self.dg.num_edges, self.dims[layer]
         a = 2 if self.dg.arg_kind == _lib.PG_ARG_U16 else 4
         return 4 * (N + 1) + 4 * E + 4 * F * E + 4 * F * N + a * F * N
 
     def spmm_bwd_bytes(self, layer: int) -> int:
         """Algorithmic bytes of one max backward: the upstream gradient
         and the argmax record read once (s*F*N + a*F*N), dX written once (s*F*N), plus
-        the fused relu mask (s*F*N) and the transposed CSR (4(N+1) + 8E')."""
-        N, E, F = self.N, self.dg.num_edges, self.pd[layer]
+        the fused relu mask (s*F*N) and the transposed CSR (4(N+1) + 8E'), true width F."""
+        N, E, F = self.N, self.dg.num_edges, self.dims[layer]
         a = 2 if self.dg.arg_kind == _lib.PG_ARG_U16 else 4
         return 4 * (N + 1) + 8 * E + (12 + a) * F * N
 
