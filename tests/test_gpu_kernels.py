@@ -22,7 +22,7 @@ def _graph(src, dst, n, chunk=256):
     return plagnn.CSRGraph(src, dst, n, chunk=chunk)
 
 
-@pytest.mark.parametrize("F", [1, 3, 63, 64, 65, 256, 300, 400, 503, 504, 512, 1100])
+@pytest.mark.parametrize("F", [1, 3, 63, 64, 65, 128, 256, 300, 400, 503, 504, 512, 1100])
 def test_spmm_max_fwd_bitexact(oracle_mod, F):
     from plagnn import ops
 
@@ -39,6 +39,36 @@ def test_spmm_max_fwd_bitexact(oracle_mod, F):
     ref, argx, arge = oracle_mod.spmm_max(og, X)
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
     np.testing.assert_array_equal(ops.argpos_to_src(dg, argpos).cpu().numpy(), argx)
+
+
+@pytest.mark.parametrize("F", [64, 65, 256])
+def test_spmm_max_fwd_special_values(oracle_mod, F):
+    """-inf / +inf / NaN entries: strict > never selects NaN or -inf, and a +-inf result is
+    stored as 0 (DGL replace_inf_with_zero). A feature with no winner (all inputs -inf or
+    NaN) records "none" (-1 from argpos_to_src) where DGL leaves argX at its initial 0;
+    unreachable on the reference path (self-loops and relu outputs >= 0)."""
+    from plagnn import ops
+
+    n = 300
+    src, dst = hub_graph(n, 900, seed=7 + F)
+    g = _graph(src, dst, n)
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False)
+    rng = np.random.default_rng(F)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    r = rng.random((n, F))
+    X[r < 0.1] = -np.inf
+    X[(r >= 0.1) & (r < 0.15)] = np.nan
+    X[(r >= 0.15) & (r < 0.17)] = np.inf
+    X[:, 0] = -np.inf  # a column no row can win
+    dg = g.on(DEV)
+    out, argpos = ops.spmm_max(dg, torch.from_numpy(X).to(DEV))
+    ref, argx, _ = oracle_mod.spmm_max(og, X)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    got = ops.argpos_to_src(dg, argpos).cpu().numpy()
+    won = got >= 0
+    np.testing.assert_array_equal(got[won], argx[won])
+    assert np.all(argx[~won] == 0) and np.all(ref[~won] == 0)
+    assert np.all(~won[:, 0]) and won.mean() > 0.5
 
 
 @pytest.mark.parametrize("F", [4, 65, 256, 503])
