@@ -601,53 +601,50 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   const int lane = lane_id();
   for (int f = lane; f < F; f += kWave) acc[f] = 0.f;
 
+  // Each window of 64 out-edges is flattened into "segments" (64-entry pieces of the
+  // edges' lists, edge-major; empty lists have none) and the segments are processed U at
+  // a time: all their loads first, then their LDS adds in order. Long lists no longer
+  // serialise a memory round trip per 64 entries, and edges that win nothing cost
+  // nothing. Segment t belongs to the edge i with excl_i <= t < excl_i + nseg_i, i.e.
+  // i = popcount(ballot(excl <= t)) - 1.
   for (int tw = t0; tw < t1; tw += kWave) {
     const int nw = min(kWave, t1 - tw);
     const int tl = tw + min(lane, nw - 1);
     const int2 gl = glist[tl];
     float wv = 1.f;
     if constexpr (HAS_W) wv = ew[tslot[tl]];
-    for (int j = 0; j < nw; j += U) {
-      const int nv = min(U, nw - j);
-      int fe[U];
+    const int nseg = lane < nw ? (gl.y + kWave - 1) / kWave : 0;
+    int incl = nseg;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    const int excl = incl - nseg;
+    const int T = bcast(incl, kWave - 1);
+    for (int s0 = 0; s0 < T; s0 += U) {
+      const int nv = min(U, T - s0);
+      int fe[U], ie[U], ne[U];
       float de[U];
 #pragma unroll
-      for (int e = 0; e < U; ++e) {
-        const int je = j + min(e, nv - 1);
-        const int base = bcast(gl.x, je);
-        const int n = bcast(gl.y, je);
+      for (int u = 0; u < U; ++u) {
+        const int t = s0 + min(u, nv - 1);
+        const int i = __popcll(__ballot(excl <= t)) - 1;
+        const int seg = t - bcast(excl, i);
+        const int base = bcast(gl.x, i) + seg * kWave;
+        const int n = min(kWave, bcast(gl.y, i) - seg * kWave);
+        ie[u] = i;
+        ne[u] = n;
         const bool on = lane < n;
-        fe[e] = on ? (int)gfeat[base + lane] : 0;
-        de[e] = on ? dpack[base + lane] : 0.f;
+        fe[u] = on ? (int)gfeat[base + lane] : 0;
+        de[u] = on ? dpack[base + lane] : 0.f;
       }
 #pragma unroll
-      for (int e = 0; e < U; ++e) {
-        if (e < nv) {
-          const int je = j + e;
-          const int n = bcast(gl.y, je);
+      for (int u = 0; u < U; ++u) {
+        if (u < nv && lane < ne[u]) {
           float w = 1.f;
-          if constexpr (HAS_W) w = bcastf(wv, je);
-          if (lane < n) acc[fe[e]] += HAS_W ? w * de[e] : de[e];
-          if (n > kWave) {
-            // long list (one winner takes many features, or low in-degree v): the rest of
-            // the list in batches of 8 segments, all loads first; a list holds distinct
-            // features, so its segments may be added in any order
-            const int base = bcast(gl.x, je);
-            for (int s0 = kWave; s0 < n; s0 += 8 * kWave) {
-              int fs[8];
-              float ds[8];
-#pragma unroll
-              for (int q = 0; q < 8; ++q) {
-                const int idx = s0 + q * kWave + lane;
-                const bool on = idx < n;
-                fs[q] = on ? (int)gfeat[base + idx] : 0;
-                ds[q] = on ? dpack[base + idx] : 0.f;
-              }
-#pragma unroll
-              for (int q = 0; q < 8; ++q)
-                if (s0 + q * kWave + lane < n) acc[fs[q]] += HAS_W ? w * ds[q] : ds[q];
-            }
-          }
+          if constexpr (HAS_W) w = bcastf(wv, ie[u]);
+          acc[fe[u]] += HAS_W ? w * de[u] : de[u];
         }
       }
     }
