@@ -402,26 +402,37 @@ __device__ __forceinline__ void pack_short_row(
     int* __restrict__ lds) {
   constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
   const int lane = lane_id();
+  // every independent load first: the row bounds, the argmax record and the upstream
+  // gradient (each lane its own features, coalesced), then the list descriptors' slots
   const int rs = ptr[v];
-  const int deg = ptr[v + 1] - rs;
-  if (deg > kPackWaveMax || deg == 0) return;
-  int* hist = lds + wave * (kPackWaveMax + 4 + kGroupMaxF / 2);
-  uint16_t* feats = reinterpret_cast<uint16_t*>(hist + kPackWaveMax + 4);
-  for (int p = lane; p < deg; p += kWave) hist[p] = 0;
-  wave_lds_sync();
+  const int re = ptr[v + 1];
   const A* ar = arg + (int64_t)v * lda;
+  const float* dr = dout + (int64_t)v * ldd;
   int a[MAXW];
+  float d[MAXW];
 #pragma unroll
   for (int i = 0; i < MAXW; ++i) {
     const int f = lane + i * kWave;
     a[i] = f < F ? (int)ar[f] : arg_none<A>();
+    d[i] = f < F ? dr[f] : 0.f;
   }
+  const int deg = re - rs;
+  if (deg > kPackWaveMax || deg == 0) return;
+  const int B = (deg + kWave - 1) / kWave;  // bins per lane, <= 4
+  int ei[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = lane * B + q;
+    ei[q] = (q < B && p < deg) ? einv[rs + p] : 0;
+  }
+  int* hist = lds + wave * (kPackWaveMax + 4);
+  for (int p = lane; p < deg; p += kWave) hist[p] = 0;
+  wave_lds_sync();
 #pragma unroll
   for (int i = 0; i < MAXW; ++i)
     if (a[i] != arg_none<A>()) atomicAdd(&hist[a[i]], 1);
   wave_lds_sync();
   // exclusive scan over the deg bins: lane owns bins [lane B, lane B + B)
-  const int B = (deg + kWave - 1) / kWave;  // <= 4
   int c[4], local = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -435,7 +446,6 @@ __device__ __forceinline__ void pack_short_row(
     const int y = __shfl_up(x, o);
     if (lane >= o) x += y;
   }
-  const int total = __shfl(x, kWave - 1);
   int run = x - local;
   const int vF = v * F;
 #pragma unroll
@@ -443,26 +453,21 @@ __device__ __forceinline__ void pack_short_row(
     const int p = lane * B + q;
     if (q < B && p < deg) {
       hist[p] = run;
-      glist[einv[rs + p]] = make_int2(vF + run, c[q]);
+      glist[ei[q]] = make_int2(vF + run, c[q]);
       run += c[q];
     }
   }
   wave_lds_sync();
+  // placement: every winner straight to its list slot (the order inside a list is free)
 #pragma unroll
   for (int i = 0; i < MAXW; ++i)
-    if (a[i] != arg_none<A>()) feats[atomicAdd(&hist[a[i]], 1)] = (uint16_t)(lane + i * kWave);
-  wave_lds_sync();
-  const float* dr = dout + (int64_t)v * ldd;
-  for (int i = lane; i < total; i += kWave) {
-    const int f = feats[i];
-    gfeat[(int64_t)vF + i] = (uint16_t)f;
-    dpack[(int64_t)vF + i] = dr[f];
-  }
+    if (a[i] != arg_none<A>()) {
+      const int pos = vF + atomicAdd(&hist[a[i]], 1);
+      gfeat[pos] = (uint16_t)(lane + i * kWave);
+      dpack[pos] = d[i];
+    }
 }
 
-// Rows longer than kPackWaveMax, one workgroup each: `rows` lists them ({row, ...} int4,
-// the split-row merges of a schedule whose chunk <= kPackWaveMax), or NULL = every row
-// (short ones exit at once).
 template <typename A>
 __device__ __forceinline__ void pack_long_row(
     int v, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
@@ -479,25 +484,51 @@ __device__ __forceinline__ void pack_long_row(
   const int vF = v * F;
   int total;
   if (deg <= kHistMax) {
+    // independent loads first (each thread its own features), placement straight to the
+    // list slots as in the wave form
+    constexpr int FPT = kGroupMaxF / kBlock;
+    const float* dr = dout + (int64_t)v * ldd;
+    int a[FPT];
+    float d[FPT];
+#pragma unroll
+    for (int i = 0; i < FPT; ++i) {
+      const int f = threadIdx.x + i * kBlock;
+      a[i] = f < F ? (int)ar[f] : arg_none<A>();
+      d[i] = f < F ? dr[f] : 0.f;
+    }
     for (int p = threadIdx.x; p < deg; p += kBlock) hist[p] = 0;
     __syncthreads();
-    for (int f = threadIdx.x; f < F; f += kBlock) {
-      const int a = (int)ar[f];
-      if (a != arg_none<A>()) atomicAdd(&hist[a], 1);
-    }
+#pragma unroll
+    for (int i = 0; i < FPT; ++i)
+      if (a[i] != arg_none<A>()) atomicAdd(&hist[a[i]], 1);
     __syncthreads();
     total = block_exclusive_scan(hist, deg, wsum);
-    for (int p = threadIdx.x; p < deg; p += kBlock) {
-      const int st = hist[p];
-      const int en = p + 1 < deg ? hist[p + 1] : total;
-      glist[einv[rs + p]] = make_int2(vF + st, en - st);
+    for (int p0 = threadIdx.x; p0 < deg; p0 += 4 * kBlock) {
+      int e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = p0 + j * kBlock;
+        e[j] = p < deg ? einv[rs + p] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = p0 + j * kBlock;
+        if (p < deg) {
+          const int st = hist[p];
+          const int en = p + 1 < deg ? hist[p + 1] : total;
+          glist[e[j]] = make_int2(vF + st, en - st);
+        }
+      }
     }
     __syncthreads();
-    for (int f = threadIdx.x; f < F; f += kBlock) {
-      const int a = (int)ar[f];
-      if (a != arg_none<A>()) feats[atomicAdd(&hist[a], 1)] = (uint16_t)f;
-    }
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FPT; ++i)
+      if (a[i] != arg_none<A>()) {
+        const int pos = vF + atomicAdd(&hist[a[i]], 1);
+        gfeat[pos] = (uint16_t)(threadIdx.x + i * kBlock);
+        dpack[pos] = d[i];
+      }
+    return;
   } else {
     // hub row: bitonic sort of (p << 16 | f) keys; "none" sorts last
     uint32_t* keys = reinterpret_cast<uint32_t*>(hist);
@@ -558,7 +589,7 @@ __device__ __forceinline__ void pack_long_row(
 // kPackWaveMax; NULL = every row, short ones exit at once) so the long rows start first;
 // the remaining blocks take 4 rows each, one wave per row.
 constexpr int kPackLds = kHistMax + 8 + kGroupMaxF / 2 + 4;
-static_assert(kPackLds >= kWavesPerBlock * (kPackWaveMax + 4 + kGroupMaxF / 2), "pack LDS");
+static_assert(kPackLds >= kWavesPerBlock * (kPackWaveMax + 4), "pack LDS");
 
 template <typename A>
 __global__ __launch_bounds__(kBlock) void group_pack_kernel(

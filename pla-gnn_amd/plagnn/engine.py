@@ -25,6 +25,7 @@ stay exactly zero through forward, backward and Adam):
 from __future__ import annotations
 
 import contextlib
+import os
 from collections import defaultdict
 from typing import Dict, List, Optional, Sequence
 
@@ -167,6 +168,16 @@ class TrainEngine:
         need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
         self.ws_bytes = self.ws.numel()
+        # PLAGNN_OVERLAP=1: weight gradients on a side stream, off the critical path (dgrad ->
+        # SpMM backward -> dgrad ...), with their own split-K workspace. Off by default: on
+        # one MI355X the captured step measured 2.125 ms with it vs 2.092 ms without (the
+        # GEMMs already fill the chip and crowd the latency-bound SpMM kernels).
+        self.overlap = os.environ.get("PLAGNN_OVERLAP", "0") == "1"
+        self.side = torch.cuda.Stream(dev) if self.overlap else None
+        need2 = 256
+        for (M_, N_, K_), sk in self._gemm_plans.items():
+            need2 = max(need2, L.pg_gemm_f32_workspace(M_, N_, K_, sk))
+        self.ws2 = torch.zeros(int(need2), dtype=torch.uint8, device=dev) if self.overlap else self.ws
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_adam: Optional[torch.cuda.CUDAGraph] = None
         self.allreduce = None
@@ -267,15 +278,35 @@ class TrainEngine:
         return _lib.stream_handle(self.device)
 
     def _gemm(self, A, B, C, transa=False, transb=False, beta=0.0, bias=None, act=NONE, dact=None,
-              rowsum=None, tag="gemm"):
+              rowsum=None, tag="gemm", ws=None):
         M = A.shape[1] if transa else A.shape[0]
         K = A.shape[0] if transa else A.shape[1]
         N = B.shape[0] if transb else B.shape[1]
         sk = self._gemm_plans.get((M, N, K), 1) if (bias is None and act == NONE and dact is None) else 1
         ep = _lib.epilogue(bias, act, LEAKY_SLOPE, dact, rowsum)
+        ws = self.ws if ws is None else ws
         with self._t(tag, 2.0 * M * N * K):
             call("pg_gemm_f32", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
-                 B.stride(0), beta, ptr(C), C.stride(0), ep, sk, ptr(self.ws), self.ws_bytes, self._s())
+                 B.stride(0), beta, ptr(C), C.stride(0), ep, sk, ptr(ws), ws.numel(), self._s())
+
+    def _wgrad(self, *args, **kw):
+        """A weight-gradient GEMM: forked onto the side stream at this point of the main
+        stream (it sees everything issued so far), joined back before Adam (_join)."""
+        if not self.overlap:
+            self._gemm(*args, **kw)
+            return
+        main = torch.cuda.current_stream(self.device)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            self._gemm(*args, ws=self.ws2, **kw)
+
+    def _join(self):
+        if self.overlap:
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+            torch.cuda.current_stream(self.device).wait_event(ev)
 
     def forward(self) -> None:
         """Logits (self.prob) and both losses; dZ = d train_loss / d z."""
@@ -319,10 +350,10 @@ class TrainEngine:
         g = self.dg.fwd.struct(self.ews)
         gt = self.dg.bwd.struct(None)
         # liner2: dW2 = dZ^T A4 (+ db2 = row sums of dZ^T); dA4 = (dZ W2) * leaky'(A4)
-        self._gemm(self.dZ, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
+        self._wgrad(self.dZ, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
         self._gemm(self.dZ, P["liner2.W"], self.dA4, act=LEAKY, dact=self.A4, tag="gemm.dgrad.liner2")
         # liner1
-        self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
+        self._wgrad(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
         self._gemm(self.dA4, P["liner1.W"], self.dA3, act=LEAKY, dact=self.A3, tag="gemm.dgrad.liner1")
         dY = self.dA3
         for l in reversed(range(self.L)):
@@ -330,7 +361,7 @@ class TrainEngine:
             Fi = pd[l]
             HM, dHM = self.HM[l], self.dHM[l]
             # d Wcat = dY^T [H | M], d b = sum_nodes dY
-            self._gemm(dY, HM, G[p + "Wcat"], transa=True, rowsum=G[p + "b"], tag=f"gemm.wgrad.cat.l{l + 1}")
+            self._wgrad(dY, HM, G[p + "Wcat"], transa=True, rowsum=G[p + "b"], tag=f"gemm.wgrad.cat.l{l + 1}")
             # d[H | M] = dY Wcat   (layer 1: only dM is needed)
             if l > 0:
                 self._gemm(dY, P[p + "Wcat"], dHM, tag=f"gemm.dgrad.cat.l{l + 1}")
@@ -342,14 +373,15 @@ class TrainEngine:
                      dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(self.dP[l]), Fi, ptr(self.ws),
                      self.ws_bytes, st)
             # d Wpool = dP^T H, d bpool = sum_nodes dP
-            self._gemm(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
-                       tag=f"gemm.wgrad.pool.l{l + 1}")
+            self._wgrad(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
+                        tag=f"gemm.wgrad.pool.l{l + 1}")
             if l > 0:
                 # dH = (dH_self + dP Wpool) * leaky'(H): H is the previous layer's output
                 dH = dHM[:, :Fi]
                 self._gemm(self.dP[l], P[p + "Wpool"], dH, beta=1.0, act=LEAKY, dact=HM[:, :Fi],
                            tag=f"gemm.dgrad.pool.l{l + 1}")
                 dY = dH
+        self._join()
 
     def adam(self) -> None:
         st = self._s()
