@@ -225,7 +225,7 @@ typedef struct pg_gemm_epilogue {
  * When split_k > 1, beta must be 0 or 1 and the epilogue may only carry rowsum (partials
  * are combined in the workspace, in slice order: deterministic). */
 /* Recommended split_k for pg_gemm_f32 (long-K products such as weight gradients):
- * about three workgroups per CU, each slice >= 96 entries of K, at most 256. */
+ * about five 64 x 64 workgroups per CU, each slice >= 96 entries of K, at most 256. */
 int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K);
 size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k);
 int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,

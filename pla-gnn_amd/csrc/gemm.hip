@@ -835,10 +835,12 @@ int launch_trans(bool ta, bool tb, bool va, bool vb, int epi, dim3 grid, hipStre
   return launch_vec<BM, BN, true, true>(va, vb, epi, grid, st, a);
 }
 
-// Tile choice: BN = 64 for outputs up to 128 columns wide, else 128; BM = 128 only when
-// that still gives at least ~3 workgroups per CU (256 CUs), so skinny-N products keep the
-// chip filled.
-inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
+// Tile choice (measured on the PLA-GNN step shapes, scripts/gemm_bench.py): split-K
+// products (weight gradients) 64 x 64; outputs wider than 512 columns 128 x 128 when that
+// still gives >= 3 workgroups per CU, else 64 x 128; 129..512 columns with short K
+// 128 x 64 (again if >= 768 tiles); everything else 64 x 64 (5 workgroups per CU: long-K
+// and small products balance best on the finest tile).
+inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& bn) {
   // tuning knob PLAGNN_GEMM_TILE = "BMxBN" (64|128 each) forces a tile
   static const int forced = [] {
     const char* e = getenv("PLAGNN_GEMM_TILE");
@@ -852,9 +854,15 @@ inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
     bn = forced % 1000;
     return;
   }
-  bn = N <= 128 ? 64 : 128;
-  const int64_t tiles128 = ((M + 127) / 128) * ((N + bn - 1) / bn) * split;
-  bm = tiles128 >= 3 * 256 ? 128 : 64;
+  auto tiles = [&](int tm, int tn) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
+  bm = bn = 64;
+  if (split > 1) return;
+  if (N > 512) {
+    bn = 128;
+    bm = tiles(128, 128) >= 3 * 256 ? 128 : 64;
+  } else if (N > 128 && K < 1024 && tiles(128, 64) >= 3 * 256) {
+    bm = 128;
+  }
 }
 
 }  // namespace
@@ -864,11 +872,17 @@ extern "C" {
 int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K < 1024) return 1;
   int bm, bn;
-  pick_tile(M, N, 1, bm, bn);
-  const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
-  if (tiles >= 768) return 1;
-  // ~3 workgroups per CU (256 CUs), each slice >= 3 K steps, at most 256 slices
-  const int64_t target = (768 + tiles - 1) / tiles;
+  pick_tile(M, N, K, 1, bm, bn);
+  if (((M + bm - 1) / bm) * ((N + bn - 1) / bn) >= 768) return 1;
+  // split products run 64 x 64 tiles: ~5 workgroups per CU (256 CUs), each slice >= 3 K
+  // steps, at most 256 slices
+  const int64_t tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  static const int64_t want = [] {  // tuning knob PLAGNN_SPLIT_TARGET: workgroups aimed at
+    const char* e = getenv("PLAGNN_SPLIT_TARGET");
+    const int64_t v = e ? atoll(e) : 1280;
+    return v > 0 ? v : 1280;
+  }();
+  const int64_t target = (want + tiles - 1) / tiles;
   const int64_t by_k = K / (3 * BK);
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, by_k), 256));
 }
@@ -914,7 +928,7 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   }
   const bool split = split_k > 1;
   int bm, bn;
-  pick_tile(M, N, split_k, bm, bn);
+  pick_tile(M, N, K, split_k, bm, bn);
   const int tiles_n = (int)((N + bn - 1) / bn);
   const int tiles = tiles_n * (int)((M + bm - 1) / bm);
   dim3 grid((unsigned)tiles, 1, (unsigned)split_k);

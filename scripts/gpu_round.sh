@@ -11,9 +11,9 @@ rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -ge 2 ]; then echo "pytest crashed/timed out; stopping"; exit $rc; fi
 if [ "${GEMM_BENCH:-0}" = "1" ]; then
-  for cfg in "" ${GEMM_VARIANTS:-"PLAGNN_GEMM_TILE=128x128" "PLAGNN_GEMM_TILE=64x64"}; do
+  for cfg in "" ${GEMM_VARIANTS:-"PLAGNN_GEMM_TILE=128x128" "PLAGNN_GEMM_TILE=64x64" "PLAGNN_GEMM_TILE=128x64" "PLAGNN_GEMM_TILE=64x128"}; do
     echo "== $cfg" >> gpurun_out/gemm_bench.txt
-    env $cfg timeout -k 10 300 python scripts/gemm_bench.py >> gpurun_out/gemm_bench.txt 2>&1
+    env $cfg timeout -k 10 300 python scripts/gemm_bench.py --no-torch --dims 512,256,256,256,100,12 >> gpurun_out/gemm_bench.txt 2>&1
     rcg=$?; if [ $rcg -ne 0 ]; then echo "gemm_bench rc=$rcg"; tail gpurun_out/gemm_bench.txt; exit $rcg; fi
   done
   grep -v amdgpu.ids gpurun_out/gemm_bench.txt

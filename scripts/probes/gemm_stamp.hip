@@ -50,7 +50,7 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> st(65536 * 4);
   (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(pg_gemm_stamp), st.size() * 8);
   int bm, bn;
-  pick_tile(M, N, 1, bm, bn);
+  pick_tile(M, N, K, 1, bm, bn);
   const int tiles = (int)(((M + bm - 1) / bm) * ((N + bn - 1) / bn));
   unsigned long long t0 = ~0ull, t1 = 0;
   double ck = 0, dur = 0;
