@@ -32,6 +32,10 @@
  *   pg_col_sum           <- bias gradients (sum of dY over nodes)
  *   pg_gemm_f32          <- nn.Linear GEMMs (fc_pool / fc_self / fc_neigh / liner1-2),
  *                           fp32 MFMA (v_mfma_f32_32x32x2_f32), exact f32
+ *   pg_ecc               <- edge_clustering_coefficients (code/data_preprocess.py:175-214),
+ *                           the ECC feature / edge-weight front end
+ *   pg_loc_correction,   <- protein_loc_correction / performances_record
+ *   pg_loc_performance      (code/train.py:19-86), the per-epoch eval
  *
  * Conventions
  *   - All buffers are caller-owned. Device entry points take device pointers and
@@ -243,6 +247,35 @@ int pg_spmm_sum_cpu(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, i
                     const int32_t* norm_ptr, float* out, int64_t ldo);
 int pg_argpos_to_src_cpu(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,
                          int64_t F, int64_t* argx, int64_t ldx);
+
+/* ---------------- device: §8f — edge clustering coefficient ---------------- */
+
+/* code/data_preprocess.py:175-214 edge_clustering_coefficients on a symmetric adjacency
+ * in CSR form (sorted, unique column ids per row):
+ *   ecc[k] for entry k = (i, j), i != j:
+ *     epsilon if min(deg_i, deg_j) - 1 == 0, else |N(i) ∩ N(j)| / (min(deg_i, deg_j) - 1)
+ *   deg = row sums of the stored values (NULL: row lengths); diagonal entries get 0.
+ * mirror[k] = index of the entry (j, i); order = rows longest first (optional, speed only).
+ * n <= 2^22 (the neighbour bitmap of a row lives in LDS). Bit-exact (integer counts, one
+ * f64 division). */
+int pg_ecc(const int32_t* ptr, const int32_t* col, const int32_t* mirror, const double* deg,
+           const int32_t* order, int64_t n, int64_t nnz, double epsilon, double* ecc,
+           pg_stream_t stream);
+
+/* ---------------- device: §8f — per-epoch evaluation ---------------- */
+
+/* code/train.py:19-39 protein_loc_correction on proba[n][C] (float32, C <= 64):
+ *   new = (p - colmin) / (colmax - colmin); new /= rowsum(new);
+ *   pred[r][c] = new > rowmax - (rowmax - rowmin) * (float)alpha ? 1.0 : 0.0  (float64)
+ * code/train.py:42-86 performances_record: out3 = {aim, coverage, accuracy}, the row terms
+ * summed in row order in float32 and divided by n, as the reference's running scalars.
+ * Scratch: pg_loc_eval_workspace(n, C) bytes. */
+size_t pg_loc_eval_workspace(int64_t n, int32_t C);
+int pg_loc_correction(const float* proba, int64_t ldp, int64_t n, int32_t C, double alpha,
+                      double* pred, int64_t ldpred, void* ws, size_t ws_bytes, pg_stream_t stream);
+int pg_loc_performance(const float* loc_true, int64_t ldt, const double* loc_pred, int64_t ldp,
+                       int64_t n, int32_t C, double* out3, void* ws, size_t ws_bytes,
+                       pg_stream_t stream);
 
 /* ---------------- misc ---------------- */
 const char* pg_last_error_string(void);

@@ -69,6 +69,9 @@ def lib():
         L.oracle_spmm_sum.argtypes = [_i64p, _i64p, _i64p, _f32p, _f32p, ctypes.c_int64, ctypes.c_int64,
                                       ctypes.c_int, _f32p]
         L.oracle_spmm_sum.restype = None
+        _f64p = ctypes.POINTER(ctypes.c_double)
+        L.oracle_ecc.argtypes = [_i64p, _i64p, _f64p, ctypes.c_int64, ctypes.c_double, _i64p, _i64p, _f64p]
+        L.oracle_ecc.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -266,3 +269,59 @@ def train_step(g: OracleGraph, x: torch.Tensor, labels: torch.Tensor, train_inde
     loss = multi_loss(logits[train_index], labels[train_index], i_weight)
     loss.backward()
     return logits.detach(), loss.detach(), {k: v.grad.detach() for k, v in leaves.items()}
+
+
+# ---------------------------------------------------------------- §8f: ECC and eval
+def edge_clustering_coefficients(ppi_net, epsilon: float = 0.0):
+    """code/data_preprocess.py:175-214 (C restatement, oracle/ecc_oracle.c): scipy COO."""
+    from scipy.sparse import coo_matrix
+
+    csr = ppi_net.tocsr()
+    n = csr.shape[0]
+    indptr = np.ascontiguousarray(csr.indptr, np.int64)
+    indices = np.ascontiguousarray(csr.indices, np.int64)
+    data = np.ascontiguousarray(csr.data, np.float64)
+    cap = max(1, 2 * len(indices))
+    rows, cols = np.empty(cap, np.int64), np.empty(cap, np.int64)
+    vals = np.empty(cap, np.float64)
+    m = lib().oracle_ecc(_p(indptr, _i64p), _p(indices, _i64p), _p(data, ctypes.POINTER(ctypes.c_double)), n,
+                         float(epsilon), _p(rows, _i64p), _p(cols, _i64p),
+                         _p(vals, ctypes.POINTER(ctypes.c_double)))
+    if m < 0:
+        raise MemoryError("oracle_ecc")
+    return coo_matrix((vals[:m], (rows[:m], cols[:m])), shape=csr.shape)
+
+
+def protein_loc_correction(loc_proba: torch.Tensor, alpha: float) -> torch.Tensor:
+    """code/train.py:19-39, the same torch-CPU float32 operations (rows vectorised; the
+    per-row threshold loop of the reference is a row-wise comparison)."""
+    loc_proba = loc_proba.detach().cpu().float()
+    min_proba = loc_proba.min(dim=0).values
+    max_proba = loc_proba.max(dim=0).values
+    new_proba = (loc_proba - min_proba) / (max_proba - min_proba)
+    sum_proba = new_proba.sum(dim=1).reshape(-1, 1)
+    new_proba = new_proba / sum_proba
+    rmax = new_proba.max(dim=1).values
+    rmin = new_proba.min(dim=1).values
+    thresholds = rmax - (rmax - rmin) * alpha
+    return (new_proba > thresholds.reshape(-1, 1)).double()
+
+
+def performances_record(loc_true: torch.Tensor, loc_pred: torch.Tensor):
+    """code/train.py:42-86: aim / coverage / accuracy, float32 running sums in row order."""
+    t = (loc_true.detach().cpu().long() == 1)
+    p = (loc_pred.detach().cpu().long() == 1)
+    aim = torch.zeros((), dtype=torch.float32)
+    cov = torch.zeros((), dtype=torch.float32)
+    acc = torch.zeros((), dtype=torch.float32)
+    for i in range(len(t)):
+        and_set = (t[i] & p[i]).sum().float()
+        pred = p[i].sum().float()
+        real = t[i].sum().float()
+        or_set = (t[i] | p[i]).sum().float()
+        if pred != 0:
+            aim = aim + and_set / pred
+        cov = cov + and_set / real
+        acc = acc + and_set / or_set
+    n = len(t)
+    return float(aim / n), float(cov / n), float(acc / n)

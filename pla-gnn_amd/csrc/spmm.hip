@@ -638,10 +638,13 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   // serialise a memory round trip per 64 entries, and edges that win nothing cost
   // nothing. Segment t belongs to the edge i with excl_i <= t < excl_i + nseg_i, i.e.
   // i = popcount(ballot(excl <= t)) - 1.
+  // the next window's descriptors are loaded while the current window is processed
+  int2 gl_next = glist[t0 + min(lane, max(0, t1 - t0 - 1))];
   for (int tw = t0; tw < t1; tw += kWave) {
     const int nw = min(kWave, t1 - tw);
     const int tl = tw + min(lane, nw - 1);
-    const int2 gl = glist[tl];
+    const int2 gl = gl_next;
+    if (tw + kWave < t1) gl_next = glist[tw + kWave + min(lane, t1 - tw - kWave - 1)];
     float wv = 1.f;
     if constexpr (HAS_W) wv = ew[tslot[tl]];
     const int nseg = lane < nw ? (gl.y + kWave - 1) / kWave : 0;

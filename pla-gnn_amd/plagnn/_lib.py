@@ -93,6 +93,10 @@ SIGNATURES = {
     "pg_adam_prepare": (_i, [_vp, _d, _d, _d, _vp]),
     "pg_adam_apply": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _d, _d, _d, _d, _vp]),
     "pg_gemm_f32_split_k": (_i, [_i64, _i64, _i64]),
+    "pg_ecc": (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _d, _vp, _vp]),
+    "pg_loc_eval_workspace": (_sz, [_i64, _i32]),
+    "pg_loc_correction": (_i, [_vp, _i64, _i64, _i32, _d, _vp, _i64, _vp, _sz, _vp]),
+    "pg_loc_performance": (_i, [_vp, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _sz, _vp]),
     "pg_gemm_f32_workspace": (_sz, [_i64, _i64, _i64, _i]),
     "pg_gemm_f32": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _ep,
                          _i, _vp, _sz, _vp]),

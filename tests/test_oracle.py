@@ -115,3 +115,27 @@ def test_ecc_golden_present():
     d = np.load(os.path.join(GOLD, "ecc.npz"))
     e = d["tri_ecc"]
     assert e[0, 1] == 1.0 and e[1, 2] == 1.0 and e[0, 3] == 0.0
+
+
+@pytest.mark.parametrize("case", ["tri", "rand30"])
+def test_ecc_oracle_matches_reference_golden(oracle_mod, case):
+    """The C restatement of code/data_preprocess.py:175-214 reproduces the reference's
+    own output (fixture made by running the reference function) bit for bit."""
+    from scipy.sparse import coo_matrix
+
+    d = np.load(os.path.join(GOLD, "ecc.npz"))
+    adj = d[f"{case}_adj"]
+    r, c = np.nonzero(adj)
+    m = coo_matrix((np.ones(len(r), np.int64), (r, c)), shape=adj.shape)
+    np.testing.assert_array_equal(oracle_mod.edge_clustering_coefficients(m).toarray(), d[f"{case}_ecc"])
+
+
+@pytest.mark.parametrize("alpha", [0.1, 0.3])
+def test_eval_oracle_matches_reference_golden(oracle_mod, alpha):
+    """protein_loc_correction / performances_record restatements (code/train.py:19-86)
+    vs the reference's own outputs on the committed fixture."""
+    d = np.load(os.path.join(GOLD, "eval.npz"))
+    pred = oracle_mod.protein_loc_correction(torch.from_numpy(d["proba"]), alpha)
+    np.testing.assert_array_equal(pred.numpy(), d[f"pred_{alpha}"])
+    perf = np.array(oracle_mod.performances_record(torch.from_numpy(d["true"]), pred), np.float64)
+    np.testing.assert_array_equal(perf, d[f"perf_{alpha}"])
