@@ -38,6 +38,8 @@ CONFIGS = {
             "S0 PPI stand-in, reference dims GNN32(503,400,300,200,100,12), fp32"),
     "cfg3": ("s0", [503, 512, 512, 512, 100, 12],
              "S0 perturbed (+-3% edges), ECC edge weights (pg_ecc, u_mul_e max), hidden 512, fp32"),
+    "cfg5": ("rmat", [503, 512, 512, 512, 100, 12],
+             "RMAT x16 PPI (N=384656, a,b,c,d=.57,.19,.19,.05, mean deg 50), hidden 512, fp32"),
 }
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_F32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
@@ -232,7 +234,7 @@ def main():
     rf["traffic"] = traffic
 
     cpu = None
-    if world == 1 and not args.no_cpu_baseline and args.config != "cfg3":
+    if world == 1 and not args.no_cpu_baseline and args.config in ("cfg2", "ref"):
         cpu = cpu_baseline(ds, dims, train_idx, w)
 
     out = {

@@ -36,6 +36,9 @@
  *                           the ECC feature / edge-weight front end
  *   pg_loc_correction,   <- protein_loc_correction / performances_record
  *   pg_loc_performance      (code/train.py:19-86), the per-epoch eval
+ *   pg_perturb_*         <- construct_gcn_matrix's np.corrcoef (code/data_preprocess.py:
+ *                           165-170) + modify_network_topology (217-257), fused: the
+ *                           N x N correlation / difference matrices are never stored
  *
  * Conventions
  *   - All buffers are caller-owned. Device entry points take device pointers and
@@ -276,6 +279,42 @@ int pg_loc_correction(const float* proba, int64_t ldp, int64_t n, int32_t C, dou
 int pg_loc_performance(const float* loc_true, int64_t ldt, const double* loc_pred, int64_t ldp,
                        int64_t n, int32_t C, double* out3, void* ws, size_t ws_bytes,
                        pg_stream_t stream);
+
+/* ---------------- device: §8f — topology perturbation ---------------- */
+
+/* code/data_preprocess.py:165-170 (np.corrcoef of the expression rows, diagonal and NaN
+ * set to 0) for the normal and the intervention state, and :217-257
+ * modify_network_topology on their difference, without materialising any N x N matrix.
+ * xc_*: [n][S] float64 CENTRED expression rows (x - x.mean(axis=1), computed by the
+ * caller as numpy does), 2 <= S <= 8; inv_fact = 1 / (S - 1).
+ *   pcc(i, j) = clip(((fma-chain dot(xc_i, xc_j)) * inv_fact) / sd_i / sd_j, -1, 1),
+ *               0 on the diagonal and where NaN;  sd_i = sqrt(dot(xc_i, xc_i) * inv_fact)
+ *   diff(i, j) = pcc_inter(i, j) - pcc_normal(i, j)
+ * pg_perturb_prepare: sd_* [n].
+ * pg_perturb_sum: *total = sum over all n*n entries of diff (squared = 0) or of
+ *   (diff - mean)^2 (squared = 1); compensated f64, deterministic. Scratch:
+ *   pg_perturb_workspace(n) bytes. The caller forms mean = total / n^2,
+ *   std = sqrt(total_sq / n^2), lo_thr = mean - thr * std, hi_thr = mean + thr * std.
+ * pg_perturb_count / pg_perturb_fill: the perturbed adjacency, given the original as CSR
+ *   (sorted unique columns per row; val = stored int64 values, NULL = all ones):
+ *   v' = 0 if v == 1 and diff < lo_thr;  1 if v == 0 and diff > hi_thr;  v otherwise.
+ *   count: non-zeros per row; fill: column ids and values of the non-zeros, row-major,
+ *   ascending columns, row i starting at offsets[i]. n <= 1 310 720 (LDS row bitmap). */
+size_t pg_perturb_workspace(int64_t n);
+int pg_perturb_prepare(const double* xc_normal, const double* xc_inter, int64_t n, int32_t S,
+                       double inv_fact, double* sd_normal, double* sd_inter, pg_stream_t stream);
+int pg_perturb_sum(const double* xc_normal, const double* xc_inter, const double* sd_normal,
+                   const double* sd_inter, int64_t n, int32_t S, double inv_fact, int squared,
+                   double mean, double* total, void* ws, size_t ws_bytes, pg_stream_t stream);
+int pg_perturb_count(const double* xc_normal, const double* xc_inter, const double* sd_normal,
+                     const double* sd_inter, int64_t n, int32_t S, double inv_fact,
+                     const int32_t* ptr, const int32_t* col, const int64_t* val, double lo_thr,
+                     double hi_thr, int32_t* counts, pg_stream_t stream);
+int pg_perturb_fill(const double* xc_normal, const double* xc_inter, const double* sd_normal,
+                    const double* sd_inter, int64_t n, int32_t S, double inv_fact,
+                    const int32_t* ptr, const int32_t* col, const int64_t* val, double lo_thr,
+                    double hi_thr, const int64_t* offsets, int32_t* out_col, int64_t* out_val,
+                    pg_stream_t stream);
 
 /* ---------------- misc ---------------- */
 const char* pg_last_error_string(void);

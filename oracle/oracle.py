@@ -72,6 +72,16 @@ def lib():
         _f64p = ctypes.POINTER(ctypes.c_double)
         L.oracle_ecc.argtypes = [_i64p, _i64p, _f64p, ctypes.c_int64, ctypes.c_double, _i64p, _i64p, _f64p]
         L.oracle_ecc.restype = ctypes.c_int64
+        L.oracle_perturb_sd.argtypes = [_f64p, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _f64p]
+        L.oracle_perturb_sd.restype = None
+        L.oracle_perturb_sum.argtypes = [_f64p, _f64p, _f64p, _f64p, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                                         ctypes.c_int, ctypes.c_double, ctypes.c_int64, ctypes.c_int64]
+        L.oracle_perturb_sum.restype = ctypes.c_double
+        L.oracle_perturb_rows.argtypes = [_f64p, _f64p, _f64p, _f64p, ctypes.c_int64, ctypes.c_int,
+                                          ctypes.c_double, _i64p, _i64p, _i64p, ctypes.c_double,
+                                          ctypes.c_double, ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, _i64p,
+                                          ctypes.c_int64]
+        L.oracle_perturb_rows.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -325,3 +335,82 @@ def performances_record(loc_true: torch.Tensor, loc_pred: torch.Tensor):
         acc = acc + and_set / or_set
     n = len(t)
     return float(aim / n), float(cov / n), float(acc / n)
+
+
+# ---------------------------------------------------------------- §8f: topology perturbation
+def pcc_matrix(expr) -> np.ndarray:
+    """code/data_preprocess.py:166-169, verbatim numpy: np.corrcoef of the rows, diagonal
+    and NaN set to 0 (dense N x N float64)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        c = np.corrcoef(np.asarray(expr, np.float64))
+    np.fill_diagonal(c, 0)
+    c[np.isnan(c)] = 0
+    return c
+
+
+def modify_network_topology(ppi_net, pcc_nor: np.ndarray, pcc_inter: np.ndarray, thr: float):
+    """code/data_preprocess.py:217-257 on dense correlation matrices (numpy, verbatim
+    operations): returns (scipy COO of the perturbed adjacency, (mean, std) of diff)."""
+    from scipy.sparse import coo_matrix
+
+    a = np.asarray(ppi_net.tocsr().todense())
+    diff = pcc_inter - pcc_nor
+    mean, std = np.mean(diff), np.std(diff)
+    lo, hi = mean - thr * std, mean + thr * std
+    res1 = np.logical_and(diff < lo, a == 1)
+    res2 = np.logical_and(diff > hi, a == 0)
+    a[res1] = 0
+    a[res2] = 1
+    return coo_matrix(a), (float(mean), float(std))
+
+
+class PerturbStream:
+    """The streaming C restatement (oracle/perturb_oracle.c) on centred expression rows:
+    never stores an N x N matrix, so it runs at the full PPI size (CPU baseline)."""
+
+    def __init__(self, ppi_net, expr_normal, expr_inter):
+        def centred(e):
+            x = np.array(e, dtype=np.float64, ndmin=2)
+            x -= x.mean(axis=1)[:, None]
+            return np.ascontiguousarray(x)
+
+        self.xn, self.xi = centred(expr_normal), centred(expr_inter)
+        self.n, self.S = self.xn.shape
+        self.inv_fact = float(np.true_divide(1, self.S - 1))
+        f64p = ctypes.POINTER(ctypes.c_double)
+        self.sdn = np.empty(self.n)
+        self.sdi = np.empty(self.n)
+        lib().oracle_perturb_sd(_p(self.xn, f64p), self.n, self.S, self.inv_fact, _p(self.sdn, f64p))
+        lib().oracle_perturb_sd(_p(self.xi, f64p), self.n, self.S, self.inv_fact, _p(self.sdi, f64p))
+        csr = ppi_net.tocsr()
+        csr.sum_duplicates()
+        csr.sort_indices()
+        self.ptr = np.ascontiguousarray(csr.indptr, np.int64)
+        self.col = np.ascontiguousarray(csr.indices, np.int64)
+        v = np.ascontiguousarray(csr.data, np.int64)
+        self.val = None if np.all(v == 1) else v
+        self._f = f64p
+
+    def _base(self):
+        f = self._f
+        return (_p(self.xn, f), _p(self.xi, f), _p(self.sdn, f), _p(self.sdi, f), self.n, self.S, self.inv_fact)
+
+    def row_sum(self, squared: bool, mean: float, r0: int, r1: int) -> float:
+        return lib().oracle_perturb_sum(*self._base(), int(squared), float(mean), r0, r1)
+
+    def stats(self, thr: float):
+        nn = float(self.n) * float(self.n)
+        mean = self.row_sum(False, 0.0, 0, self.n) / nn
+        std = float(np.sqrt(self.row_sum(True, mean, 0, self.n) / nn))
+        return mean, std, mean - thr * std, mean + thr * std
+
+    def rows(self, lo: float, hi: float, r0: int, r1: int):
+        cap = int(self.ptr[r1] - self.ptr[r0]) + (r1 - r0) * self.n
+        cap = min(cap, (r1 - r0) * self.n)
+        rr, cc, vv = (np.empty(max(cap, 1), np.int64) for _ in range(3))
+        m = lib().oracle_perturb_rows(*self._base(), _p(self.ptr, _i64p), _p(self.col, _i64p),
+                                      _p(self.val, _i64p), lo, hi, r0, r1, _p(rr, _i64p), _p(cc, _i64p),
+                                      _p(vv, _i64p), len(rr))
+        if m < 0:
+            raise MemoryError("oracle_perturb_rows")
+        return rr[:m], cc[:m], vv[:m]

@@ -97,6 +97,12 @@ SIGNATURES = {
     "pg_loc_eval_workspace": (_sz, [_i64, _i32]),
     "pg_loc_correction": (_i, [_vp, _i64, _i64, _i32, _d, _vp, _i64, _vp, _sz, _vp]),
     "pg_loc_performance": (_i, [_vp, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _sz, _vp]),
+    "pg_perturb_workspace": (_sz, [_i64]),
+    "pg_perturb_prepare": (_i, [_vp, _vp, _i64, _i32, _d, _vp, _vp, _vp]),
+    "pg_perturb_sum": (_i, [_vp, _vp, _vp, _vp, _i64, _i32, _d, _i, _d, _vp, _vp, _sz, _vp]),
+    "pg_perturb_count": (_i, [_vp, _vp, _vp, _vp, _i64, _i32, _d, _vp, _vp, _vp, _d, _d, _vp, _vp]),
+    "pg_perturb_fill": (_i, [_vp, _vp, _vp, _vp, _i64, _i32, _d, _vp, _vp, _vp, _d, _d, _vp, _vp, _vp,
+                             _vp]),
     "pg_gemm_f32_workspace": (_sz, [_i64, _i64, _i64, _i]),
     "pg_gemm_f32": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _ep,
                          _i, _vp, _sz, _vp]),

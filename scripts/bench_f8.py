@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from scipy.sparse import coo_matrix  # noqa: E402
 
 import oracle  # noqa: E402  (CPU baseline leg only)
-from plagnn import _lib, data, ecc, loc_eval  # noqa: E402
+from plagnn import _lib, data, ecc, loc_eval, perturb  # noqa: E402
 from plagnn._lib import call, ptr  # noqa: E402
 
 
@@ -81,6 +81,65 @@ def main():
                       "cpu_baseline": {"ms": round(cpu * 1e3, 1), "cores": 1, "kind": "port",
                                        "sample": "oracle torch-CPU restatement, per-row Python loop as train.py:60-78"},
                       "matches_oracle": list(ev()) == list(perf_ref)}))
+
+    # 8f-4: topology perturbation (normal vs intervention expression, N x 3 like the GEO sets)
+    en = ds.expr
+    ei = en * np.random.default_rng(4).lognormal(0.0, 0.5, en.shape)
+    ei[np.random.default_rng(5).random(n) < 0.05] = 0.0
+    thr = 2.2
+    perturb.modify_network_topology_expr(adj, en, ei, thr)  # warm-up (module load, first launch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    got, pst = perturb.modify_network_topology_expr(adj, en, ei, thr, return_stats=True)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    # the four device passes alone (sd, sum, sum of squares, count, fill), HIP events
+    xn, xi = perturb._centred(en), perturb._centred(ei)
+    tx, ti = torch.from_numpy(xn).to(dev), torch.from_numpy(xi).to(dev)
+    sdn, sdi = torch.empty(n, dtype=torch.float64, device=dev), torch.empty(n, dtype=torch.float64, device=dev)
+    wsp = torch.empty(int(_lib.lib().pg_perturb_workspace(n)), dtype=torch.uint8, device=dev)
+    tot = torch.zeros(2, dtype=torch.float64, device=dev)
+    pc = adj.tocsr()
+    pc.sort_indices()
+    tp, tc = torch.from_numpy(pc.indptr.astype(np.int32)).to(dev), torch.from_numpy(pc.indices.astype(np.int32)).to(dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(np.diff(got.tocsr().indptr), out=offs[1:])
+    to = torch.from_numpy(offs).to(dev)
+    oc = torch.empty(max(got.nnz, 1), dtype=torch.int32, device=dev)
+    ov = torch.empty(max(got.nnz, 1), dtype=torch.int64, device=dev)
+    base = (ptr(tx), ptr(ti), ptr(sdn), ptr(sdi), n, 3, 0.5)
+
+    def passes():
+        call("pg_perturb_prepare", ptr(tx), ptr(ti), n, 3, 0.5, ptr(sdn), ptr(sdi), st)
+        call("pg_perturb_sum", *base, 0, 0.0, ptr(tot[0:1]), ptr(wsp), wsp.numel(), st)
+        call("pg_perturb_sum", *base, 1, pst.mean, ptr(tot[1:2]), ptr(wsp), wsp.numel(), st)
+        call("pg_perturb_count", *base, ptr(tp), ptr(tc), 0, pst.lo_thr, pst.hi_thr, ptr(cnt), st)
+        call("pg_perturb_fill", *base, ptr(tp), ptr(tc), 0, pst.lo_thr, pst.hi_thr, ptr(to), ptr(oc), ptr(ov), st)
+    ksec = hip_time(passes, reps=3)
+    # CPU: the streaming C restatement, 1 core, on a row sample (all four passes over
+    # those rows x all columns), scaled to N rows
+    ps = oracle.PerturbStream(adj, en, ei)
+    rs = 300
+    t0 = time.perf_counter()
+    ps.row_sum(False, 0.0, 0, rs)
+    ps.row_sum(True, pst.mean, 0, rs)
+    r_, c_, v_ = ps.rows(pst.lo_thr, pst.hi_thr, 0, rs)
+    cpu_rows = time.perf_counter() - t0
+    cpu_full = cpu_rows * n / rs
+    sub = got.tocsr()[0:rs].tocoo()
+    exact = bool(np.array_equal(sub.row, r_) and np.array_equal(sub.col, c_) and np.array_equal(sub.data, v_))
+    pairs = float(n) * n
+    print(json.dumps({"row": "8f-4 topology perturbation (corrcoef x2 + modify_network_topology)", "n": n,
+                      "samples": 3, "thr": thr, "edges_in": int(adj.nnz), "edges_out": int(got.nnz),
+                      "removed": pst.removed, "added": pst.added,
+                      "gpu_kernels_ms": round(ksec * 1e3, 3), "gpu_call_ms": round(wall * 1e3, 1),
+                      "pairs_per_s": round(pairs / ksec, 1),
+                      "cpu_baseline": {"ms": round(cpu_full * 1e3, 1), "pairs_per_s": round(pairs / cpu_full, 1),
+                                       "cores": 1, "kind": "port",
+                                       "sample": f"oracle/perturb_oracle.c (streaming restatement) over {rs} of {n} "
+                                                 f"rows x all columns, scaled to {n} rows"},
+                      "bit_exact_vs_oracle_sample_rows": exact}))
 
 
 if __name__ == "__main__":

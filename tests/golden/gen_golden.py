@@ -13,7 +13,10 @@ executed in a namespace holding torch / numpy:
     weight_cal               code/train.py:111-126
 data_preprocess.py imports cleanly (pandas/scipy/sklearn/tqdm), so
     edge_clustering_coefficients  code/data_preprocess.py:175-214
-is called directly. Only the produced input/output arrays are committed (no source).
+is called directly, and so are
+    construct_gcn_matrix          code/data_preprocess.py:128-172 (on a synthetic GEO-style CSV)
+    modify_network_topology       code/data_preprocess.py:217-257
+Only the produced input/output arrays are committed (no source).
 """
 from __future__ import annotations
 
@@ -95,9 +98,63 @@ def gen_ecc():
     np.savez(os.path.join(HERE, "ecc.npz"), **out)
 
 
+def gen_perturb():
+    """Reference end to end: a GEO-style expression CSV (duplicate ids averaged, ids not in
+    the PPI dropped, PPI proteins missing from the CSV zero-filled) -> construct_gcn_matrix
+    for both states -> modify_network_topology. Stored: the expression matrices it returns
+    (our drop-in's input), the PPI, and the perturbed PPI; plus diff's mean / std."""
+    import tempfile
+
+    import pandas as pd
+    from scipy.sparse import coo_matrix
+
+    sys.path.insert(0, REF)
+    import data_preprocess as dp  # noqa: E402
+
+    out = {}
+    for name, n, p_edge, thr, seed in (("small", 60, 0.12, 1.0, 5), ("mid", 400, 0.05, 1.5, 6)):
+        rng = np.random.default_rng(seed)
+        ids = [f"P{i:05d}" for i in range(n)]
+        normal = ["GSM1", "GSM2", "GSM3"]
+        inter = ["GSM4", "GSM5", "GSM6"]
+        rows = []
+        for i, pid in enumerate(ids):
+            if rng.random() < 0.2:
+                continue  # protein absent from the expression set -> zero row
+            for _ in range(1 + int(rng.random() < 0.15)):  # some ids measured twice
+                rows.append([pid] + list(rng.lognormal(1.0, 1.0, 6)))
+        rows.append(["XNOTPPI"] + list(rng.lognormal(1.0, 1.0, 6)))  # not in the PPI
+        df = pd.DataFrame(rows, columns=["uniprot_id"] + normal + inter)
+        with tempfile.TemporaryDirectory() as td:
+            csv = os.path.join(td, "expr.csv")
+            df.to_csv(csv, index=False)
+            gcn_n, expr_n = dp.construct_gcn_matrix(csv, normal, ids)
+            gcn_i, expr_i = dp.construct_gcn_matrix(csv, inter, ids)
+        a = np.triu(rng.random((n, n)) < p_edge, 1)
+        a = a | a.T
+        r, c = np.nonzero(a)
+        data = np.ones(len(r), np.int64)
+        if name == "small":  # one duplicated edge: value 2 after tocsr(), untouched by both rules
+            r, c, data = np.append(r, r[0]), np.append(c, c[0]), np.append(data, 1)
+        ppi = coo_matrix((data, (r, c)), shape=(n, n))
+        res = dp.modify_network_topology(ppi, gcn_n, gcn_i, thr).tocoo()
+        diff = gcn_i.tocsr() - gcn_n.tocsr()
+        diff = diff.toarray()
+        out[f"{name}_expr_normal"] = np.asarray(expr_n, np.float64)
+        out[f"{name}_expr_inter"] = np.asarray(expr_i, np.float64)
+        out[f"{name}_ppi_row"], out[f"{name}_ppi_col"], out[f"{name}_ppi_val"] = ppi.row, ppi.col, ppi.data
+        out[f"{name}_thr"] = np.float64(thr)
+        out[f"{name}_out_row"], out[f"{name}_out_col"] = res.row, res.col
+        out[f"{name}_out_val"] = np.asarray(res.data, np.int64)
+        out[f"{name}_mean_std"] = np.array([np.mean(diff), np.std(diff)])
+        out[f"{name}_pcc_normal"] = gcn_n.toarray() if n <= 60 else np.zeros(0)
+    np.savez_compressed(os.path.join(HERE, "perturb.npz"), **out)
+
+
 if __name__ == "__main__":
     ns = _train_functions()
     gen_loss(ns)
     gen_eval(ns)
     gen_ecc()
+    gen_perturb()
     print("golden fixtures written to", HERE)

@@ -139,3 +139,42 @@ def test_eval_oracle_matches_reference_golden(oracle_mod, alpha):
     np.testing.assert_array_equal(pred.numpy(), d[f"pred_{alpha}"])
     perf = np.array(oracle_mod.performances_record(torch.from_numpy(d["true"]), pred), np.float64)
     np.testing.assert_array_equal(perf, d[f"perf_{alpha}"])
+
+
+# ---------------------------------------------------------------- §8f: topology perturbation
+def _perturb_case(d, name):
+    from scipy.sparse import coo_matrix
+
+    n = d[f"{name}_expr_normal"].shape[0]
+    ppi = coo_matrix((d[f"{name}_ppi_val"], (d[f"{name}_ppi_row"], d[f"{name}_ppi_col"])), shape=(n, n))
+    out = coo_matrix((d[f"{name}_out_val"], (d[f"{name}_out_row"], d[f"{name}_out_col"])), shape=(n, n))
+    return ppi, d[f"{name}_expr_normal"], d[f"{name}_expr_inter"], float(d[f"{name}_thr"]), out
+
+
+@pytest.mark.parametrize("name", ["small", "mid"])
+def test_perturb_numpy_oracle_matches_reference_golden(oracle_mod, name):
+    d = np.load(os.path.join(GOLD, "perturb.npz"))
+    ppi, en, ei, thr, ref = _perturb_case(d, name)
+    pn, pi = oracle_mod.pcc_matrix(en), oracle_mod.pcc_matrix(ei)
+    if d[f"{name}_pcc_normal"].size:
+        np.testing.assert_array_equal(pn, d[f"{name}_pcc_normal"])
+    got, (mean, std) = oracle_mod.modify_network_topology(ppi, pn, pi, thr)
+    np.testing.assert_array_equal(got.row, ref.row)
+    np.testing.assert_array_equal(got.col, ref.col)
+    np.testing.assert_array_equal(got.data, ref.data)
+    np.testing.assert_array_equal([mean, std], d[f"{name}_mean_std"])
+    assert got.nnz != len(d[f"{name}_ppi_row"])  # the threshold fires in both fixtures
+
+
+@pytest.mark.parametrize("name", ["small", "mid"])
+def test_perturb_stream_oracle_matches_reference_golden(oracle_mod, name):
+    d = np.load(os.path.join(GOLD, "perturb.npz"))
+    ppi, en, ei, thr, ref = _perturb_case(d, name)
+    ps = oracle_mod.PerturbStream(ppi, en, ei)
+    mean, std, lo, hi = ps.stats(thr)
+    # compensated sums vs numpy's pairwise sums: a few ulp apart
+    np.testing.assert_allclose([mean, std], d[f"{name}_mean_std"], rtol=1e-13, atol=1e-16)
+    r, c, v = ps.rows(lo, hi, 0, ps.n)
+    np.testing.assert_array_equal(r, ref.row)
+    np.testing.assert_array_equal(c, ref.col)
+    np.testing.assert_array_equal(v, ref.data)
