@@ -32,6 +32,9 @@
  *   pg_col_sum           <- bias gradients (sum of dY over nodes)
  *   pg_gemm_f32          <- nn.Linear GEMMs (fc_pool / fc_self / fc_neigh / liner1-2),
  *                           fp32 MFMA (v_mfma_f32_32x32x2_f32), exact f32
+ *   pg_gemm_bf16,        <- the same layers and aggregation in the bf16-storage mode
+ *   pg_spmm_max_*_bf16      (BASELINE configs[4]: bf16 storage, f32 accumulate); not run
+ *   pg_cast_*               by the reference (fp32 only): reference-unpinned
  *   pg_ecc               <- edge_clustering_coefficients (code/data_preprocess.py:175-214),
  *                           the ECC feature / edge-weight front end
  *   pg_loc_correction,   <- protein_loc_correction / performances_record
@@ -78,6 +81,10 @@ typedef void* pg_stream_t; /* hipStream_t */
 #define PG_ARG_I32 32 /* same, int32, -1 = none (rows with degree >= 65535) */
 
 /* activation codes for pg_bias_act / pg_gemm_f32 epilogues */
+/* storage types of pg_gemm_bf16's output */
+#define PG_DTYPE_F32 0
+#define PG_DTYPE_BF16 1
+
 #define PG_ACT_NONE 0
 #define PG_ACT_RELU 1
 #define PG_ACT_LEAKY 2 /* F.leaky_relu, negative_slope given separately */
@@ -239,6 +246,38 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
                 int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
                 size_t ws_bytes, pg_stream_t stream);
+
+/* ---------------- device: bf16 storage mode (f32 accumulate) ---------------- */
+
+/* pg_gemm_f32's contract with bf16 operands (uint16 bits, row-major): op(A), op(B) bf16,
+ * products on v_mfma_f32_32x32x16_bf16 with f32 accumulate; C is f32 (c_dtype =
+ * PG_DTYPE_F32) or bf16 (PG_DTYPE_BF16, rounded to nearest even). The epilogue's bias and
+ * rowsum are f32; C read for beta != 0 is in C's storage type; ep->dact points to bf16
+ * values (activation outputs are stored bf16 in this mode).
+ * Requirements: 16-B aligned A, B, C; lda, ldb multiples of 8; the contiguous extent of
+ * each operand (K for A / B^T, M for A^T, N for B) a multiple of 8; N and ldc multiples of
+ * 4; split_k > 1 only with an f32 C. Else PG_ERR_UNSUPPORTED. */
+int pg_gemm_bf16_split_k(int64_t M, int64_t N, int64_t K);
+size_t pg_gemm_bf16_workspace(int64_t M, int64_t N, int64_t K, int split_k);
+int pg_gemm_bf16(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
+                 const void* A, int64_t lda, const void* B, int64_t ldb, float beta, void* C,
+                 int64_t ldc, int c_dtype, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
+                 size_t ws_bytes, pg_stream_t stream);
+/* pg_spmm_max_fwd / pg_spmm_max_bwd on bf16 features (X, out, dout, mask_src, dx): the
+ * max is a selection, so out holds the winning bf16 value exactly (u_mul_e products are
+ * rounded to nearest even); the backward accumulates in f32 and rounds dx once. Same
+ * workspace queries. The backward needs PG_ARG_U16 records and F <= 1024. */
+int pg_spmm_max_fwd_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t F, void* out,
+                         int64_t ldo, void* argpos, int64_t lda, int arg_kind, void* ws,
+                         size_t ws_bytes, pg_stream_t stream);
+int pg_spmm_max_bwd_bf16(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
+                         int arg_kind, const void* dout, int64_t ldd, int64_t F,
+                         const void* mask_src, int64_t ldm, void* dx, int64_t ldx, void* ws,
+                         size_t ws_bytes, pg_stream_t stream);
+/* dst[i] = bf16(src[map ? map[i] : i]) (map[i] < 0: 0), round to nearest even: the bf16
+ * weight copies of the f32 master parameters, in any layout the GEMMs want. */
+int pg_cast_f32_bf16(const float* src, const int32_t* map, int64_t n, void* dst, pg_stream_t stream);
+int pg_cast_bf16_f32(const void* src, int64_t n, float* dst, pg_stream_t stream);
 
 /* ---------------- host (_cpu): the same operations on host pointers ---------------- */
 int pg_spmm_max_fwd_cpu(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,

@@ -245,6 +245,29 @@ __global__ __launch_bounds__(kBlock) void adam_apply_kernel(
   }
 }
 
+// bf16 storage helpers: dst[i] = bf16(src[map ? map[i] : i]) (round to nearest even;
+// map[i] < 0 writes 0), and the widening copy back.
+__global__ __launch_bounds__(kBlock) void cast_bf16_kernel(const float* __restrict__ src,
+                                                           const int32_t* __restrict__ map, int64_t n,
+                                                           uint16_t* __restrict__ dst) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    float v = 0.f;
+    if (map) {
+      const int32_t j = map[i];
+      if (j >= 0) v = src[j];
+    } else {
+      v = src[i];
+    }
+    dst[i] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(v));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void widen_bf16_kernel(const uint16_t* __restrict__ src, int64_t n,
+                                                            float* __restrict__ dst) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+    dst[i] = __uint_as_float((uint32_t)src[i] << 16);
+}
+
 }  // namespace
 
 extern "C" {
@@ -360,6 +383,25 @@ int pg_adam_apply(float* param, const float* grad, float* exp_avg, float* exp_av
                      param, grad, exp_avg, exp_avg_sq, n, state, (float)beta1, (float)beta2,
                      (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, (float)weight_decay);
   return hip_status("pg_adam_apply");
+}
+
+int pg_cast_f32_bf16(const float* src, const int32_t* map, int64_t n, void* dst,
+                     pg_stream_t stream) {
+  if (n < 0) return pg::set_error(PG_ERR_INVALID, "pg_cast_f32_bf16: n < 0");
+  if (n == 0) return pg::ok();
+  if (!src || !dst) return pg::set_error(PG_ERR_INVALID, "pg_cast_f32_bf16: NULL buffer");
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_1d(n, 4096)), dim3(kBlock), 0, (hipStream_t)stream, src,
+                     map, n, (uint16_t*)dst);
+  return hip_status("pg_cast_f32_bf16");
+}
+
+int pg_cast_bf16_f32(const void* src, int64_t n, float* dst, pg_stream_t stream) {
+  if (n < 0) return pg::set_error(PG_ERR_INVALID, "pg_cast_bf16_f32: n < 0");
+  if (n == 0) return pg::ok();
+  if (!src || !dst) return pg::set_error(PG_ERR_INVALID, "pg_cast_bf16_f32: NULL buffer");
+  hipLaunchKernelGGL(widen_bf16_kernel, dim3(grid_1d(n, 4096)), dim3(kBlock), 0, (hipStream_t)stream,
+                     (const uint16_t*)src, n, dst);
+  return hip_status("pg_cast_bf16_f32");
 }
 
 }  // extern "C"

@@ -35,8 +35,11 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "gemm_common.hpp"
 
 namespace {
+
+using namespace pg_gemm;
 
 constexpr int BK = 32;
 constexpr int HK = BK / 2;  // k-values per lane half per K step
@@ -68,19 +71,6 @@ __device__ unsigned long long pg_gemm_kphase[64][4];   // start, prologue done, 
 #endif
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
-
-// Epilogue modes: activation of the result, or multiplication by the derivative of an
-// activation given its OUTPUT y (the fused backward of relu / leaky_relu), or split-K.
-enum Epi { EPI_NONE = 0, EPI_RELU = 1, EPI_LEAKY = 2, EPI_DRELU = 3, EPI_DLEAKY = 4, EPI_SPLIT = 5 };
-
-template <int EPI>
-__device__ __forceinline__ float epi_apply(float x, float y, float slope) {
-  if constexpr (EPI == EPI_RELU) return x > 0.f ? x : 0.f;
-  else if constexpr (EPI == EPI_LEAKY) return x > 0.f ? x : x * slope;
-  else if constexpr (EPI == EPI_DRELU) return y > 0.f ? x : 0.f;
-  else if constexpr (EPI == EPI_DLEAKY) return y > 0.f ? x : x * slope;
-  else return x;
-}
 
 // Load a ROWS x BK tile of a matrix stored [row][k] (k contiguous) or [k][row] (KMAJ),
 // rows [r0, r0+ROWS) x k [k0, k0+BK), zero outside [0,R) x [0,kz1). 4 floats per unit.
@@ -704,57 +694,6 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
 #endif
 }
 
-// Split-K combine: C = alpha * sum_z ws[z] (+ beta * C); the row sums likewise (their
-// slices follow the partial slabs in the workspace). G threads per output: thread group g
-// sums slices [S g / G, S (g+1) / G) in order, then one thread adds the G group sums in
-// order (a fixed order: deterministic). Consecutive threads take consecutive outputs, so
-// every slab read is coalesced.
-template <int G>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws,
-                                                            int splits, int M, int N, float alpha,
-                                                            float beta, float* __restrict__ C,
-                                                            int64_t ldc, const float* __restrict__ ws_rowsum,
-                                                            float* __restrict__ rowsum) {
-  constexpr int OPB = 256 / G;  // outputs per block
-  __shared__ float part[256];
-  const int64_t n = (int64_t)M * N;
-  const int64_t total = n + (rowsum ? M : 0);
-  const int ol = threadIdx.x % OPB, g = threadIdx.x / OPB;
-  const int z0 = (int)((int64_t)splits * g / G), z1 = (int)((int64_t)splits * (g + 1) / G);
-  for (int64_t base = (int64_t)blockIdx.x * OPB; base < total; base += (int64_t)gridDim.x * OPB) {
-    const int64_t i = base + ol;
-    float s = 0.f;
-    if (i < total) {
-      if (i < n) {
-        for (int z = z0; z < z1; ++z) s += ws[(int64_t)z * n + i];
-      } else {
-        for (int z = z0; z < z1; ++z) s += ws_rowsum[(int64_t)z * M + (i - n)];
-      }
-    }
-    if constexpr (G > 1) {
-      part[threadIdx.x] = s;
-      __syncthreads();
-      if (g == 0) {
-#pragma unroll
-        for (int q = 1; q < G; ++q) s += part[q * OPB + ol];
-      }
-      __syncthreads();
-    }
-    if (g == 0 && i < total) {
-      if (i >= n) {
-        rowsum[i - n] = s;
-      } else {
-        const int64_t r = i / N;
-        const int c = (int)(i - r * N);
-        float v = alpha * s;
-        if (beta != 0.f) v = v + beta * C[r * ldc + c];
-        C[r * ldc + c] = v;
-      }
-    }
-  }
-}
-
-inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 struct Args {
   int M, N, K, kps, tiles_n, tiles;
@@ -959,7 +898,7 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   if (split) {
     const int64_t n = M * N + (ep->rowsum ? M : 0);
     // threads per output: enough slice groups that each thread sums <= ~8 slices
-    const int G = split_k <= 8 ? 1 : split_k <= 32 ? 4 : 16;
+    const int G = splitk_groups(split_k);
     const int opb = 256 / G;
     const int blocks = (int)std::min<int64_t>(8192, (n + opb - 1) / opb);
 #define PG_R(G_)                                                                              \

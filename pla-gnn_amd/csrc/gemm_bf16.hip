@@ -1,0 +1,511 @@
+// bf16-storage GEMM on the gfx950 matrix cores (v_mfma_f32_32x32x16_bf16: bf16 operands,
+// f32 accumulate) with the same fused epilogues as the fp32 GEMM (gemm.hip). Serves the
+// nn.Linear layers of the PLA-GNN step (code/model.py:13-17) in the bf16-storage mode of
+// the engine (BASELINE configs[4]: "hidden=512 bf16"): activations and their gradients
+// are stored as bf16, weights are bf16 copies of the f32 master parameters, every
+// product accumulates in f32, weight gradients leave in f32.
+//
+// Tiling: BM x BN per 256-thread workgroup (BM, BN in {64, 128}); 2 x 2 waves, each
+// owning (BM/2) x (BN/2) = TM x TN MFMA tiles of 32 x 32; K step 64 (four MFMA k-steps of
+// 16). K tiles go global -> LDS by LDS-DMA (global_load_lds_dwordx4, no register round
+// trip) into two images per operand; the tile for step t+1 is issued at the top of step
+// t and waited for by the step's single barrier. Fragments for k-step s+1 are read while
+// the MFMAs of k-step s run (across K steps too), as in the fp32 kernel.
+//
+// Operand images (one DMA wave-instruction fills 1 KiB of LDS lane-linearly, so every
+// swizzle is applied to the DMA's per-lane SOURCE address):
+//   row image, operand stored k-contiguous (A[m][k], or B stored [n][k]): [row][64 k],
+//     128-B rows of 8 chunks of 8 k; chunk c of row r sits at c ^ ((r >> 1) & 7): the
+//     16-lane groups of the ds_read_b128 fragment reads (16 consecutive rows, one chunk)
+//     hit 16 distinct bank quads.
+//   k image, operand stored row-contiguous (A stored [k][m] for dY^T X weight gradients,
+//     B stored [k][n]): [64 k][ROWS], chunk c (8 rows) of k-row k at c ^ f(k), f(k) =
+//     ((k >> 1) & 1) * 4 for 128-B k-rows, (k & 3) * 4 for 256-B k-rows. Fragments come
+//     from ds_read_b64_tr_b16 (cdna_hip_programming.md T10): each 16-lane group reads a
+//     4 k x 16 row block and every lane receives its row's 4 k-values; two reads give the
+//     8 k-values of a 32x32x16 fragment. With f(k) each 32-lane half covers all 64 banks
+//     once (conflict-free).
+// MFMA 32x32x16 bf16 operand map (cdna_hip_programming.md §3): lane l (r = l & 31,
+// h = l >> 5) holds A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7; C/D as the
+// f32 form: row = (reg & 3) + 8 (reg >> 2) + 4h, col = r.
+// Requirements (checked): 16-B aligned operands, leading dimensions and contiguous
+// extents (K of a row image, M / N of a k image) multiples of 8. Rows past M / N are
+// read from a clamped valid row (they only feed outputs that are never stored); a
+// partial last K tile is zero-filled by ds_write.
+// Output: f32 or bf16 (round to nearest even); C for beta != 0 is read in the output's
+// storage type; dact (the activation output of the fused activation backward) is bf16.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "common.hpp"
+#include "gemm_common.hpp"
+
+namespace {
+
+using namespace pg_gemm;
+
+constexpr int BK = 64;  // bf16 k-values per K step
+constexpr int kThreads = 256;
+
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+using lds_bf16x4 = __attribute__((address_space(3))) bf16x4;
+
+// element offset (u16 units) of (row, k) in an image
+template <int ROWS, bool KMAJ>
+__device__ __forceinline__ int img_off(int row, int k) {
+  if constexpr (!KMAJ) {
+    return row * BK + ((((k >> 3) ^ ((row >> 1) & 7))) << 3) + (k & 7);
+  } else {
+    const int f = ROWS == 64 ? ((k >> 1) & 1) * 4 : (k & 3) * 4;
+    return k * ROWS + ((((row >> 3) ^ f)) << 3) + (row & 7);
+  }
+}
+
+// DMA of one ROWS x BK tile (rows [r0, r0 + ROWS) x k [k0, k0 + BK)) into an image;
+// units past K (kvalid) are zero-filled by the lane that owns them.
+template <int ROWS, bool KMAJ, bool FULL>
+__device__ __forceinline__ void dma_tile(const uint16_t* __restrict__ P, int64_t ld, int r0, int R,
+                                         int k0, int kvalid, uint16_t* S, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < ROWS / 32; ++j) {
+    const int piece = j * 4 + wave;   // 1-KiB piece of the image
+    const int u = piece * 64 + lane;  // 16-B unit
+    const uint16_t* src;
+    bool valid;
+    if constexpr (!KMAJ) {
+      const int row = u >> 3, c = (u & 7) ^ ((row >> 1) & 7);
+      valid = 8 * c < kvalid;
+      src = P + (int64_t)min(r0 + row, R - 1) * ld + k0 + 8 * c;
+    } else {
+      constexpr int CPR = ROWS / 8;  // chunks per k-row
+      const int k = u / CPR, pos = u % CPR;
+      const int f = ROWS == 64 ? ((k >> 1) & 1) * 4 : (k & 3) * 4;
+      const int c = pos ^ f;
+      valid = k < kvalid;
+      src = P + (int64_t)(k0 + k) * ld + min(r0 + 8 * c, R - 8);
+    }
+    if (FULL || valid) __builtin_amdgcn_global_load_lds(src, S + piece * 512, 16, 0, 0);
+    else *reinterpret_cast<uint4*>(S + u * 8) = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
+// the 8 k-values of k-step s for MFMA row/col `rc` (tile-local) of lane half h
+template <int ROWS, bool KMAJ>
+__device__ __forceinline__ bf16x8 frag(const uint16_t* __restrict__ S, int rc, int s, int lane) {
+  if constexpr (!KMAJ) {
+    const int h = lane >> 5;
+    return *reinterpret_cast<const bf16x8*>(S + img_off<ROWS, false>(rc, 16 * s + 8 * h));
+  } else {
+    // ds_read_b64_tr_b16: lane 4q + p of a 16-lane group supplies the address of block row
+    // q (k), columns 4p .. 4p + 3 (rows of the operand); the group's block is k-rows
+    // kb .. kb + 3 x operand rows m0 .. m0 + 15, and lane i of the group receives row m0 + i.
+    // rc = tile base row + (lane & 31); the group's m0 = rc - (lane & 15).
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int m = rc - (lane & 15) + 4 * p;
+    const int kb = 16 * s + 8 * (g >> 1);
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (lds_bf16x4*)(S + img_off<ROWS, true>(m, kb + q)));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (lds_bf16x4*)(S + img_off<ROWS, true>(m, kb + 4 + q)));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
+__device__ __forceinline__ uint16_t f2bf(float x) {
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(x));
+}
+
+// row sums of the A tile in LDS over its BK k-values (thread t: row t % BM, k-group t / BM)
+template <int BM, bool AK>
+__device__ __forceinline__ float img_rowsum(const uint16_t* __restrict__ As, int tid) {
+  constexpr int G = kThreads / BM;
+  const int m = tid % BM, g = tid / BM;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < BK / G; ++i) s += bf2f(As[img_off<BM, AK>(m, g + i * G)]);
+  return s;
+}
+
+// epilogue through LDS: the accumulator tile is transposed into a [BM][BN] f32 image and
+// written row-major, 4 consecutive outputs per thread (16-B f32 / 8-B bf16 stores)
+template <int BM, int BN, int EPI, bool OBF>
+__device__ __forceinline__ void finish_tile(const f32x16 (&acc)[BM / 64][BN / 64], float rs, bool do_rs,
+                                            float* __restrict__ lds, int tid, int m0, int n0, int M, int N,
+                                            float alpha, float beta, void* __restrict__ Cv, int64_t ldc,
+                                            const float* __restrict__ bias, float slope,
+                                            const uint16_t* __restrict__ dact, int64_t lddact,
+                                            float* __restrict__ rowsum, float* __restrict__ ws,
+                                            float* __restrict__ ws_rowsum) {
+  constexpr bool SPLIT = EPI == EPI_SPLIT;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+  if (do_rs) {
+    lds[tid] = rs;
+    __syncthreads();
+    if (tid < BM && m0 + tid < M) {
+      float t = 0.f;
+      for (int g = 0; g < kThreads / BM; ++g) t += lds[g * BM + tid];
+      if constexpr (SPLIT) ws_rowsum[(int64_t)blockIdx.z * M + m0 + tid] = t;
+      else rowsum[m0 + tid] = t;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        lds[row * BN + wn * (BN / 2) + j * 32 + l32] = acc[i][j][r];
+      }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < BM * BN / 4 / kThreads; ++it) {
+    const int u = it * kThreads + tid;
+    const int row = u / (BN / 4), c = (u % (BN / 4)) * 4;
+    const int gr = m0 + row, gc = n0 + c;
+    if (gr >= M || gc >= N) continue;
+    const float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
+    if constexpr (SPLIT) {
+      *reinterpret_cast<float4*>(ws + ((int64_t)blockIdx.z * M + gr) * N + gc) = v;
+    } else {
+      float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
+      if constexpr (OBF) {
+        uint16_t* cp = (uint16_t*)Cv + (int64_t)gr * ldc + gc;
+        if (beta != 0.f) {
+          const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
+          o[0] = o[0] + beta * bf2f(c2.x & 0xFFFF); o[1] = o[1] + beta * bf2f(c2.x >> 16);
+          o[2] = o[2] + beta * bf2f(c2.y & 0xFFFF); o[3] = o[3] + beta * bf2f(c2.y >> 16);
+        }
+        if (bias) {
+          const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
+          o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
+        }
+        float y[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
+          const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
+          y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
+        }
+        uint2 w;
+        w.x = (uint32_t)f2bf(epi_apply<EPI>(o[0], y[0], slope)) |
+              ((uint32_t)f2bf(epi_apply<EPI>(o[1], y[1], slope)) << 16);
+        w.y = (uint32_t)f2bf(epi_apply<EPI>(o[2], y[2], slope)) |
+              ((uint32_t)f2bf(epi_apply<EPI>(o[3], y[3], slope)) << 16);
+        *reinterpret_cast<uint2*>(cp) = w;
+      } else {
+        float* cp = (float*)Cv + (int64_t)gr * ldc + gc;
+        if (beta != 0.f) {
+          const float4 c4 = *reinterpret_cast<const float4*>(cp);
+          o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
+          o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
+        }
+        if (bias) {
+          const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
+          o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
+        }
+        float y[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
+          const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
+          y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
+        }
+        *reinterpret_cast<float4*>(cp) =
+            make_float4(epi_apply<EPI>(o[0], y[0], slope), epi_apply<EPI>(o[1], y[1], slope),
+                        epi_apply<EPI>(o[2], y[2], slope), epi_apply<EPI>(o[3], y[3], slope));
+      }
+    }
+  }
+}
+
+template <int BM, int BN, bool TA, bool TB, int EPI, bool OBF>
+__global__ __launch_bounds__(kThreads) void gemm_bf16_kernel(
+    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
+    const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+    float beta, void* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
+    const uint16_t* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
+    float* __restrict__ ws, float* __restrict__ ws_rowsum) {
+  constexpr bool AK = TA, BKM = !TB;  // k images for A stored [k][m] / B stored [k][n]
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int IA = BM * BK, IB = BN * BK;  // image sizes (u16)
+  // one LDS array [A0 | A1 | B0 | B1]; the epilogue reuses it as a [BM][BN] f32 image
+  constexpr int STAGE = 2 * (IA + IB);
+  constexpr int EPI_U16 = 2 * BM * BN;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[STAGE > EPI_U16 ? STAGE : EPI_U16];
+
+  // XCD-aware tile order (as gemm.hip): blocks b, b + 8, ... share an XCD and get a
+  // contiguous run of row-major tile ids, so the tiles sharing A rows meet in one L2
+  const int b = blockIdx.x;
+  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
+  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, l32 = lane & 31;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kz0 = blockIdx.z * k_per_split;
+  const int kz1 = min(K, kz0 + k_per_split);
+  const bool do_rs = rowsum != nullptr && tn == 0;
+  float rs = 0.f;
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = kz1 > kz0 ? (kz1 - kz0 + BK - 1) / BK : 0;
+  auto issue = [&](int t, int buf) {
+    const int k0 = kz0 + t * BK;
+    if (kz1 - k0 >= BK) {
+      dma_tile<BM, AK, true>(A, lda, m0, M, k0, BK, lds + buf * IA, wave, lane);
+      dma_tile<BN, BKM, true>(B, ldb, n0, N, k0, BK, lds + 2 * IA + buf * IB, wave, lane);
+    } else {
+      dma_tile<BM, AK, false>(A, lda, m0, M, k0, kz1 - k0, lds + buf * IA, wave, lane);
+      dma_tile<BN, BKM, false>(B, ldb, n0, N, k0, kz1 - k0, lds + 2 * IA + buf * IB, wave, lane);
+    }
+  };
+
+  if (nk > 0) {
+    issue(0, 0);
+    __syncthreads();
+    const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
+    bf16x8 fa[2][TM], fb[2][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[0][i] = frag<BM, AK>(lds, ra + i * 32, 0, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[0][j] = frag<BN, BKM>(lds + 2 * IA, rb + j * 32, 0, lane);
+    for (int t = 0; t < nk; ++t) {
+      const int cur = t & 1;
+      const bool more = t + 1 < nk;
+      if (more) issue(t + 1, cur ^ 1);
+      const uint16_t* As = lds + cur * IA;
+      const uint16_t* Bs = lds + 2 * IA + cur * IB;
+      if (do_rs) rs += img_rowsum<BM, AK>(As, tid);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int u = s & 1;
+        if (s < 3) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa[u ^ 1][i] = frag<BM, AK>(As, ra + i * 32, s + 1, lane);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb[u ^ 1][j] = frag<BN, BKM>(Bs, rb + j * 32, s + 1, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[u][i], fb[u][j], acc[i][j], 0, 0, 0);
+        if (s == 2) {
+          __syncthreads();  // tile t+1 landed and every wave is past its reads of tile t-1
+          if (more) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) fa[0][i] = frag<BM, AK>(lds + (cur ^ 1) * IA, ra + i * 32, 0, lane);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              fb[0][j] = frag<BN, BKM>(lds + 2 * IA + (cur ^ 1) * IB, rb + j * 32, 0, lane);
+          }
+        }
+      }
+    }
+    __syncthreads();  // the epilogue reuses the staging array
+  }
+  finish_tile<BM, BN, EPI, OBF>(acc, rs, do_rs, reinterpret_cast<float*>(lds), tid, m0, n0, M, N, alpha,
+                                beta, C, ldc, bias, slope, dact, lddact, rowsum, ws, ws_rowsum);
+}
+
+struct Args {
+  int M, N, K, kps, tiles_n, tiles;
+  float alpha;
+  const uint16_t* A;
+  int64_t lda;
+  const uint16_t* B;
+  int64_t ldb;
+  float beta;
+  void* C;
+  int64_t ldc;
+  const float* bias;
+  float slope;
+  const uint16_t* dact;
+  int64_t lddact;
+  float* rowsum;
+  float* ws;
+  float* ws_rowsum;
+};
+
+template <int BM, int BN, bool TA, bool TB, bool OBF>
+int launch_epi(int epi, dim3 grid, hipStream_t st, const Args& a) {
+#define PG_L(EPI_)                                                                              \
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, EPI_, OBF>), grid, dim3(kThreads), 0, st, \
+                     a.M, a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb,   \
+                     a.beta, a.C, a.ldc, a.bias, a.slope, a.dact, a.lddact, a.rowsum, a.ws,      \
+                     a.ws_rowsum)
+  switch (epi) {
+    case EPI_NONE: PG_L(EPI_NONE); break;
+    case EPI_RELU: PG_L(EPI_RELU); break;
+    case EPI_LEAKY: PG_L(EPI_LEAKY); break;
+    case EPI_DRELU: PG_L(EPI_DRELU); break;
+    case EPI_DLEAKY: PG_L(EPI_DLEAKY); break;
+    case EPI_SPLIT:
+      if constexpr (!OBF) {
+        PG_L(EPI_SPLIT);
+        break;
+      }
+      return PG_ERR_INVALID;
+    default: return PG_ERR_INVALID;
+  }
+#undef PG_L
+  return PG_OK;
+}
+
+template <int BM, int BN>
+int launch_tile(bool ta, bool tb, bool obf, int epi, dim3 grid, hipStream_t st, const Args& a) {
+#define PG_T(TA_, TB_)                                              \
+  return obf ? launch_epi<BM, BN, TA_, TB_, true>(epi, grid, st, a) \
+             : launch_epi<BM, BN, TA_, TB_, false>(epi, grid, st, a)
+  if (!ta && !tb) PG_T(false, false);
+  if (!ta && tb) PG_T(false, true);
+  if (ta && !tb) PG_T(true, false);
+  PG_T(true, true);
+#undef PG_T
+}
+
+// Tile choice: 128 x 128 while that still gives >= 2 workgroups per CU (LDS holds two
+// 64-KiB workgroups), else 128 x 64, else 64 x 64. Split products run 64 x 64.
+inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
+  static const int forced = [] {  // tuning knob PLAGNN_GEMM_BF16_TILE = "BMxBN"
+    const char* e = getenv("PLAGNN_GEMM_BF16_TILE");
+    if (!e) return 0;
+    int a = 0, b = 0;
+    if (sscanf(e, "%dx%d", &a, &b) != 2 || (a != 64 && a != 128) || (b != 64 && b != 128)) return 0;
+    return a * 1000 + b;
+  }();
+  if (forced) {
+    bm = forced / 1000;
+    bn = forced % 1000;
+    return;
+  }
+  auto tiles = [&](int tm, int tn) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
+  bm = bn = 64;
+  if (split > 1) return;
+  if (N > 64 && tiles(128, 128) >= 512) {
+    bm = bn = 128;
+  } else if (tiles(128, 64) >= 512) {
+    bm = 128;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pg_gemm_bf16_split_k(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K < 2048) return 1;
+  int bm, bn;
+  pick_tile(M, N, 1, bm, bn);
+  if (((M + bm - 1) / bm) * ((N + bn - 1) / bn) >= 768) return 1;
+  const int64_t tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  const int64_t target = (1280 + tiles - 1) / tiles;  // ~5 workgroups per CU
+  const int64_t by_k = K / (3 * BK);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, by_k), 256));
+}
+
+size_t pg_gemm_bf16_workspace(int64_t M, int64_t N, int64_t K, int split_k) {
+  (void)K;
+  if (split_k <= 1 || M <= 0 || N <= 0) return 0;
+  return (size_t)split_k * (size_t)M * (size_t)(N + 1) * 4;
+}
+
+int pg_gemm_bf16(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
+                 const void* A, int64_t lda, const void* B, int64_t ldb, float beta, void* C,
+                 int64_t ldc, int c_dtype, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
+                 size_t ws_bytes, pg_stream_t stream) {
+  const pg_gemm_epilogue_t none{nullptr, PG_ACT_NONE, 0.f, nullptr, 0, nullptr};
+  if (!ep) ep = &none;
+  const int act = ep->act;
+  if (M < 0 || N < 0 || K < 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_bf16: bad sizes");
+  if (c_dtype != PG_DTYPE_F32 && c_dtype != PG_DTYPE_BF16)
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_bf16: c_dtype must be PG_DTYPE_F32 or PG_DTYPE_BF16");
+  if (ldc < N || (!transa && lda < K) || (transa && lda < M) || (!transb && ldb < N) ||
+      (transb && ldb < K))
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_bf16: leading dimension too small");
+  if (act != PG_ACT_NONE && act != PG_ACT_RELU && act != PG_ACT_LEAKY)
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_bf16: bad act %d", act);
+  if (split_k < 1) split_k = 1;
+  const bool obf = c_dtype == PG_DTYPE_BF16;
+  if (split_k > 1 && (obf || ep->bias || act != PG_ACT_NONE || ep->dact || (beta != 0.f && beta != 1.f)))
+    return pg::set_error(PG_ERR_INVALID,
+                         "pg_gemm_bf16: split_k > 1 needs an f32 C, no bias/act, beta 0|1");
+  if (ep->dact && (act == PG_ACT_NONE || ep->lddact < N))
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_bf16: dact needs act relu|leaky and lddact >= N");
+  if (M == 0 || N == 0) return pg::ok();
+  // operand layout requirements of the DMA staging (16-B units of 8 bf16)
+  const int64_t ext_a = transa ? M : K, ext_b = transb ? K : N;
+  if (!al16(A) || !al16(B) || !al16(C) || lda % 8 || ldb % 8 || ext_a % 8 || ext_b % 8 || N % 4 ||
+      ldc % (obf ? 4 : 4) || (ep->bias && !al16(ep->bias)) ||
+      (ep->dact && (((uintptr_t)ep->dact & 7) || ep->lddact % 4)))
+    return pg::set_error(PG_ERR_UNSUPPORTED,
+                         "pg_gemm_bf16: operands must be 16-B aligned with leading dimensions and "
+                         "contiguous extents multiples of 8, N and ldc multiples of 4");
+  if (split_k > 1 && ws_bytes < pg_gemm_bf16_workspace(M, N, K, split_k))
+    return pg::set_error(PG_ERR_WORKSPACE, "pg_gemm_bf16: workspace too small");
+  if (split_k > 1 && !al16(ws)) return pg::set_error(PG_ERR_INVALID, "pg_gemm_bf16: workspace alignment");
+  int kps = (int)K;
+  if (split_k > 1) {
+    kps = (int)((K + split_k - 1) / split_k);
+    kps = (kps + BK - 1) / BK * BK;
+    split_k = (int)((K + kps - 1) / kps);
+    if (split_k < 1) split_k = 1;
+  }
+  const bool split = split_k > 1;
+  int bm, bn;
+  pick_tile(M, N, split_k, bm, bn);
+  // a k image needs >= 8 valid rows for its clamped 16-B chunks
+  if ((transa && M < 8) || (!transb && N < 8))
+    return pg::set_error(PG_ERR_UNSUPPORTED, "pg_gemm_bf16: row-contiguous operand narrower than 8");
+  const int tiles_n = (int)((N + bn - 1) / bn);
+  const int tiles = tiles_n * (int)((M + bm - 1) / bm);
+  dim3 grid((unsigned)tiles, 1, (unsigned)split_k);
+  hipStream_t st = (hipStream_t)stream;
+  float* wsf = split ? (float*)ws : nullptr;
+  const Args a{(int)M, (int)N, (int)K, kps, tiles_n, tiles, alpha, (const uint16_t*)A, lda,
+               (const uint16_t*)B, ldb, beta, C, ldc, ep->bias, ep->slope,
+               (const uint16_t*)ep->dact, ep->lddact, ep->rowsum, wsf,
+               split ? wsf + (int64_t)split_k * M * N : nullptr};
+  const bool ta = transa != 0, tb = transb != 0;
+  const int epi = split ? EPI_SPLIT
+                        : ep->dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
+                                   : (act == PG_ACT_RELU ? EPI_RELU : act == PG_ACT_LEAKY ? EPI_LEAKY : EPI_NONE);
+  int rc;
+  if (bm == 128 && bn == 128) rc = launch_tile<128, 128>(ta, tb, obf, epi, grid, st, a);
+  else if (bm == 128) rc = launch_tile<128, 64>(ta, tb, obf, epi, grid, st, a);
+  else if (bn == 128) rc = launch_tile<64, 128>(ta, tb, obf, epi, grid, st, a);
+  else rc = launch_tile<64, 64>(ta, tb, obf, epi, grid, st, a);
+  if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_bf16: dispatch failed");
+  if (split) {
+    const int64_t n = M * N + (ep->rowsum ? M : 0);
+    const int G = splitk_groups(split_k);
+    const int opb = 256 / G;
+    const int blocks = (int)std::min<int64_t>(8192, (n + opb - 1) / opb);
+#define PG_R(G_)                                                                              \
+  hipLaunchKernelGGL(splitk_reduce_kernel<G_>, dim3(blocks), dim3(256), 0, st, (const float*)wsf, \
+                     split_k, (int)M, (int)N, alpha, beta, (float*)C, ldc, (const float*)a.ws_rowsum, \
+                     ep->rowsum)
+    if (G == 1) PG_R(1);
+    else if (G == 4) PG_R(4);
+    else PG_R(16);
+#undef PG_R
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return pg::set_error((int)e, "pg_gemm_bf16: launch failed: %s", hipGetErrorString(e));
+  return pg::ok();
+}
+
+}  // extern "C"

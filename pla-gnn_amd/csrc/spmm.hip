@@ -44,29 +44,56 @@ __device__ __forceinline__ int wave_id_uniform() {
 }
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// ---- element types: float, or bf16 storage (uint16_t bits) computed in f32 ------------
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+template <typename T>
+__device__ __forceinline__ T from_f(float x);
+template <>
+__device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <>
+__device__ __forceinline__ uint16_t from_f<uint16_t>(float x) {  // round to nearest even
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(x));
+}
+
 // ---- per-lane feature tile access ----------------------------------------------------
-template <int W>
-__device__ __forceinline__ void load_tile(const float* __restrict__ row, int f, int F,
+template <int W, typename T = float>
+__device__ __forceinline__ void load_tile(const T* __restrict__ row, int f, int F,
                                           float (&r)[W], float fill) {
   if constexpr (W == 4) {
     if (f < F) {
-      const float4 t = *reinterpret_cast<const float4*>(row + f);
-      r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+      if constexpr (sizeof(T) == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(row + f);
+        r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+      } else {
+        const uint2 t = *reinterpret_cast<const uint2*>(row + f);
+        r[0] = to_f((uint16_t)(t.x & 0xFFFF)); r[1] = to_f((uint16_t)(t.x >> 16));
+        r[2] = to_f((uint16_t)(t.y & 0xFFFF)); r[3] = to_f((uint16_t)(t.y >> 16));
+      }
     } else {
       r[0] = r[1] = r[2] = r[3] = fill;
     }
   } else {
-    r[0] = f < F ? row[f] : fill;
+    r[0] = f < F ? to_f(row[f]) : fill;
   }
 }
 
-template <int W>
-__device__ __forceinline__ void store_tile(float* __restrict__ row, int f, int F,
+template <int W, typename T = float>
+__device__ __forceinline__ void store_tile(T* __restrict__ row, int f, int F,
                                            const float (&r)[W]) {
   if constexpr (W == 4) {
-    if (f < F) *reinterpret_cast<float4*>(row + f) = make_float4(r[0], r[1], r[2], r[3]);
+    if (f < F) {
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<float4*>(row + f) = make_float4(r[0], r[1], r[2], r[3]);
+      } else {
+        uint2 t;
+        t.x = (uint32_t)from_f<uint16_t>(r[0]) | ((uint32_t)from_f<uint16_t>(r[1]) << 16);
+        t.y = (uint32_t)from_f<uint16_t>(r[2]) | ((uint32_t)from_f<uint16_t>(r[3]) << 16);
+        *reinterpret_cast<uint2*>(row + f) = t;
+      }
+    }
   } else {
-    if (f < F) row[f] = r[0];
+    if (f < F) row[f] = from_f<T>(r[0]);
   }
 }
 
@@ -125,12 +152,12 @@ struct EdgeU {
 };
 
 // ---- max forward ---------------------------------------------------------------------
-template <int W, int NC, bool HAS_W, typename A>
+template <int W, int NC, bool HAS_W, typename A, typename T = float>
 __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
     const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
     const int32_t* __restrict__ eslot, const float* __restrict__ ew,
-    const int4* __restrict__ items, int n_items, const float* __restrict__ X, int64_t ldx, int F,
-    float* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
+    const int4* __restrict__ items, int n_items, const T* __restrict__ X, int64_t ldx, int F,
+    T* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
     float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw) {
   constexpr int U = EdgeU<W, NC>::value;
   const int it = blockIdx.x * kWavesPerBlock + wave_id_uniform();
@@ -162,9 +189,9 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
       float v[U][NC][W];
 #pragma unroll
       for (int e = 0; e < U; ++e) {
-        const float* xr = X + (int64_t)bcast(idxv, j + min(e, nv - 1)) * ldx;
+        const T* xr = X + (int64_t)bcast(idxv, j + min(e, nv - 1)) * ldx;
 #pragma unroll
-        for (int c = 0; c < NC; ++c) load_tile<W>(xr, (c * kWave + lane) * W, F, v[e][c], ninf);
+        for (int c = 0; c < NC; ++c) load_tile<W, T>(xr, (c * kWave + lane) * W, F, v[e][c], ninf);
       }
 #pragma unroll
       for (int e = 0; e < U; ++e) {
@@ -194,12 +221,12 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
 #pragma unroll
       for (int i = 0; i < W; ++i)
         if (__builtin_isinf(best[c][i])) best[c][i] = 0.f;
-    float* orow = out + (int64_t)row * ldo;
+    T* orow = out + (int64_t)row * ldo;
     A* arow = arg + (int64_t)row * lda;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int f = (c * kWave + lane) * W;
-      store_tile<W>(orow, f, F, best[c]);
+      store_tile<W, T>(orow, f, F, best[c]);
       store_arg<W, A>(arow, f, F, bpos[c]);
     }
   } else {
@@ -216,12 +243,12 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
 
 // Combine the partial maxima of split rows in chunk order (earlier chunk wins ties).
 // One workgroup per split row, one thread per feature; slot loads batched.
-template <typename A>
+template <typename A, typename T = float>
 __global__ __launch_bounds__(kBlock) void max_merge_kernel(const int4* __restrict__ merges,
                                                            int n_merges, int F,
                                                            const float* __restrict__ ws_val,
                                                            const A* __restrict__ ws_arg,
-                                                           int64_t ldw, float* __restrict__ out,
+                                                           int64_t ldw, T* __restrict__ out,
                                                            int64_t ldo, A* __restrict__ arg,
                                                            int64_t lda) {
   const int4 m = merges[blockIdx.x];
@@ -241,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void max_merge_kernel(const int4* __restric
         }
     }
     if (__builtin_isinf(best)) best = 0.f;
-    out[(int64_t)row * ldo + f] = best;
+    out[(int64_t)row * ldo + f] = from_f<T>(best);
     arg[(int64_t)row * lda + f] = (A)bp;
   }
 }
@@ -394,10 +421,10 @@ __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   return total;
 }
 
-template <typename A>
+template <typename A, typename T>
 __device__ __forceinline__ void pack_short_row(
     int v, int wave, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
-    const A* __restrict__ arg, int64_t lda, int F, const float* __restrict__ dout, int64_t ldd,
+    const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
     uint16_t* __restrict__ gfeat, int2* __restrict__ glist, float* __restrict__ dpack,
     int* __restrict__ lds) {
   constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
@@ -407,14 +434,14 @@ __device__ __forceinline__ void pack_short_row(
   const int rs = ptr[v];
   const int re = ptr[v + 1];
   const A* ar = arg + (int64_t)v * lda;
-  const float* dr = dout + (int64_t)v * ldd;
+  const T* dr = dout + (int64_t)v * ldd;
   int a[MAXW];
   float d[MAXW];
 #pragma unroll
   for (int i = 0; i < MAXW; ++i) {
     const int f = lane + i * kWave;
     a[i] = f < F ? (int)ar[f] : arg_none<A>();
-    d[i] = f < F ? dr[f] : 0.f;
+    d[i] = f < F ? to_f(dr[f]) : 0.f;
   }
   const int deg = re - rs;
   if (deg > kPackWaveMax || deg == 0) return;
@@ -468,10 +495,10 @@ __device__ __forceinline__ void pack_short_row(
     }
 }
 
-template <typename A>
+template <typename A, typename T>
 __device__ __forceinline__ void pack_long_row(
     int v, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
-    const A* __restrict__ arg, int64_t lda, int F, const float* __restrict__ dout, int64_t ldd,
+    const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
     uint16_t* __restrict__ gfeat, int2* __restrict__ glist, float* __restrict__ dpack,
     int* __restrict__ lds) {
   int* hist = lds;
@@ -487,14 +514,14 @@ __device__ __forceinline__ void pack_long_row(
     // independent loads first (each thread its own features), placement straight to the
     // list slots as in the wave form
     constexpr int FPT = kGroupMaxF / kBlock;
-    const float* dr = dout + (int64_t)v * ldd;
+    const T* dr = dout + (int64_t)v * ldd;
     int a[FPT];
     float d[FPT];
 #pragma unroll
     for (int i = 0; i < FPT; ++i) {
       const int f = threadIdx.x + i * kBlock;
       a[i] = f < F ? (int)ar[f] : arg_none<A>();
-      d[i] = f < F ? dr[f] : 0.f;
+      d[i] = f < F ? to_f(dr[f]) : 0.f;
     }
     for (int p = threadIdx.x; p < deg; p += kBlock) hist[p] = 0;
     __syncthreads();
@@ -576,11 +603,11 @@ __device__ __forceinline__ void pack_long_row(
     for (int i = threadIdx.x; i < total; i += kBlock) feats[i] = (uint16_t)(keys[i] & 0xFFFFu);
     __syncthreads();
   }
-  const float* dr = dout + (int64_t)v * ldd;
+  const T* dr = dout + (int64_t)v * ldd;
   for (int i = threadIdx.x; i < total; i += kBlock) {
     const int f = feats[i];
     gfeat[(int64_t)vF + i] = (uint16_t)f;
-    dpack[(int64_t)vF + i] = dr[f];
+    dpack[(int64_t)vF + i] = to_f(dr[f]);
   }
 }
 
@@ -591,20 +618,20 @@ __device__ __forceinline__ void pack_long_row(
 constexpr int kPackLds = kHistMax + 8 + kGroupMaxF / 2 + 4;
 static_assert(kPackLds >= kWavesPerBlock * (kPackWaveMax + 4), "pack LDS");
 
-template <typename A>
+template <typename A, typename T = float>
 __global__ __launch_bounds__(kBlock) void group_pack_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
     const int32_t* __restrict__ einv, const A* __restrict__ arg, int64_t lda, int F,
-    const float* __restrict__ dout, int64_t ldd, uint16_t* __restrict__ gfeat,
+    const T* __restrict__ dout, int64_t ldd, uint16_t* __restrict__ gfeat,
     int2* __restrict__ glist, float* __restrict__ dpack) {
   __shared__ __attribute__((aligned(16))) int lds[kPackLds];
   const int b = blockIdx.x;
   if (b < n_long) {
-    pack_long_row<A>(rows ? rows[b].x : b, ptr, einv, arg, lda, F, dout, ldd, gfeat, glist, dpack, lds);
+    pack_long_row<A, T>(rows ? rows[b].x : b, ptr, einv, arg, lda, F, dout, ldd, gfeat, glist, dpack, lds);
   } else {
     const int wave = wave_id_uniform();
     const int v = (b - n_long) * kWavesPerBlock + wave;
-    if (v < n_rows) pack_short_row<A>(v, wave, ptr, einv, arg, lda, F, dout, ldd, gfeat, glist, dpack, lds);
+    if (v < n_rows) pack_short_row<A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, gfeat, glist, dpack, lds);
   }
 }
 
@@ -614,12 +641,12 @@ __global__ __launch_bounds__(kBlock) void invert_slots_kernel(const int32_t* __r
     einv[tslot[t]] = (int32_t)t;
 }
 
-template <bool HAS_W>
+template <bool HAS_W, typename T = float>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const float* __restrict__ ew, const int32_t* __restrict__ tslot,
     const int4* __restrict__ items, int n_items, const int2* __restrict__ glist,
     const uint16_t* __restrict__ gfeat, const float* __restrict__ dpack, int F,
-    const float* __restrict__ mask, int64_t ldm, float* __restrict__ dx, int64_t ldx,
+    const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx,
     float* __restrict__ ws, int64_t ldw) {
   constexpr int U = 16;
   __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
@@ -655,9 +682,9 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
       if (lane >= o) incl += y;
     }
     const int excl = incl - nseg;
-    const int T = bcast(incl, kWave - 1);
-    for (int s0 = 0; s0 < T; s0 += U) {
-      const int nv = min(U, T - s0);
+    const int nseg_all = bcast(incl, kWave - 1);
+    for (int s0 = 0; s0 < nseg_all; s0 += U) {
+      const int nv = min(U, nseg_all - s0);
       int fe[U], ie[U], ne[U];
       float de[U];
 #pragma unroll
@@ -685,12 +712,12 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   }
   wave_lds_sync();
   if (slot < 0) {
-    float* xr = dx + (int64_t)row * ldx;
-    const float* mr = mask ? mask + (int64_t)row * ldm : nullptr;
+    T* xr = dx + (int64_t)row * ldx;
+    const T* mr = mask ? mask + (int64_t)row * ldm : nullptr;
     for (int f = lane; f < F; f += kWave) {
       float a = acc[f];
-      if (mr && !(mr[f] > 0.f)) a = 0.f;
-      xr[f] = a;
+      if (mr && !(to_f(mr[f]) > 0.f)) a = 0.f;
+      xr[f] = from_f<T>(a);
     }
   } else {
     float* wr = ws + (int64_t)slot * ldw;
@@ -700,10 +727,11 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
 
 // Sum partial slots in order; optional relu' mask (bwd) or 1/deg (mean fwd).
 // One workgroup per split row, one thread per feature.
+template <typename T = float>
 __global__ __launch_bounds__(kBlock) void sum_merge_kernel(
     const int4* __restrict__ merges, int n_merges, int F, const float* __restrict__ ws,
     int64_t ldw, const int32_t* __restrict__ ptr, int divide_by_deg,
-    const float* __restrict__ mask, int64_t ldm, float* __restrict__ out, int64_t ldo) {
+    const T* __restrict__ mask, int64_t ldm, T* __restrict__ out, int64_t ldo) {
   const int4 m = merges[blockIdx.x];
   const int row = m.x, s0 = m.y, ns = m.z;
   const float deg = divide_by_deg ? (float)(ptr[row + 1] - ptr[row]) : 1.f;
@@ -718,8 +746,8 @@ __global__ __launch_bounds__(kBlock) void sum_merge_kernel(
         if (s + e < s0 + ns) acc += v[e];
     }
     if (divide_by_deg) acc = acc / deg;
-    if (mask && !(mask[(int64_t)row * ldm + f] > 0.f)) acc = 0.f;
-    out[(int64_t)row * ldo + f] = acc;
+    if (mask && !(to_f(mask[(int64_t)row * ldm + f]) > 0.f)) acc = 0.f;
+    out[(int64_t)row * ldo + f] = from_f<T>(acc);
   }
 }
 
@@ -926,8 +954,8 @@ inline TilePlan plan_tiles(int64_t F, std::initializer_list<int64_t> lds,
   return {vec, vec ? vec_ftile() : (int64_t)kFTileScalar};
 }
 
-template <typename A>
-int launch_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
+template <typename A, typename T>
+int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
                    int64_t ldo, A* arg, int64_t lda, float* ws_val, A* ws_arg, int64_t ldw,
                    hipStream_t st) {
   // argpos rows: u16 x4 = 8 B -> need 8-B alignment only; treat via the same 16-B check on
@@ -945,7 +973,7 @@ int launch_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, fl
       constexpr int NC = decltype(nc_c)::value;
       constexpr int W = decltype(w_c)::value;
       constexpr bool HW = decltype(hw_c)::value;
-      hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A>), dim3(blocks), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T>), dim3(blocks), dim3(kBlock), 0, st,
                          g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
                          X + f0, ldx, Ft, out + f0, ldo, arg + f0, lda,
                          ws_val ? ws_val + f0 : nullptr, ws_arg ? ws_arg + f0 : nullptr, ldw);
@@ -963,7 +991,7 @@ int launch_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, fl
     }
     if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_max_fwd: unsupported feature tile");
     if (g->n_merges > 0) {
-      hipLaunchKernelGGL((max_merge_kernel<A>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL((max_merge_kernel<A, T>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
                          (const int4*)g->merges, (int)g->n_merges, Ft, ws_val + f0, ws_arg + f0,
                          ldw, out + f0, ldo, arg + f0, lda);
     }
@@ -1005,7 +1033,7 @@ int launch_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const A* arg, int64_t 
     }
     if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_max_bwd: unsupported feature tile");
     if (gt->n_merges > 0) {
-      hipLaunchKernelGGL(sum_merge_kernel, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL(sum_merge_kernel<float>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
                          (const int4*)gt->merges, (int)gt->n_merges, Ft, ws + f0, ldw, gt->ptr, 0,
                          mask ? mask + f0 : nullptr, ldm, dx + f0, ldx);
     }
@@ -1031,9 +1059,14 @@ size_t pg_spmm_max_fwd_workspace(const pg_csr_t* g, int64_t F, int arg_kind) {
   return vals + args;
 }
 
-int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
-                    int64_t ldo, void* argpos, int64_t lda, int arg_kind, void* ws,
-                    size_t ws_bytes, pg_stream_t stream) {
+}  // extern "C"
+
+namespace {
+
+template <typename T>
+int max_fwd_entry(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out, int64_t ldo,
+                  void* argpos, int64_t lda, int arg_kind, void* ws, size_t ws_bytes,
+                  pg_stream_t stream) {
   PG_TRY(pg::check_csr(g, "pg_spmm_max_fwd", true));
   if (!pg::valid_arg_kind(arg_kind))
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: bad arg_kind %d", arg_kind);
@@ -1051,10 +1084,27 @@ int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, f
   void* ws_arg = need ? (char*)ws + round_up(g->n_slots * ldw * 4, 256) : nullptr;
   hipStream_t st = (hipStream_t)stream;
   if (arg_kind == PG_ARG_U16)
-    return launch_max_fwd<uint16_t>(g, X, ldx, F, out, ldo, (uint16_t*)argpos, lda, ws_val,
-                                    (uint16_t*)ws_arg, ldw, st);
-  return launch_max_fwd<int32_t>(g, X, ldx, F, out, ldo, (int32_t*)argpos, lda, ws_val,
-                                 (int32_t*)ws_arg, ldw, st);
+    return launch_max_fwd<uint16_t, T>(g, X, ldx, F, out, ldo, (uint16_t*)argpos, lda, ws_val,
+                                       (uint16_t*)ws_arg, ldw, st);
+  return launch_max_fwd<int32_t, T>(g, X, ldx, F, out, ldo, (int32_t*)argpos, lda, ws_val,
+                                    (int32_t*)ws_arg, ldw, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
+                    int64_t ldo, void* argpos, int64_t lda, int arg_kind, void* ws,
+                    size_t ws_bytes, pg_stream_t stream) {
+  return max_fwd_entry<float>(g, X, ldx, F, out, ldo, argpos, lda, arg_kind, ws, ws_bytes, stream);
+}
+
+int pg_spmm_max_fwd_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t F, void* out,
+                         int64_t ldo, void* argpos, int64_t lda, int arg_kind, void* ws,
+                         size_t ws_bytes, pg_stream_t stream) {
+  return max_fwd_entry<uint16_t>(g, (const uint16_t*)X, ldx, F, (uint16_t*)out, ldo, argpos, lda,
+                                 arg_kind, ws, ws_bytes, stream);
 }
 
 // [split-row partials][grouped path: gfeat N x F u16 | glist nnz x int2 | dpack N x F f32 |
@@ -1074,10 +1124,14 @@ size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
   return b;
 }
 
-int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
-                    int arg_kind, const float* dout, int64_t ldd, int64_t F,
-                    const float* mask_src, int64_t ldm, float* dx, int64_t ldx, void* ws,
-                    size_t ws_bytes, pg_stream_t stream) {
+}  // extern "C"
+
+namespace {
+
+template <typename T>
+int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
+                  int arg_kind, const T* dout, int64_t ldd, int64_t F, const T* mask_src,
+                  int64_t ldm, T* dx, int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream) {
   PG_TRY(pg::check_csr(g, "pg_spmm_max_bwd", false));
   PG_TRY(pg::check_csr(gt, "pg_spmm_max_bwd", true));
   if (!pg::valid_arg_kind(arg_kind))
@@ -1122,29 +1176,56 @@ int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, i
     const bool listed = g->merges != nullptr && g->chunk > 0 && g->chunk <= kPackWaveMax;
     const int n_long = (int)(listed ? g->n_merges : N);
     const int n_short_blocks = (int)((N + kWavesPerBlock - 1) / kWavesPerBlock);
-    hipLaunchKernelGGL((group_pack_kernel<uint16_t>), dim3((unsigned)(n_long + n_short_blocks)),
+    hipLaunchKernelGGL((group_pack_kernel<uint16_t, T>), dim3((unsigned)(n_long + n_short_blocks)),
                        dim3(kBlock), 0, st, listed ? (const int4*)g->merges : nullptr, n_long,
                        (int)N, g->ptr, einv, arg16, lda, (int)F, dout, ldd, gfeat, glist, dpack);
     const int blocks = grid_for(gt->n_items);
     if (g->ew)
-      hipLaunchKernelGGL((max_bwd_pull_kernel<true>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
+      hipLaunchKernelGGL((max_bwd_pull_kernel<true, T>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
                          gt->eslot, (const int4*)gt->items, (int)gt->n_items, glist, gfeat, dpack,
                          (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F));
     else
-      hipLaunchKernelGGL((max_bwd_pull_kernel<false>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
+      hipLaunchKernelGGL((max_bwd_pull_kernel<false, T>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
                          gt->eslot, (const int4*)gt->items, (int)gt->n_items, glist, gfeat, dpack,
                          (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F));
     if (gt->n_merges > 0)
-      hipLaunchKernelGGL(sum_merge_kernel, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
                          (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
                          mask_src, ldm, dx, ldx);
     return hip_status("pg_spmm_max_bwd");
   }
-  if (arg_kind == PG_ARG_U16)
-    return launch_max_bwd<uint16_t>(g, gt, (const uint16_t*)argpos, lda, dout, ldd, F, mask_src,
-                                    ldm, dx, ldx, w, ws_ld(F), st);
-  return launch_max_bwd<int32_t>(g, gt, (const int32_t*)argpos, lda, dout, ldd, F, mask_src, ldm,
-                                 dx, ldx, w, ws_ld(F), st);
+  if constexpr (sizeof(T) == 4) {
+    if (arg_kind == PG_ARG_U16)
+      return launch_max_bwd<uint16_t>(g, gt, (const uint16_t*)argpos, lda, dout, ldd, F, mask_src,
+                                      ldm, dx, ldx, w, ws_ld(F), st);
+    return launch_max_bwd<int32_t>(g, gt, (const int32_t*)argpos, lda, dout, ldd, F, mask_src, ldm,
+                                   dx, ldx, w, ws_ld(F), st);
+  } else {
+    return pg::set_error(PG_ERR_UNSUPPORTED,
+                         "pg_spmm_max_bwd_bf16: needs PG_ARG_U16 records and F <= %d (grouped path)",
+                         kGroupMaxF);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
+                    int arg_kind, const float* dout, int64_t ldd, int64_t F,
+                    const float* mask_src, int64_t ldm, float* dx, int64_t ldx, void* ws,
+                    size_t ws_bytes, pg_stream_t stream) {
+  return max_bwd_entry<float>(g, gt, argpos, lda, arg_kind, dout, ldd, F, mask_src, ldm, dx, ldx,
+                              ws, ws_bytes, stream);
+}
+
+int pg_spmm_max_bwd_bf16(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
+                         int arg_kind, const void* dout, int64_t ldd, int64_t F,
+                         const void* mask_src, int64_t ldm, void* dx, int64_t ldx, void* ws,
+                         size_t ws_bytes, pg_stream_t stream) {
+  return max_bwd_entry<uint16_t>(g, gt, argpos, lda, arg_kind, (const uint16_t*)dout, ldd, F,
+                                 (const uint16_t*)mask_src, ldm, (uint16_t*)dx, ldx, ws, ws_bytes,
+                                 stream);
 }
 
 int pg_spmm_max_bwd_scatter(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,
@@ -1242,7 +1323,7 @@ int pg_spmm_sum(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, int n
     }
     if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_sum: unsupported feature tile");
     if (g->n_merges > 0)
-      hipLaunchKernelGGL(sum_merge_kernel, dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL(sum_merge_kernel<float>, dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
                          (const int4*)g->merges, (int)g->n_merges, Ft, w + f0, ldw, g->ptr,
                          norm_mode == 1 ? 1 : 0, nullptr, 0, out + f0, ldo);
   }

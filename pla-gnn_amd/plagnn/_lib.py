@@ -17,6 +17,8 @@ LIB_PATH = os.environ.get("PLAGNN_LIB") or os.path.join(_HERE, "libplagnn.so")
 
 PG_ARG_U16 = 16
 PG_ARG_I32 = 32
+PG_DTYPE_F32 = 0
+PG_DTYPE_BF16 = 1
 PG_ACT_NONE = 0
 PG_ACT_RELU = 1
 PG_ACT_LEAKY = 2
@@ -106,6 +108,15 @@ SIGNATURES = {
     "pg_gemm_f32_workspace": (_sz, [_i64, _i64, _i64, _i]),
     "pg_gemm_f32": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _ep,
                          _i, _vp, _sz, _vp]),
+    "pg_gemm_bf16_split_k": (_i, [_i64, _i64, _i64]),
+    "pg_gemm_bf16_workspace": (_sz, [_i64, _i64, _i64, _i]),
+    "pg_gemm_bf16": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _i, _ep,
+                          _i, _vp, _sz, _vp]),
+    "pg_spmm_max_fwd_bf16": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i, _vp, _sz, _vp]),
+    "pg_spmm_max_bwd_bf16": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
+                                  _vp, _sz, _vp]),
+    "pg_cast_f32_bf16": (_i, [_vp, _vp, _i64, _vp, _vp]),
+    "pg_cast_bf16_f32": (_i, [_vp, _i64, _vp, _vp]),
     "pg_spmm_max_fwd_cpu": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i]),
     "pg_spmm_max_bwd_cpu": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64]),
     "pg_spmm_sum_cpu": (_i, [_csr, _vp, _i64, _i64, _i, _vp, _vp, _i64]),

@@ -42,7 +42,8 @@ def _check_device(dg: DeviceGraph, *ts):
     for t in ts:
         if t is not None and t.device != dg.device:
             raise ValueError(f"tensor on {t.device}, graph on {dg.device}")
-        if t is not None and t.dtype not in (torch.float32, torch.int16, torch.int32, torch.int64):
+        if t is not None and t.dtype not in (torch.float32, torch.bfloat16, torch.int16, torch.int32,
+                                             torch.int64):
             raise TypeError(f"unsupported dtype {t.dtype}")
 
 
@@ -52,21 +53,24 @@ def spmm_max(dg: DeviceGraph, X: torch.Tensor, ew_slots: Optional[torch.Tensor] 
              ) -> Tuple[torch.Tensor, torch.Tensor]:
     """out[v] = max over in-edges of X[u] (* w), argpos = winning in-row position.
     DGL update_all(copy_u|u_mul_e, max) (code/model.py:20,22,24)."""
-    if X.dtype != torch.float32:
-        raise TypeError("spmm_max: float32 features expected")
+    if X.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError("spmm_max: float32 or bfloat16 features expected")
+    bf = X.dtype == torch.bfloat16
     _check_device(dg, X, ew_slots)
     n, F = dg.num_nodes, X.shape[1]
     if X.shape[0] != n:
         raise ValueError(f"spmm_max: X has {X.shape[0]} rows, graph has {n} nodes")
     if out is None:
-        out = torch.empty(n, F, dtype=torch.float32, device=X.device)
+        out = torch.empty(n, F, dtype=X.dtype, device=X.device)
     if argpos is None:
         argpos = torch.empty(n, F, dtype=dg.arg_dtype, device=X.device)
     g = dg.fwd.struct(ew_slots)
+    if bf and not dg.is_cuda:
+        raise TypeError("spmm_max: bfloat16 storage runs on the GPU only")
     if dg.is_cuda:
         ws_n = _lib.lib().pg_spmm_max_fwd_workspace(g, F, dg.arg_kind)
         ws = _workspace(ws_n, X.device)
-        call("pg_spmm_max_fwd", g, ptr(X), _ld(X), F, ptr(out), _ld(out), ptr(argpos), _ld(argpos),
+        call("pg_spmm_max_fwd_bf16" if bf else "pg_spmm_max_fwd", g, ptr(X), _ld(X), F, ptr(out), _ld(out), ptr(argpos), _ld(argpos),
              dg.arg_kind, ptr(ws), ws_n, _stream(X))
     else:
         call("pg_spmm_max_fwd_cpu", g, ptr(X), _ld(X), F, ptr(out), _ld(out), ptr(argpos),
@@ -81,16 +85,19 @@ def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
     gathered per source in ascending destination order; optional fused relu' mask
     (mask[u,f] > 0)."""
     _check_device(dg, argpos, dout, ew_slots, mask)
+    bf = dout.dtype == torch.bfloat16
+    if bf and ((mask is not None and mask.dtype != torch.bfloat16) or not dg.is_cuda):
+        raise TypeError("spmm_max_backward: bfloat16 storage (GPU) needs a bfloat16 mask")
     n, F = dg.num_nodes, dout.shape[1]
     if dx is None:
-        dx = torch.empty(n, F, dtype=torch.float32, device=dout.device)
+        dx = torch.empty(n, F, dtype=dout.dtype, device=dout.device)
     g = dg.fwd.struct(ew_slots)
     gt = dg.bwd.struct(None)
     ldm = _ld(mask) if mask is not None else 0
     if dg.is_cuda:
         ws_n = _lib.lib().pg_spmm_max_bwd_workspace(gt, F)
         ws = _workspace(ws_n, dout.device)
-        call("pg_spmm_max_bwd", g, gt, ptr(argpos), _ld(argpos), dg.arg_kind, ptr(dout), _ld(dout),
+        call("pg_spmm_max_bwd_bf16" if bf else "pg_spmm_max_bwd", g, gt, ptr(argpos), _ld(argpos), dg.arg_kind, ptr(dout), _ld(dout),
              F, ptr(mask), ldm, ptr(dx), _ld(dx), ptr(ws), ws_n, _stream(dout))
     else:
         call("pg_spmm_max_bwd_cpu", g, gt, ptr(argpos), _ld(argpos), dg.arg_kind, ptr(dout),
@@ -199,6 +206,58 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
     ep = _lib.epilogue(bias, act, slope, dact, rowsum)
     call("pg_gemm_f32", int(transa), int(transb), M, N, K, alpha, ptr(A), _ld(A), ptr(B), _ld(B),
          beta, ptr(out), _ld(out), ep, split_k, ptr(ws), ws_n, _stream(A))
+    return out
+
+
+def gemm_bf16(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = False,
+              out: Optional[torch.Tensor] = None, out_dtype=torch.float32, alpha: float = 1.0,
+              beta: float = 0.0, bias: Optional[torch.Tensor] = None, act: int = _lib.PG_ACT_NONE,
+              slope: float = LEAKY_SLOPE, split_k: Optional[int] = None,
+              dact: Optional[torch.Tensor] = None, rowsum: Optional[torch.Tensor] = None
+              ) -> torch.Tensor:
+    """pg_gemm_bf16: bfloat16 operands, f32 accumulate on v_mfma_f32_32x32x16_bf16, output
+    float32 or bfloat16 (`out` / `out_dtype`), the same epilogues as gemm() (bias f32, dact
+    bfloat16, rowsum f32)."""
+    if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16 or A.device.type != "cuda":
+        raise TypeError("gemm_bf16: bfloat16 operands on a HIP device expected")
+    M = A.shape[1] if transa else A.shape[0]
+    K = A.shape[0] if transa else A.shape[1]
+    Kb = B.shape[1] if transb else B.shape[0]
+    N = B.shape[0] if transb else B.shape[1]
+    if K != Kb:
+        raise ValueError(f"gemm_bf16: inner dims {K} vs {Kb}")
+    if out is None:
+        if beta != 0.0:
+            raise ValueError("gemm_bf16: beta != 0 needs out")
+        out = torch.empty(M, N, dtype=out_dtype, device=A.device)
+    if out.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError("gemm_bf16: float32 or bfloat16 output")
+    if dact is not None and dact.dtype != torch.bfloat16:
+        raise TypeError("gemm_bf16: dact must be bfloat16")
+    obf = out.dtype == torch.bfloat16
+    if split_k is None:
+        split_k = 1 if (obf or bias is not None or act != _lib.PG_ACT_NONE or dact is not None
+                        or beta not in (0.0, 1.0)) else int(_lib.lib().pg_gemm_bf16_split_k(M, N, K))
+    ws_n = _lib.lib().pg_gemm_bf16_workspace(M, N, K, split_k)
+    ws = _workspace(ws_n, A.device)
+    ep = _lib.epilogue(bias, act, slope, dact, rowsum)
+    call("pg_gemm_bf16", int(transa), int(transb), M, N, K, alpha, ptr(A), _ld(A), ptr(B), _ld(B),
+         beta, ptr(out), _ld(out), _lib.PG_DTYPE_BF16 if obf else _lib.PG_DTYPE_F32, ep, split_k,
+         ptr(ws), ws_n, _stream(A))
+    return out
+
+
+def cast_bf16(src: torch.Tensor, index: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16(src[index]) (round to nearest even; index < 0 gives 0) with pg_cast_f32_bf16."""
+    if src.dtype != torch.float32 or not src.is_contiguous():
+        raise TypeError("cast_bf16: contiguous float32 source expected")
+    n = index.numel() if index is not None else src.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.bfloat16, device=src.device)
+    if index is not None and index.dtype != torch.int32:
+        raise TypeError("cast_bf16: int32 index expected")
+    call("pg_cast_f32_bf16", ptr(src), ptr(index), n, ptr(out), _stream(src))
     return out
 
 

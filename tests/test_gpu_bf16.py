@@ -1,0 +1,144 @@
+"""bf16-storage mode (BASELINE configs[4]: bf16 storage, f32 accumulate) — not run by the
+reference (fp32 only), so reference-unpinned; pinned here against the fp32 path:
+
+* pg_gemm_bf16 vs a float64 product of the same bf16 operands: f32 outputs within the
+  f32-accumulation bound 2e-6 sqrt(K) (|A| |B|); bf16 outputs within one bf16 rounding
+  of that. Every transposition (row images and ds_read_b64_tr_b16 k images), ragged
+  M / N / K tails, every epilogue, split-K.
+* pg_spmm_max_fwd_bf16 / pg_spmm_max_bwd_bf16 vs the fp32 kernels (bit-exact vs the
+  oracle) on the bf16 values widened to f32: bit-identical after rounding the fp32
+  result to bf16 (the max is a selection; the backward sums in the same f32 order).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import hub_graph
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(DEV)
+
+
+def _ref(A, B, ta, tb):
+    a = A.double().t() if ta else A.double()
+    b = B.double().t() if tb else B.double()
+    return a @ b, a.abs() @ b.abs()
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(1000, 256, 512), (4104, 520, 264), (200, 72, 1000), (64, 8, 8)])
+def test_gemm_bf16_f32_out(ta, tb, M, N, K):
+    from plagnn import ops
+
+    A = _bf((K, M) if ta else (M, K), M + K)
+    B = _bf((N, K) if tb else (K, N), N + 3 * K)
+    got = ops.gemm_bf16(A, B, ta, tb, split_k=1).double()
+    ref, mag = _ref(A, B, ta, tb)
+    bound = 2e-6 * np.sqrt(K) * mag + 1e-30
+    assert bool(((got - ref).abs() <= bound).all()), float(((got - ref).abs() / bound).max())
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (False, False)])
+def test_gemm_bf16_bf16_out_epilogues(ta, tb):
+    from plagnn import _lib, ops
+
+    M, N, K = 3000, 264, 520
+    A = _bf((K, M) if ta else (M, K), 5)
+    B = _bf((N, K) if tb else (K, N), 6)
+    bias = torch.randn(N, device=DEV)
+    ref, mag = _ref(A, B, ta, tb)
+    tol = 2e-6 * np.sqrt(K) * mag
+    # bias + leaky_relu, bf16 out
+    got = ops.gemm_bf16(A, B, ta, tb, out_dtype=torch.bfloat16, bias=bias, act=_lib.PG_ACT_LEAKY).double()
+    r = ref + bias.double()
+    r = torch.where(r > 0, r, r * 0.01)
+    assert bool(((got - r).abs() <= r.abs() * 2.0 ** -8 + tol).all())
+    # relu
+    got = ops.gemm_bf16(A, B, ta, tb, out_dtype=torch.bfloat16, bias=bias, act=_lib.PG_ACT_RELU).double()
+    r = (ref + bias.double()).clamp_min(0)
+    assert bool(((got - r).abs() <= r.abs() * 2.0 ** -8 + tol).all())
+    # fused leaky' with a bf16 activation output, f32 out
+    y = _bf((M, N), 7)
+    got = ops.gemm_bf16(A, B, ta, tb, act=_lib.PG_ACT_LEAKY, dact=y).double()
+    r = torch.where(y.double() > 0, ref, ref * 0.01)
+    assert bool(((got - r).abs() <= tol + 1e-30).all())
+    # beta = 1 into a bf16 C
+    c0 = _bf((M, N), 8)
+    c = c0.clone()
+    ops.gemm_bf16(A, B, ta, tb, out=c, beta=1.0)
+    r = ref + c0.double()
+    assert bool(((c.double() - r).abs() <= r.abs() * 2.0 ** -8 + tol).all())
+
+
+def test_gemm_bf16_rowsum_and_split_k():
+    """Weight-gradient shape: dW = dY^T X with K = nodes, both operands k images,
+    bias gradient as the row sums of dY^T, split-K with an ordered combine."""
+    from plagnn import ops
+
+    Nn, Fo, Fi = 24000, 264, 512
+    dY = _bf((Nn, Fo), 11)
+    X = _bf((Nn, Fi), 12)
+    ref, mag = _ref(dY, X, True, False)
+    for sk in (1, 7, None):
+        rs = torch.empty(Fo, device=DEV)
+        got = ops.gemm_bf16(dY, X, True, False, rowsum=rs, split_k=sk).double()
+        assert bool(((got - ref).abs() <= 2e-6 * np.sqrt(Nn) * mag).all()), sk
+        rref = dY.double().sum(0)
+        assert bool(((rs.double() - rref).abs() <= 2e-6 * np.sqrt(Nn) * dY.double().abs().sum(0)).all()), sk
+    a = ops.gemm_bf16(dY, X, True, False, split_k=9)
+    b = ops.gemm_bf16(dY, X, True, False, split_k=9)
+    assert torch.equal(a, b)  # deterministic
+
+
+def test_gemm_bf16_rejects_unaligned_extents():
+    from plagnn import _lib, ops
+
+    A = _bf((64, 20), 1)  # K = 20 not a multiple of 8
+    B = _bf((20, 64), 2)
+    with pytest.raises(_lib.PlagnnError):
+        ops.gemm_bf16(A, B)
+
+
+@pytest.mark.parametrize("F,weighted", [(64, False), (256, False), (512, True), (1000, False)])
+def test_spmm_max_bf16_matches_fp32_kernels(F, weighted):
+    import plagnn
+    from plagnn import ops
+
+    n = 700
+    src, dst = hub_graph(n, 2000, seed=F)
+    g = plagnn.CSRGraph(src, dst, n)
+    dg = g.on(DEV)
+    gen = torch.Generator().manual_seed(F)
+    X = torch.randn(n, F, generator=gen)
+    X[torch.rand(n, F, generator=gen) < 0.4] = 0.0
+    Xb = X.to(torch.bfloat16).to(DEV)
+    ew = None
+    if weighted:
+        ew = dg.edge_weight_slots(torch.rand(g.num_edges, generator=gen) + 0.5)
+    out_b, arg_b = ops.spmm_max(dg, Xb, ew)
+    out_f, arg_f = ops.spmm_max(dg, Xb.float(), ew)
+    assert torch.equal(arg_b, arg_f)
+    assert torch.equal(out_b, out_f.to(torch.bfloat16))
+    # backward: relu' mask from a bf16 "P", bf16 upstream gradient
+    dout = torch.randn(n, F, generator=gen).to(torch.bfloat16).to(DEV)
+    mask = Xb
+    dx_b = ops.spmm_max_backward(dg, arg_b, dout, ew, mask=mask)
+    dx_f = ops.spmm_max_backward(dg, arg_f, dout.float(), ew, mask=mask.float())
+    assert dx_b.dtype == torch.bfloat16
+    assert torch.equal(dx_b, dx_f.to(torch.bfloat16))
+
+
+def test_cast_bf16_gather():
+    from plagnn import ops
+
+    src = torch.randn(1000, device=DEV)
+    idx = torch.tensor([5, -1, 999, 0, 5], dtype=torch.int32, device=DEV)
+    got = ops.cast_bf16(src, idx)
+    ref = torch.stack([src[5], src.new_zeros(()), src[999], src[0], src[5]]).to(torch.bfloat16)
+    assert torch.equal(got, ref)
+    assert torch.equal(ops.cast_bf16(src), src.to(torch.bfloat16))
