@@ -39,15 +39,21 @@ CONFIGS = {
     "cfg3": ("s0", [503, 512, 512, 512, 100, 12],
              "S0 perturbed (+-3% edges), ECC edge weights (pg_ecc, u_mul_e max), hidden 512, fp32"),
     "cfg5": ("rmat", [503, 512, 512, 512, 100, 12],
-             "RMAT x16 PPI (N=384656, a,b,c,d=.57,.19,.19,.05, mean deg 50), hidden 512, fp32"),
+             "RMAT x16 PPI (N=384656, a,b,c,d=.57,.19,.19,.05, mean deg 50), hidden 512, bf16 storage, f32 accumulate"),
+    "cfg5-f32": ("rmat", [503, 512, 512, 512, 100, 12],
+                 "RMAT x16 PPI (N=384656, a,b,c,d=.57,.19,.19,.05, mean deg 50), hidden 512, fp32"),
 }
+BF16_CONFIGS = {"cfg5"}  # BASELINE configs[4]: "hidden=512 bf16"
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_F32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
+# MI355X_MICROARCH.md: bf16 MFMA ~2.5 PF dense = 256 CUs x 4 SIMDs x (2*32*32*16 flops per
+# 32-cycle v_mfma_f32_32x32x16_bf16) x 2.4 GHz
+PEAK_BF16_TFLOPS = 2516.6
 
 
-def _group(name: str) -> str:
+def _group(name: str, gemm_group: str = "gemm_f32") -> str:
     if name.startswith("gemm"):
-        return "gemm_f32"
+        return gemm_group
     return name.split(".")[0]
 
 
@@ -157,7 +163,10 @@ def main():
     if args.config == "cfg3":
         src, dst, ew = _cfg3_graph(ds, 70 + rank)
         graph = plagnn.CSRGraph(src, dst, ds.n)
-    engine = plagnn.TrainEngine(graph, torch.from_numpy(ds.feat), torch.from_numpy(ds.loc.astype(np.float32)),
+    bf16 = args.config in BF16_CONFIGS
+    Engine = plagnn.TrainEngineBF16 if bf16 else plagnn.TrainEngine
+    gemm_group = "gemm_bf16" if bf16 else "gemm_f32"
+    engine = Engine(graph, torch.from_numpy(ds.feat), torch.from_numpy(ds.loc.astype(np.float32)),
                                 dims, w, train_idx, val_idx, lr=5e-5, device=dev, edge_weight=ew,
                                 seed=rank)
     allreduce = None
@@ -203,7 +212,7 @@ def main():
             json.dump(bd, f, indent=1)
     groups = {}
     for name, r in bd.items():
-        gname = _group(name)
+        gname = _group(name, gemm_group)
         g = groups.setdefault(gname, {"ms": 0.0, "work": 0.0, "launches": 0.0})
         g["ms"] += r["ms"]
         g["work"] += r["work"]
@@ -213,11 +222,12 @@ def main():
     def roof(gname):
         g = groups[gname]
         sec = g["ms"] / 1e3
-        if gname == "gemm_f32":
+        if gname == gemm_group:
             # algorithmic flops at the true (unpadded) dims, not the padded launch shapes
             ach = engine.flops_per_step() / sec / 1e12
-            return {"kernel": gname, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F32_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_TFLOPS, 4),
+            peak = PEAK_BF16_TFLOPS if bf16 else PEAK_F32_TFLOPS
+            return {"kernel": gname, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                     "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
         ach = g["work"] / sec / 1e9
         return {"kernel": gname, "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
@@ -248,7 +258,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "bf16" if bf16 else "f32",
         "data": "synthetic (seeded power-law PPI stand-in; real PPI/GEO/UniProt inputs are not shipped)",
         "config": {"workload": f"{args.config}: {desc}", "nodes": ds.n, "edges_with_self_loops": graph.num_edges,
                    "sage_layers": len(dims) - 3, "dims": dims, "edges_per_step": engine.edges_per_step,

@@ -4,6 +4,7 @@
   ops          C-ABI calls (SpMM max/sum, GEMM, ...) and autograd wrappers (ops.py)
   GNN32, GNN   the reference's model on the engine's SAGEConv (model.py)
   TrainEngine  the whole training step, explicit and HIP-graph captured (engine.py)
+  TrainEngineBF16  the same step in bf16 storage, f32 accumulate (engine_bf16.py)
   data         synthetic PPI stand-ins in the reference's on-disk formats (data.py)
 """
 from ._lib import PlagnnError, lib  # noqa: F401
@@ -21,4 +22,8 @@ def __getattr__(name):
         from .engine import TrainEngine
 
         return TrainEngine
+    if name == "TrainEngineBF16":
+        from .engine_bf16 import TrainEngineBF16
+
+        return TrainEngineBF16
     raise AttributeError(name)

@@ -60,6 +60,8 @@ class _Flat:
 
 
 class TrainEngine:
+    WIDTH_ALIGN = 4  # every padded width is a multiple of this
+
     def __init__(self, graph: CSRGraph, features: torch.Tensor, labels: torch.Tensor,
                  dims: Sequence[int], class_weight, train_index, val_index=None,
                  lr: float = 5e-5, betas=(0.9, 0.999), eps: float = 1e-8,
@@ -80,7 +82,8 @@ class TrainEngine:
         C = self.dims[-1]
         self.C = C
         dev = self.device
-        pd = [round4(d) for d in self.dims]
+        a = self.WIDTH_ALIGN
+        pd = [(d + a - 1) // a * a for d in self.dims]
         # SAGE layer inputs: a multiple of 64 when that costs <= 2 % more columns (503 -> 512):
         # whole feature tiles for the SpMM kernels; pads are zero and stay zero
         for l in range(self.L):
@@ -131,7 +134,16 @@ class TrainEngine:
         self.train_index = torch.as_tensor(np.asarray(train_index, np.int32), device=dev)
         self.val_index = None if val_index is None else torch.as_tensor(
             np.asarray(val_index, np.int32), device=dev)
+        self._alloc_buffers(features)
+        self._alloc_workspace()
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.graph_adam: Optional[torch.cuda.CUDAGraph] = None
+        self.allreduce = None
+        self.steps_done = 0
+        self._timing: Optional[list] = None  # [(name, work, start_event, end_event)]
 
+    def _alloc_buffers(self, features: torch.Tensor) -> None:
+        N, pd, dev = self.N, self.pd, self.device
         # ---- activations ----
         f32 = dict(dtype=torch.float32, device=dev)
         self.HM, self.Pl, self.arg = [], [], []
@@ -153,7 +165,9 @@ class TrainEngine:
         self.dHM = [torch.zeros(N, 2 * pd[l], **f32) for l in range(self.L)]
         self.dP = [torch.zeros(N, pd[l], **f32) for l in range(self.L)]
 
+    def _alloc_workspace(self) -> None:
         # ---- workspace (one buffer, sized for the largest call) ----
+        N, pd, C, dev = self.N, self.pd, self.C, self.device
         L = _lib.lib()
         need = 0
         for l in range(self.L):
@@ -178,11 +192,6 @@ class TrainEngine:
         for (M_, N_, K_), sk in self._gemm_plans.items():
             need2 = max(need2, L.pg_gemm_f32_workspace(M_, N_, K_, sk))
         self.ws2 = torch.zeros(int(need2), dtype=torch.uint8, device=dev) if self.overlap else self.ws
-        self.graph: Optional[torch.cuda.CUDAGraph] = None
-        self.graph_adam: Optional[torch.cuda.CUDAGraph] = None
-        self.allreduce = None
-        self.steps_done = 0
-        self._timing: Optional[list] = None  # [(name, work, start_event, end_event)]
 
     # ------------------------------------------------------------------ parameters
     def _wgrad_shapes(self):
