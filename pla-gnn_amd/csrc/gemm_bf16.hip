@@ -47,7 +47,6 @@ namespace {
 using namespace pg_gemm;
 
 constexpr int BK = 64;  // bf16 k-values per K step
-constexpr int kThreads = 256;
 
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
@@ -67,12 +66,13 @@ __device__ __forceinline__ int img_off(int row, int k) {
 
 // DMA of one ROWS x BK tile (rows [r0, r0 + ROWS) x k [k0, k0 + BK)) into an image;
 // units past K (kvalid) are zero-filled by the lane that owns them.
-template <int ROWS, bool KMAJ, bool FULL>
+template <int ROWS, bool KMAJ, bool FULL, int NW>
 __device__ __forceinline__ void dma_tile(const uint16_t* __restrict__ P, int64_t ld, int r0, int R,
                                          int k0, int kvalid, uint16_t* S, int wave, int lane) {
+  static_assert((ROWS / 8) % NW == 0, "image pieces per wave");
 #pragma unroll
-  for (int j = 0; j < ROWS / 32; ++j) {
-    const int piece = j * 4 + wave;   // 1-KiB piece of the image
+  for (int j = 0; j < ROWS / 8 / NW; ++j) {
+    const int piece = j * NW + wave;  // 1-KiB piece of the image
     const int u = piece * 64 + lane;  // 16-B unit
     const uint16_t* src;
     bool valid;
@@ -121,9 +121,9 @@ __device__ __forceinline__ uint16_t f2bf(float x) {
 }
 
 // row sums of the A tile in LDS over its BK k-values (thread t: row t % BM, k-group t / BM)
-template <int BM, bool AK>
+template <int BM, bool AK, int NT>
 __device__ __forceinline__ float img_rowsum(const uint16_t* __restrict__ As, int tid) {
-  constexpr int G = kThreads / BM;
+  constexpr int G = NT / BM;
   const int m = tid % BM, g = tid / BM;
   float s = 0.f;
 #pragma unroll
@@ -131,111 +131,125 @@ __device__ __forceinline__ float img_rowsum(const uint16_t* __restrict__ As, int
   return s;
 }
 
-// epilogue through LDS: the accumulator tile is transposed into a [BM][BN] f32 image and
-// written row-major, 4 consecutive outputs per thread (16-B f32 / 8-B bf16 stores)
-template <int BM, int BN, int EPI, bool OBF>
-__device__ __forceinline__ void finish_tile(const f32x16 (&acc)[BM / 64][BN / 64], float rs, bool do_rs,
-                                            float* __restrict__ lds, int tid, int m0, int n0, int M, int N,
-                                            float alpha, float beta, void* __restrict__ Cv, int64_t ldc,
-                                            const float* __restrict__ bias, float slope,
+// epilogue through LDS: the accumulator tile is transposed into a row-major f32 image and
+// written out 4 consecutive outputs per thread (16-B f32 / 8-B bf16 stores). A tile whose
+// f32 image does not fit the staging array (256 x 256) goes in PASSES row bands: in pass
+// p the waves of wave row p stage their rows.
+template <int BM, int BN, int WM, int WN, int EPI, bool OBF, int PASSES>
+__device__ __forceinline__ void finish_tile(const f32x16 (&acc)[BM / WM / 32][BN / WN / 32], float rs,
+                                            bool do_rs, float* __restrict__ lds, int tid, int m0, int n0,
+                                            int M, int N, float alpha, float beta, void* __restrict__ Cv,
+                                            int64_t ldc, const float* __restrict__ bias, float slope,
                                             const uint16_t* __restrict__ dact, int64_t lddact,
                                             float* __restrict__ rowsum, float* __restrict__ ws,
                                             float* __restrict__ ws_rowsum) {
   constexpr bool SPLIT = EPI == EPI_SPLIT;
-  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int NT = 64 * WM * WN;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int BAND = BM / PASSES;  // rows staged per pass
+  static_assert(PASSES == 1 || PASSES == WM, "one pass per wave row");
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+  const int wm = wave / WN, wn = wave % WN, h = lane >> 5, l32 = lane & 31;
   if (do_rs) {
     lds[tid] = rs;
     __syncthreads();
     if (tid < BM && m0 + tid < M) {
       float t = 0.f;
-      for (int g = 0; g < kThreads / BM; ++g) t += lds[g * BM + tid];
+      for (int g = 0; g < NT / BM; ++g) t += lds[g * BM + tid];
       if constexpr (SPLIT) ws_rowsum[(int64_t)blockIdx.z * M + m0 + tid] = t;
       else rowsum[m0 + tid] = t;
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int pass = 0; pass < PASSES; ++pass) {
+    if (PASSES == 1 || wm == pass) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        lds[row * BN + wn * (BN / 2) + j * 32 + l32] = acc[i][j][r];
-      }
-  __syncthreads();
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-  for (int it = 0; it < BM * BN / 4 / kThreads; ++it) {
-    const int u = it * kThreads + tid;
-    const int row = u / (BN / 4), c = (u % (BN / 4)) * 4;
-    const int gr = m0 + row, gc = n0 + c;
-    if (gr >= M || gc >= N) continue;
-    const float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
-    if constexpr (SPLIT) {
-      *reinterpret_cast<float4*>(ws + ((int64_t)blockIdx.z * M + gr) * N + gc) = v;
-    } else {
-      float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
-      if constexpr (OBF) {
-        uint16_t* cp = (uint16_t*)Cv + (int64_t)gr * ldc + gc;
-        if (beta != 0.f) {
-          const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
-          o[0] = o[0] + beta * bf2f(c2.x & 0xFFFF); o[1] = o[1] + beta * bf2f(c2.x >> 16);
-          o[2] = o[2] + beta * bf2f(c2.y & 0xFFFF); o[3] = o[3] + beta * bf2f(c2.y >> 16);
-        }
-        if (bias) {
-          const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
-          o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
-        }
-        float y[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
-          const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
-          y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
-        }
-        uint2 w;
-        w.x = (uint32_t)f2bf(epi_apply<EPI>(o[0], y[0], slope)) |
-              ((uint32_t)f2bf(epi_apply<EPI>(o[1], y[1], slope)) << 16);
-        w.y = (uint32_t)f2bf(epi_apply<EPI>(o[2], y[2], slope)) |
-              ((uint32_t)f2bf(epi_apply<EPI>(o[3], y[3], slope)) << 16);
-        *reinterpret_cast<uint2*>(cp) = w;
+          for (int r = 0; r < 16; ++r) {
+            const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h - pass * BAND;
+            lds[row * BN + wn * (BN / WN) + j * 32 + l32] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < BAND * BN / 4 / NT; ++it) {
+      const int u = it * NT + tid;
+      const int row = u / (BN / 4), c = (u % (BN / 4)) * 4;
+      const int gr = m0 + pass * BAND + row, gc = n0 + c;
+      if (gr >= M || gc >= N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
+      if constexpr (SPLIT) {
+        *reinterpret_cast<float4*>(ws + ((int64_t)blockIdx.z * M + gr) * N + gc) = v;
       } else {
-        float* cp = (float*)Cv + (int64_t)gr * ldc + gc;
-        if (beta != 0.f) {
-          const float4 c4 = *reinterpret_cast<const float4*>(cp);
-          o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
-          o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
+        float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
+        if constexpr (OBF) {
+          uint16_t* cp = (uint16_t*)Cv + (int64_t)gr * ldc + gc;
+          if (beta != 0.f) {
+            const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
+            o[0] = o[0] + beta * bf2f(c2.x & 0xFFFF); o[1] = o[1] + beta * bf2f(c2.x >> 16);
+            o[2] = o[2] + beta * bf2f(c2.y & 0xFFFF); o[3] = o[3] + beta * bf2f(c2.y >> 16);
+          }
+          if (bias) {
+            const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
+            o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
+          }
+          float y[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
+            const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
+            y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
+          }
+          uint2 w;
+          w.x = (uint32_t)f2bf(epi_apply<EPI>(o[0], y[0], slope)) |
+                ((uint32_t)f2bf(epi_apply<EPI>(o[1], y[1], slope)) << 16);
+          w.y = (uint32_t)f2bf(epi_apply<EPI>(o[2], y[2], slope)) |
+                ((uint32_t)f2bf(epi_apply<EPI>(o[3], y[3], slope)) << 16);
+          *reinterpret_cast<uint2*>(cp) = w;
+        } else {
+          float* cp = (float*)Cv + (int64_t)gr * ldc + gc;
+          if (beta != 0.f) {
+            const float4 c4 = *reinterpret_cast<const float4*>(cp);
+            o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
+            o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
+          }
+          if (bias) {
+            const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
+            o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
+          }
+          float y[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
+            const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
+            y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
+          }
+          *reinterpret_cast<float4*>(cp) =
+              make_float4(epi_apply<EPI>(o[0], y[0], slope), epi_apply<EPI>(o[1], y[1], slope),
+                          epi_apply<EPI>(o[2], y[2], slope), epi_apply<EPI>(o[3], y[3], slope));
         }
-        if (bias) {
-          const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
-          o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
-        }
-        float y[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
-          const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
-          y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
-        }
-        *reinterpret_cast<float4*>(cp) =
-            make_float4(epi_apply<EPI>(o[0], y[0], slope), epi_apply<EPI>(o[1], y[1], slope),
-                        epi_apply<EPI>(o[2], y[2], slope), epi_apply<EPI>(o[3], y[3], slope));
       }
     }
+    if (PASSES > 1) __syncthreads();
   }
 }
 
-template <int BM, int BN, bool TA, bool TB, int EPI, bool OBF>
-__global__ __launch_bounds__(kThreads) void gemm_bf16_kernel(
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool OBF>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
     int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
     float beta, void* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
     const uint16_t* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
     float* __restrict__ ws, float* __restrict__ ws_rowsum) {
   constexpr bool AK = TA, BKM = !TB;  // k images for A stored [k][m] / B stored [k][n]
-  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;  // 32 x 32 MFMA tiles per wave
   constexpr int IA = BM * BK, IB = BN * BK;  // image sizes (u16)
-  // one LDS array [A0 | A1 | B0 | B1]; the epilogue reuses it as a [BM][BN] f32 image
+  // one LDS array [A0 | A1 | B0 | B1]; the epilogue reuses it as a row-major f32 image of
+  // the tile (in WM row bands when the whole tile does not fit)
   constexpr int STAGE = 2 * (IA + IB);
-  constexpr int EPI_U16 = 2 * BM * BN;
+  constexpr int PASSES = 2 * BM * BN > STAGE ? WM : 1;
+  constexpr int EPI_U16 = 2 * BM * BN / PASSES;
   __shared__ __attribute__((aligned(16))) uint16_t lds[STAGE > EPI_U16 ? STAGE : EPI_U16];
 
   // XCD-aware tile order (as gemm.hip): blocks b, b + 8, ... share an XCD and get a
@@ -245,7 +259,7 @@ __global__ __launch_bounds__(kThreads) void gemm_bf16_kernel(
   const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, l32 = lane & 31;
+  const int wm = wave / WN, wn = wave % WN, l32 = lane & 31;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kz0 = blockIdx.z * k_per_split;
   const int kz1 = min(K, kz0 + k_per_split);
@@ -263,18 +277,18 @@ __global__ __launch_bounds__(kThreads) void gemm_bf16_kernel(
   auto issue = [&](int t, int buf) {
     const int k0 = kz0 + t * BK;
     if (kz1 - k0 >= BK) {
-      dma_tile<BM, AK, true>(A, lda, m0, M, k0, BK, lds + buf * IA, wave, lane);
-      dma_tile<BN, BKM, true>(B, ldb, n0, N, k0, BK, lds + 2 * IA + buf * IB, wave, lane);
+      dma_tile<BM, AK, true, NW>(A, lda, m0, M, k0, BK, lds + buf * IA, wave, lane);
+      dma_tile<BN, BKM, true, NW>(B, ldb, n0, N, k0, BK, lds + 2 * IA + buf * IB, wave, lane);
     } else {
-      dma_tile<BM, AK, false>(A, lda, m0, M, k0, kz1 - k0, lds + buf * IA, wave, lane);
-      dma_tile<BN, BKM, false>(B, ldb, n0, N, k0, kz1 - k0, lds + 2 * IA + buf * IB, wave, lane);
+      dma_tile<BM, AK, false, NW>(A, lda, m0, M, k0, kz1 - k0, lds + buf * IA, wave, lane);
+      dma_tile<BN, BKM, false, NW>(B, ldb, n0, N, k0, kz1 - k0, lds + 2 * IA + buf * IB, wave, lane);
     }
   };
 
   if (nk > 0) {
     issue(0, 0);
     __syncthreads();
-    const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
+    const int ra = wm * (BM / WM) + l32, rb = wn * (BN / WN) + l32;
     bf16x8 fa[2][TM], fb[2][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) fa[0][i] = frag<BM, AK>(lds, ra + i * 32, 0, lane);
@@ -286,7 +300,7 @@ __global__ __launch_bounds__(kThreads) void gemm_bf16_kernel(
       if (more) issue(t + 1, cur ^ 1);
       const uint16_t* As = lds + cur * IA;
       const uint16_t* Bs = lds + 2 * IA + cur * IB;
-      if (do_rs) rs += img_rowsum<BM, AK>(As, tid);
+      if (do_rs) rs += img_rowsum<BM, AK, NT>(As, tid);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int u = s & 1;
@@ -315,7 +329,7 @@ __global__ __launch_bounds__(kThreads) void gemm_bf16_kernel(
     }
     __syncthreads();  // the epilogue reuses the staging array
   }
-  finish_tile<BM, BN, EPI, OBF>(acc, rs, do_rs, reinterpret_cast<float*>(lds), tid, m0, n0, M, N, alpha,
+  finish_tile<BM, BN, WM, WN, EPI, OBF, PASSES>(acc, rs, do_rs, reinterpret_cast<float*>(lds), tid, m0, n0, M, N, alpha,
                                 beta, C, ldc, bias, slope, dact, lddact, rowsum, ws, ws_rowsum);
 }
 
@@ -338,10 +352,10 @@ struct Args {
   float* ws_rowsum;
 };
 
-template <int BM, int BN, bool TA, bool TB, bool OBF>
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool OBF>
 int launch_epi(int epi, dim3 grid, hipStream_t st, const Args& a) {
-#define PG_L(EPI_)                                                                              \
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, EPI_, OBF>), grid, dim3(kThreads), 0, st, \
+#define PG_L(EPI_)                                                                                    \
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, TA, TB, EPI_, OBF>), grid, dim3(64 * WM * WN), 0, st, \
                      a.M, a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb,   \
                      a.beta, a.C, a.ldc, a.bias, a.slope, a.dact, a.lddact, a.rowsum, a.ws,      \
                      a.ws_rowsum)
@@ -363,11 +377,11 @@ int launch_epi(int epi, dim3 grid, hipStream_t st, const Args& a) {
   return PG_OK;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WM, int WN>
 int launch_tile(bool ta, bool tb, bool obf, int epi, dim3 grid, hipStream_t st, const Args& a) {
-#define PG_T(TA_, TB_)                                              \
-  return obf ? launch_epi<BM, BN, TA_, TB_, true>(epi, grid, st, a) \
-             : launch_epi<BM, BN, TA_, TB_, false>(epi, grid, st, a)
+#define PG_T(TA_, TB_)                                                      \
+  return obf ? launch_epi<BM, BN, WM, WN, TA_, TB_, true>(epi, grid, st, a) \
+             : launch_epi<BM, BN, WM, WN, TA_, TB_, false>(epi, grid, st, a)
   if (!ta && !tb) PG_T(false, false);
   if (!ta && tb) PG_T(false, true);
   if (ta && !tb) PG_T(true, false);
@@ -375,15 +389,20 @@ int launch_tile(bool ta, bool tb, bool obf, int epi, dim3 grid, hipStream_t st, 
 #undef PG_T
 }
 
-// Tile choice: 128 x 128 while that still gives >= 2 workgroups per CU (LDS holds two
-// 64-KiB workgroups), else 128 x 64, else 64 x 64. Split products run 64 x 64.
-inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
+// Tile choice. The bf16 MFMA rate (4096 flop/clk/CU) needs ~64 flop per byte staged
+// from L2 (BM BN / (BM + BN) per workgroup): 256 x 256 tiles (4 waves of 128 x 128, the
+// 256 accumulators in AGPRs at one wave per SIMD; one 128-KiB workgroup per CU) wherever they still give >= 1 workgroup per CU, 128 x 128
+// (two per CU) next, 128 x 64 / 64 x 64 for narrow or small products. Split products
+// (weight gradients) use 256 x 256 when both sides allow it, else 64 x 64.
+inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& bn) {
   static const int forced = [] {  // tuning knob PLAGNN_GEMM_BF16_TILE = "BMxBN"
     const char* e = getenv("PLAGNN_GEMM_BF16_TILE");
     if (!e) return 0;
     int a = 0, b = 0;
-    if (sscanf(e, "%dx%d", &a, &b) != 2 || (a != 64 && a != 128) || (b != 64 && b != 128)) return 0;
-    return a * 1000 + b;
+    if (sscanf(e, "%dx%d", &a, &b) != 2) return 0;
+    const int v = a * 1000 + b;
+    if (v != 64064 && v != 128064 && v != 64128 && v != 128128 && v != 256128 && v != 256256) return 0;
+    return v;
   }();
   if (forced) {
     bm = forced / 1000;
@@ -392,8 +411,14 @@ inline void pick_tile(int64_t M, int64_t N, int split, int& bm, int& bn) {
   }
   auto tiles = [&](int tm, int tn) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
   bm = bn = 64;
-  if (split > 1) return;
-  if (N > 64 && tiles(128, 128) >= 512) {
+  if (split > 1) {
+    if (M >= 256 && N >= 256) bm = bn = 256;
+    return;
+  }
+  // (a short K leaves a 256 x 256 workgroup, alone on its CU, mostly in its epilogue)
+  if (N >= 256 && K >= 384 && tiles(256, 256) >= 256) {
+    bm = bn = 256;
+  } else if (N > 64 && tiles(128, 128) >= 512) {
     bm = bn = 128;
   } else if (tiles(128, 64) >= 512) {
     bm = 128;
@@ -407,10 +432,13 @@ extern "C" {
 int pg_gemm_bf16_split_k(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K < 2048) return 1;
   int bm, bn;
-  pick_tile(M, N, 1, bm, bn);
-  if (((M + bm - 1) / bm) * ((N + bn - 1) / bn) >= 768) return 1;
-  const int64_t tiles = ((M + 63) / 64) * ((N + 63) / 64);
-  const int64_t target = (1280 + tiles - 1) / tiles;  // ~5 workgroups per CU
+  pick_tile(M, N, K, 1, bm, bn);
+  if (((M + bm - 1) / bm) * ((N + bn - 1) / bn) >= 256 * (bm == 256 ? 1 : 3)) return 1;
+  pick_tile(M, N, K, 2, bm, bn);
+  const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  // workgroups aimed at: one 256 x 256 per CU (LDS-bound), else ~5 64 x 64 per CU
+  const int64_t want = bm == 256 ? 256 : 1280;
+  const int64_t target = (want + tiles - 1) / tiles;
   const int64_t by_k = K / (3 * BK);
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, by_k), 256));
 }
@@ -465,7 +493,7 @@ int pg_gemm_bf16(int transa, int transb, int64_t M, int64_t N, int64_t K, float 
   }
   const bool split = split_k > 1;
   int bm, bn;
-  pick_tile(M, N, split_k, bm, bn);
+  pick_tile(M, N, K, split_k, bm, bn);
   // a k image needs >= 8 valid rows for its clamped 16-B chunks
   if ((transa && M < 8) || (!transb && N < 8))
     return pg::set_error(PG_ERR_UNSUPPORTED, "pg_gemm_bf16: row-contiguous operand narrower than 8");
@@ -483,10 +511,12 @@ int pg_gemm_bf16(int transa, int transb, int64_t M, int64_t N, int64_t K, float 
                         : ep->dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
                                    : (act == PG_ACT_RELU ? EPI_RELU : act == PG_ACT_LEAKY ? EPI_LEAKY : EPI_NONE);
   int rc;
-  if (bm == 128 && bn == 128) rc = launch_tile<128, 128>(ta, tb, obf, epi, grid, st, a);
-  else if (bm == 128) rc = launch_tile<128, 64>(ta, tb, obf, epi, grid, st, a);
-  else if (bn == 128) rc = launch_tile<64, 128>(ta, tb, obf, epi, grid, st, a);
-  else rc = launch_tile<64, 64>(ta, tb, obf, epi, grid, st, a);
+  if (bm == 256 && bn == 256) rc = launch_tile<256, 256, 2, 2>(ta, tb, obf, epi, grid, st, a);
+  else if (bm == 256) rc = launch_tile<256, 128, 2, 2>(ta, tb, obf, epi, grid, st, a);
+  else if (bm == 128 && bn == 128) rc = launch_tile<128, 128, 2, 2>(ta, tb, obf, epi, grid, st, a);
+  else if (bm == 128) rc = launch_tile<128, 64, 2, 2>(ta, tb, obf, epi, grid, st, a);
+  else if (bn == 128) rc = launch_tile<64, 128, 2, 2>(ta, tb, obf, epi, grid, st, a);
+  else rc = launch_tile<64, 64, 2, 2>(ta, tb, obf, epi, grid, st, a);
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_bf16: dispatch failed");
   if (split) {
     const int64_t n = M * N + (ep->rowsum ? M : 0);

@@ -1160,6 +1160,8 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     p += round_up(N * F * 2, 256);
     int2* glist = (int2*)p;
     p += round_up(g->nnz * 8, 256);
+    // the upstream gradient in list order, f32 even for bf16 storage: 2-B scattered
+    // placement stores measured 30 % slower for the whole backward (RMWs on partial lines)
     float* dpack = (float*)p;
     p += round_up(N * F * 4, 256);
     const int32_t* einv = g->einv;

@@ -31,7 +31,8 @@ def _ref(A, B, ta, tb):
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("M,N,K", [(1000, 256, 512), (4104, 520, 264), (200, 72, 1000), (64, 8, 8)])
+@pytest.mark.parametrize("M,N,K", [(1000, 256, 512), (4104, 520, 264), (200, 72, 1000), (64, 8, 8),
+                                   (65544, 520, 136)])  # the last one on 256 x 256 tiles
 def test_gemm_bf16_f32_out(ta, tb, M, N, K):
     from plagnn import ops
 
@@ -44,10 +45,11 @@ def test_gemm_bf16_f32_out(ta, tb, M, N, K):
 
 
 @pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (False, False)])
-def test_gemm_bf16_bf16_out_epilogues(ta, tb):
+@pytest.mark.parametrize("M", [3000, 70000])  # 128 x 128 and 256 x 256 tiles
+def test_gemm_bf16_bf16_out_epilogues(ta, tb, M):
     from plagnn import _lib, ops
 
-    M, N, K = 3000, 264, 520
+    N, K = 264, 520
     A = _bf((K, M) if ta else (M, K), 5)
     B = _bf((N, K) if tb else (K, N), 6)
     bias = torch.randn(N, device=DEV)
