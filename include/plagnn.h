@@ -25,6 +25,8 @@
  *                           per-row edge positions
  *   pg_sigmoid_multi_loss<- th.sigmoid (code/model.py:29) + multi_loss
  *                           (code/train.py:89-108) forward and backward
+ *   pg_mlp_head          <- liner2 + sigmoid + multi_loss (train and val) + their backward
+ *                           down to liner1's activation (code/model.py:28-29), fused
  *   pg_adam_*            <- torch.optim.Adam(model.parameters(), lr) .step()
  *                           (code/train.py:180, 205), torch 1.10 formula
  *   pg_bias_act[_bwd]    <- nn.Linear bias add + F.relu / F.leaky_relu(0.01)
@@ -201,6 +203,20 @@ int pg_col_sum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* o
  *   dz (if not NULL) = d loss / d z for rows in index, 0 elsewhere (all n_rows rows written).
  * class_w[2c] = (float)w_c and class_w[2c+1] = (float)(w_c + 1), both rounded from the
  * float64 weights of weight_cal (code/train.py:111-126). C <= 64. loss may be NULL. */
+/* The model head after liner1, fused (code/model.py:28-29, code/train.py:89-108, 199-207):
+ *   z = A4 W2^T + b2;  prob = sigmoid(z);  multi_loss over the rows with row_set 1 (train,
+ *   loss2[0], n = n_train) and row_set 2 (val, loss2[1], n = n_val);  dz = d loss2[0] / dz
+ *   (0 outside the train rows);  dA4 = (dz W2) * leaky'(A4) with negative slope `slope`.
+ * A4 [n][K] and dA4 [n][K] are f32 or bf16 (a_dtype); W2 [C][K], b2 [C] f32; K <= 128,
+ * C <= 16. Optional outputs (NULL = skip): prob, dz, dz_bf16 (a bf16 copy of dz, leading
+ * dimension lddz), dA4. Scratch: pg_mlp_head_workspace(n, C) bytes. */
+size_t pg_mlp_head_workspace(int64_t n, int32_t C);
+int pg_mlp_head(const void* A4, int64_t lda, int64_t n, int32_t K, int a_dtype, const float* W2,
+                int64_t ldw, const float* b2, int32_t C, const float* labels, int64_t ldl,
+                const float* class_w, const int8_t* row_set, int64_t n_train, int64_t n_val,
+                float* prob, int64_t ldp, float* dz, int64_t lddz, void* dz_bf16, void* dA4,
+                int64_t ldg, float slope, float* loss2, void* ws, size_t ws_bytes,
+                pg_stream_t stream);
 size_t pg_sigmoid_multi_loss_workspace(int64_t n_index, int32_t C);
 int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C,
                           const float* labels, int64_t ldl, const float* class_w,

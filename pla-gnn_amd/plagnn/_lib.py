@@ -92,6 +92,9 @@ SIGNATURES = {
     "pg_sigmoid_multi_loss_workspace": (_sz, [_i64, _i32]),
     "pg_sigmoid_multi_loss": (_i, [_vp, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _i64,
                                    _vp, _vp, _i64, _vp, _sz, _vp]),
+    "pg_mlp_head_workspace": (_sz, [_i64, _i32]),
+    "pg_mlp_head": (_i, [_vp, _i64, _i64, _i32, _i, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _i64,
+                         _vp, _i64, _vp, _i64, _vp, _vp, _i64, _f, _vp, _vp, _sz, _vp]),
     "pg_adam_prepare": (_i, [_vp, _d, _d, _d, _vp]),
     "pg_adam_apply": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _d, _d, _d, _d, _vp]),
     "pg_gemm_f32_split_k": (_i, [_i64, _i64, _i64]),

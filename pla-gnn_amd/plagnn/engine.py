@@ -134,6 +134,17 @@ class TrainEngine:
         self.train_index = torch.as_tensor(np.asarray(train_index, np.int32), device=dev)
         self.val_index = None if val_index is None else torch.as_tensor(
             np.asarray(val_index, np.int32), device=dev)
+        # per-row set for the fused head: 1 = train, 2 = val, 0 = neither
+        rs = np.zeros(N, np.int8)
+        rs[np.asarray(train_index, np.int64)] = 1
+        if val_index is not None:
+            vi = np.asarray(val_index, np.int64)
+            if np.any(rs[vi] == 1):
+                raise ValueError("train and val rows overlap")
+            rs[vi] = 2
+        self.row_set = torch.from_numpy(rs).to(dev)
+        self.n_train = len(np.asarray(train_index))
+        self.n_val = 0 if val_index is None else len(np.asarray(val_index))
         self._alloc_buffers(features)
         self._alloc_workspace()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -155,7 +166,6 @@ class TrainEngine:
         self.HM[0][:, :self.dims[0]] = features.to(dev, torch.float32)
         self.A3 = torch.zeros(N, pd[-3], **f32)
         self.A4 = torch.zeros(N, pd[-2], **f32)
-        self.Z = torch.zeros(N, pd[-1], **f32)
         self.prob = torch.zeros(N, pd[-1], **f32)
         self.loss = torch.zeros(2, **f32)  # [train, val]
         # backward buffers
@@ -179,7 +189,7 @@ class TrainEngine:
             sk = ops._split_k(M_, N_, K_)
             self._gemm_plans[(M_, N_, K_)] = sk
             need = max(need, L.pg_gemm_f32_workspace(M_, N_, K_, sk))
-        need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C))
+        need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
         self.ws_bytes = self.ws.numel()
         # PLAGNN_OVERLAP=1: weight gradients on a side stream, off the critical path (dgrad ->
@@ -340,27 +350,26 @@ class TrainEngine:
                        tag=f"gemm.fwd.cat.l{l + 1}")
         self._gemm(self.A3, P["liner1.W"], self.A4, transb=True, bias=P["liner1.b"], act=LEAKY,
                    tag="gemm.fwd.liner1")
-        self._gemm(self.A4, P["liner2.W"], self.Z, transb=True, bias=P["liner2.b"], act=NONE,
-                   tag="gemm.fwd.liner2")
-        C = self.C
+        self._head(_lib.PG_DTYPE_F32, self.A4, self.dZ, None, self.dA4)
+
+    def _head(self, a_dtype, A4, dZ, dZb, dA4) -> None:
+        """liner2 + sigmoid + train/val multi_loss + dZ + dA4 = (dZ W2) * leaky'(A4): one
+        fused pass (pg_mlp_head; code/model.py:28-29, code/train.py:89-108, 199-207)."""
+        P, pd, C = self.P, self.pd, self.C
         cp = pd[-1]
-        with self._t("loss"):
-            call("pg_sigmoid_multi_loss", ptr(self.Z), cp, self.N, C, ptr(self.labels), cp, ptr(self.cw),
-                 ptr(self.train_index), self.train_index.numel(), ptr(self.prob), cp, ptr(self.loss[0:1]),
-                 ptr(self.dZ), cp, ptr(self.ws), self.ws_bytes, st)
-            if self.val_index is not None and self.val_index.numel() > 0:
-                call("pg_sigmoid_multi_loss", ptr(self.Z), cp, self.N, C, ptr(self.labels), cp, ptr(self.cw),
-                     ptr(self.val_index), self.val_index.numel(), 0, cp, ptr(self.loss[1:2]), 0, cp,
-                     ptr(self.ws), self.ws_bytes, st)
+        with self._t("head"):
+            call("pg_mlp_head", ptr(A4), A4.stride(0), self.N, pd[-2], a_dtype, ptr(P["liner2.W"]), pd[-2],
+                 ptr(P["liner2.b"]), C, ptr(self.labels), cp, ptr(self.cw), ptr(self.row_set), self.n_train,
+                 self.n_val, ptr(self.prob), cp, ptr(dZ), cp, ptr(dZb), ptr(dA4), dA4.stride(0), LEAKY_SLOPE,
+                 ptr(self.loss), ptr(self.ws), self.ws_bytes, self._s())
 
     def backward(self) -> None:
         st = self._s()
         G, P, pd = self.G, self.P, self.pd
         g = self.dg.fwd.struct(self.ews)
         gt = self.dg.bwd.struct(None)
-        # liner2: dW2 = dZ^T A4 (+ db2 = row sums of dZ^T); dA4 = (dZ W2) * leaky'(A4)
+        # liner2: dW2 = dZ^T A4 (+ db2 = row sums of dZ^T); dA4 came from the fused head
         self._wgrad(self.dZ, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
-        self._gemm(self.dZ, P["liner2.W"], self.dA4, act=LEAKY, dact=self.A4, tag="gemm.dgrad.liner2")
         # liner1
         self._wgrad(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
         self._gemm(self.dA4, P["liner1.W"], self.dA3, act=LEAKY, dact=self.A3, tag="gemm.dgrad.liner1")
@@ -475,8 +484,10 @@ class TrainEngine:
         return 4 * (N + 1) + 8 * E + (12 + a) * F * N
 
     def flops_per_step(self) -> int:
-        """Dense GEMM flops of one step at the true (unpadded) dims, forward + backward
-        (layer-1 input gradient skipped, as autograd does for the constant features)."""
+        """Flops of the step's GEMM launches at the true (unpadded) dims, forward + backward
+        (layer-1 input gradient skipped, as autograd does for the constant features). liner2's
+        forward and input-gradient products run inside the fused head, not as GEMMs, and are
+        not counted; its weight gradient is."""
         N, d = self.N, self.dims
         f = 0
         for l in range(self.L):
@@ -485,6 +496,6 @@ class TrainEngine:
             wgrad = fwd
             igrad = 2 * N * fo * fi + (2 * N * fo * fi + 2 * N * fi * fi if l > 0 else 0)
             f += fwd + wgrad + igrad
-        for (a, b) in ((d[-3], d[-2]), (d[-2], d[-1])):
-            f += 3 * 2 * N * a * b
+        f += 3 * 2 * N * d[-3] * d[-2]   # liner1: forward, weight and input gradients
+        f += 2 * N * d[-2] * d[-1]       # liner2: weight gradient
         return f

@@ -49,7 +49,6 @@ class TrainEngineBF16(TrainEngine):
         self.HM[0][:, :self.dims[0]] = features.to(dev, torch.float32).to(torch.bfloat16)
         self.A3 = torch.zeros(N, pd[-3], **bf)
         self.A4 = torch.zeros(N, pd[-2], **bf)
-        self.Z = torch.zeros(N, pd[-1], **f32)
         self.prob = torch.zeros(N, pd[-1], **f32)
         self.loss = torch.zeros(2, **f32)
         self.dZ = torch.zeros(N, pd[-1], **f32)
@@ -67,7 +66,6 @@ class TrainEngineBF16(TrainEngine):
             wl.add(f"conv{l + 1}.Wcat", (Fo, 2 * Fi))
             wl.add(f"conv{l + 1}.Wstack", (Fo + Fi, Fi))  # [Wself ; Wpool]
         wl.add("liner1.W", (pd[-2], pd[-3]))
-        wl.add("liner2.W", (pd[-1], pd[-2]))
         idx = np.full(wl.size, -1, np.int64)
         src = self.flat_layout.offsets
 
@@ -87,7 +85,6 @@ class TrainEngineBF16(TrainEngine):
             put(p + "Wcat", wc)
             put(p + "Wstack", np.concatenate([wc[:, :Fi], wp], axis=0))
         put("liner1.W", ids("liner1.W", (pd[-2], pd[-3])))
-        put("liner2.W", ids("liner2.W", (pd[-1], pd[-2])))
         self.wb_layout = wl
         self.wb_map = torch.from_numpy(idx.astype(np.int32)).to(self.device)
         self.wb = torch.zeros(wl.size, dtype=torch.bfloat16, device=self.device)
@@ -157,18 +154,8 @@ class TrainEngineBF16(TrainEngine):
                        tag=f"gemm.fwd.cat.l{l + 1}")
         self._gemm(self.A3, W["liner1.W"], self.A4, transb=True, bias=P["liner1.b"], act=LEAKY,
                    tag="gemm.fwd.liner1")
-        self._gemm(self.A4, W["liner2.W"], self.Z, transb=True, bias=P["liner2.b"], act=NONE,
-                   tag="gemm.fwd.liner2")
-        C, cp = self.C, pd[-1]
-        with self._t("loss"):
-            call("pg_sigmoid_multi_loss", ptr(self.Z), cp, self.N, C, ptr(self.labels), cp, ptr(self.cw),
-                 ptr(self.train_index), self.train_index.numel(), ptr(self.prob), cp, ptr(self.loss[0:1]),
-                 ptr(self.dZ), cp, ptr(self.ws), self.ws_bytes, st)
-            if self.val_index is not None and self.val_index.numel() > 0:
-                call("pg_sigmoid_multi_loss", ptr(self.Z), cp, self.N, C, ptr(self.labels), cp, ptr(self.cw),
-                     ptr(self.val_index), self.val_index.numel(), 0, cp, ptr(self.loss[1:2]), 0, cp,
-                     ptr(self.ws), self.ws_bytes, st)
-            call("pg_cast_f32_bf16", ptr(self.dZ), 0, self.dZ.numel(), ptr(self.dZb), st)
+        # liner2 + loss + dZ + dA4 (f32 W2 / b2; bf16 A4, dZ copy and dA4)
+        self._head(BF16, self.A4, self.dZ, self.dZb, self.dA4)
 
     def backward(self) -> None:
         st = self._s()
@@ -177,7 +164,6 @@ class TrainEngineBF16(TrainEngine):
         gt = self.dg.bwd.struct(None)
         # liner2 / liner1 (weights W[out][in] as k images for the input gradients)
         self._gemm(self.dZb, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
-        self._gemm(self.dZb, W["liner2.W"], self.dA4, act=LEAKY, dact=self.A4, tag="gemm.dgrad.liner2")
         self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
         top = self.L - 1
         self._gemm(self.dA4, W["liner1.W"], self.DYP[top][:, :pd[top + 1]], act=LEAKY, dact=self.A3,
