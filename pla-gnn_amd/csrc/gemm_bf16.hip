@@ -46,18 +46,25 @@ namespace {
 
 using namespace pg_gemm;
 
-constexpr int BK = 64;  // bf16 k-values per K step
+constexpr int BK = 64;  // bf16 k-values per K step (two-stage kernels; deep ones use 32)
+#ifndef PG_BF16_DEEP
+#define PG_BF16_DEEP 0
+#endif
 
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 using lds_bf16x4 = __attribute__((address_space(3))) bf16x4;
 
-// element offset (u16 units) of (row, k) in an image
-template <int ROWS, bool KMAJ>
+// element offset (u16 units) of (row, k) in an image of KB k-values per row. Row images:
+// 128-B rows (KB = 64) swizzle chunk c to c ^ ((row >> 1) & 7), 64-B rows (KB = 32) to
+// c ^ ((row >> 2) & 3): either way 16 consecutive rows at one chunk hit 16 distinct bank
+// quads for ds_read_b128.
+template <int ROWS, bool KMAJ, int KB = BK>
 __device__ __forceinline__ int img_off(int row, int k) {
   if constexpr (!KMAJ) {
-    return row * BK + ((((k >> 3) ^ ((row >> 1) & 7))) << 3) + (k & 7);
+    if constexpr (KB == 64) return row * KB + ((((k >> 3) ^ ((row >> 1) & 7))) << 3) + (k & 7);
+    else return row * KB + ((((k >> 3) ^ ((row >> 2) & 3))) << 3) + (k & 7);
   } else {
     const int f = ROWS == 64 ? ((k >> 1) & 1) * 4 : (k & 3) * 4;
     return k * ROWS + ((((row >> 3) ^ f)) << 3) + (row & 7);
@@ -66,18 +73,21 @@ __device__ __forceinline__ int img_off(int row, int k) {
 
 // DMA of one ROWS x BK tile (rows [r0, r0 + ROWS) x k [k0, k0 + BK)) into an image;
 // units past K (kvalid) are zero-filled by the lane that owns them.
-template <int ROWS, bool KMAJ, bool FULL, int NW>
+template <int ROWS, bool KMAJ, bool FULL, int NW, int KB = BK>
 __device__ __forceinline__ void dma_tile(const uint16_t* __restrict__ P, int64_t ld, int r0, int R,
                                          int k0, int kvalid, uint16_t* S, int wave, int lane) {
-  static_assert((ROWS / 8) % NW == 0, "image pieces per wave");
+  constexpr int PIECES = ROWS * KB * 2 / 1024;  // 1-KiB pieces of the image
+  static_assert(PIECES % NW == 0, "image pieces per wave");
 #pragma unroll
-  for (int j = 0; j < ROWS / 8 / NW; ++j) {
-    const int piece = j * NW + wave;  // 1-KiB piece of the image
+  for (int j = 0; j < PIECES / NW; ++j) {
+    const int piece = j * NW + wave;
     const int u = piece * 64 + lane;  // 16-B unit
     const uint16_t* src;
     bool valid;
     if constexpr (!KMAJ) {
-      const int row = u >> 3, c = (u & 7) ^ ((row >> 1) & 7);
+      constexpr int UPR = KB / 8;  // units per row
+      const int row = u / UPR;
+      const int c = KB == 64 ? ((u & 7) ^ ((row >> 1) & 7)) : ((u & 3) ^ ((row >> 2) & 3));
       valid = 8 * c < kvalid;
       src = P + (int64_t)min(r0 + row, R - 1) * ld + k0 + 8 * c;
     } else {
@@ -94,11 +104,11 @@ __device__ __forceinline__ void dma_tile(const uint16_t* __restrict__ P, int64_t
 }
 
 // the 8 k-values of k-step s for MFMA row/col `rc` (tile-local) of lane half h
-template <int ROWS, bool KMAJ>
+template <int ROWS, bool KMAJ, int KB = BK>
 __device__ __forceinline__ bf16x8 frag(const uint16_t* __restrict__ S, int rc, int s, int lane) {
   if constexpr (!KMAJ) {
     const int h = lane >> 5;
-    return *reinterpret_cast<const bf16x8*>(S + img_off<ROWS, false>(rc, 16 * s + 8 * h));
+    return *reinterpret_cast<const bf16x8*>(S + img_off<ROWS, false, KB>(rc, 16 * s + 8 * h));
   } else {
     // ds_read_b64_tr_b16: lane 4q + p of a 16-lane group supplies the address of block row
     // q (k), columns 4p .. 4p + 3 (rows of the operand); the group's block is k-rows
@@ -108,9 +118,9 @@ __device__ __forceinline__ bf16x8 frag(const uint16_t* __restrict__ S, int rc, i
     const int m = rc - (lane & 15) + 4 * p;
     const int kb = 16 * s + 8 * (g >> 1);
     const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-        (lds_bf16x4*)(S + img_off<ROWS, true>(m, kb + q)));
+        (lds_bf16x4*)(S + img_off<ROWS, true, KB>(m, kb + q)));
     const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-        (lds_bf16x4*)(S + img_off<ROWS, true>(m, kb + 4 + q)));
+        (lds_bf16x4*)(S + img_off<ROWS, true, KB>(m, kb + 4 + q)));
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
@@ -121,14 +131,21 @@ __device__ __forceinline__ uint16_t f2bf(float x) {
 }
 
 // row sums of the A tile in LDS over its BK k-values (thread t: row t % BM, k-group t / BM)
-template <int BM, bool AK, int NT>
+template <int BM, bool AK, int NT, int KB = BK>
 __device__ __forceinline__ float img_rowsum(const uint16_t* __restrict__ As, int tid) {
   constexpr int G = NT / BM;
   const int m = tid % BM, g = tid / BM;
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < BK / G; ++i) s += bf2f(As[img_off<BM, AK>(m, g + i * G)]);
+  for (int i = 0; i < KB / G; ++i) s += bf2f(As[img_off<BM, AK, KB>(m, g + i * G)]);
   return s;
+}
+
+// s_waitcnt vmcnt(N) alone (expcnt, lgkmcnt left at their no-wait maxima), gfx9 encoding
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
 // epilogue through LDS: the accumulator tile is transposed into a row-major f32 image and
@@ -234,7 +251,13 @@ __device__ __forceinline__ void finish_tile(const f32x16 (&acc)[BM / WM / 32][BN
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool OBF>
+// KB k-values per stage, NS LDS stages. NS = 2: the tile for step t+1 is issued at the top
+// of step t and waited for by __syncthreads. NS > 2 (the 256 x 256 tiles, one workgroup per
+// CU, where nothing else hides the DMA latency): NS - 1 tiles in flight; each step waits for
+// the next tile only with a counted s_waitcnt vmcnt (the later tiles stay in flight) and a
+// raw s_barrier (cdna_hip_programming.md "Pipelining across barriers"); a partial last K
+// tile (fewer DMAs) switches the count to 0.
+template <int BM, int BN, int WM, int WN, int KB, int NS, bool TA, bool TB, int EPI, bool OBF>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
     int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
@@ -244,10 +267,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
   constexpr bool AK = TA, BKM = !TB;  // k images for A stored [k][m] / B stored [k][n]
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;  // 32 x 32 MFMA tiles per wave
-  constexpr int IA = BM * BK, IB = BN * BK;  // image sizes (u16)
-  // one LDS array [A0 | A1 | B0 | B1]; the epilogue reuses it as a row-major f32 image of
-  // the tile (in WM row bands when the whole tile does not fit)
-  constexpr int STAGE = 2 * (IA + IB);
+  constexpr int IA = BM * KB, IB = BN * KB;  // image sizes (u16)
+  constexpr int SS = KB / 16;                // MFMA k-steps per stage
+  constexpr int D = (BM + BN) * KB * 2 / 1024 / NW;  // DMA instructions per tile and wave
+  static_assert(SS >= 2 && SS % 2 == 0, "an even number (>= 2) of MFMA k-steps per stage");
+  // one LDS array [A0 .. A(NS-1) | B0 .. B(NS-1)]; the epilogue reuses it as a row-major f32
+  // image of the tile (in WM row bands when the whole tile does not fit)
+  constexpr int STAGE = NS * (IA + IB);
   constexpr int PASSES = 2 * BM * BN > STAGE ? WM : 1;
   constexpr int EPI_U16 = 2 * BM * BN / PASSES;
   __shared__ __attribute__((aligned(16))) uint16_t lds[STAGE > EPI_U16 ? STAGE : EPI_U16];
@@ -273,60 +299,83 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nk = kz1 > kz0 ? (kz1 - kz0 + BK - 1) / BK : 0;
+  const int nk = kz1 > kz0 ? (kz1 - kz0 + KB - 1) / KB : 0;
+  const bool tail = ((kz1 - kz0) % KB) != 0;  // the last tile is partial (fewer DMAs)
   auto issue = [&](int t, int buf) {
-    const int k0 = kz0 + t * BK;
-    if (kz1 - k0 >= BK) {
-      dma_tile<BM, AK, true, NW>(A, lda, m0, M, k0, BK, lds + buf * IA, wave, lane);
-      dma_tile<BN, BKM, true, NW>(B, ldb, n0, N, k0, BK, lds + 2 * IA + buf * IB, wave, lane);
+    const int k0 = kz0 + t * KB;
+    if (kz1 - k0 >= KB) {
+      dma_tile<BM, AK, true, NW, KB>(A, lda, m0, M, k0, KB, lds + buf * IA, wave, lane);
+      dma_tile<BN, BKM, true, NW, KB>(B, ldb, n0, N, k0, KB, lds + NS * IA + buf * IB, wave, lane);
     } else {
-      dma_tile<BM, AK, false, NW>(A, lda, m0, M, k0, kz1 - k0, lds + buf * IA, wave, lane);
-      dma_tile<BN, BKM, false, NW>(B, ldb, n0, N, k0, kz1 - k0, lds + 2 * IA + buf * IB, wave, lane);
+      dma_tile<BM, AK, false, NW, KB>(A, lda, m0, M, k0, kz1 - k0, lds + buf * IA, wave, lane);
+      dma_tile<BN, BKM, false, NW, KB>(B, ldb, n0, N, k0, kz1 - k0, lds + NS * IA + buf * IB, wave, lane);
+    }
+  };
+  // wait until tile `need` has landed (all waves), given tiles up to `last` issued
+  auto sync_tile = [&](int need, int last) {
+    if constexpr (NS == 2) {
+      __syncthreads();
+    } else {
+      const int after = last - need;  // tiles issued after `need`, still allowed in flight
+      if (after <= 0 || (tail && last == nk - 1)) wait_vmcnt<0>();
+      else if (after == 1) wait_vmcnt<D>();
+      else wait_vmcnt<2 * D>();
+      static_assert(NS <= 4, "vmcnt cases");
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS stores (zero fill)
+      __builtin_amdgcn_s_barrier();
     }
   };
 
   if (nk > 0) {
-    issue(0, 0);
-    __syncthreads();
+    int issued = -1;
+    for (int p = 0; p < NS - 1 && p < nk; ++p) issue(p, p), issued = p;
+    sync_tile(0, issued);
     const int ra = wm * (BM / WM) + l32, rb = wn * (BN / WN) + l32;
     bf16x8 fa[2][TM], fb[2][TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) fa[0][i] = frag<BM, AK>(lds, ra + i * 32, 0, lane);
+    for (int i = 0; i < TM; ++i) fa[0][i] = frag<BM, AK, KB>(lds, ra + i * 32, 0, lane);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) fb[0][j] = frag<BN, BKM>(lds + 2 * IA, rb + j * 32, 0, lane);
+    for (int j = 0; j < TN; ++j) fb[0][j] = frag<BN, BKM, KB>(lds + NS * IA, rb + j * 32, 0, lane);
     for (int t = 0; t < nk; ++t) {
-      const int cur = t & 1;
-      const bool more = t + 1 < nk;
-      if (more) issue(t + 1, cur ^ 1);
+      const int cur = t % NS;
+      // the next tile into the buffer every wave finished reading before the last barrier
+      if (t + NS - 1 < nk) {
+        issue(t + NS - 1, (t + NS - 1) % NS);
+        issued = t + NS - 1;
+      }
       const uint16_t* As = lds + cur * IA;
-      const uint16_t* Bs = lds + 2 * IA + cur * IB;
-      if (do_rs) rs += img_rowsum<BM, AK, NT>(As, tid);
+      const uint16_t* Bs = lds + NS * IA + cur * IB;
+      if (do_rs) rs += img_rowsum<BM, AK, NT, KB>(As, tid);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < SS; ++s) {
         const int u = s & 1;
-        if (s < 3) {
+        if (s < SS - 1) {
 #pragma unroll
-          for (int i = 0; i < TM; ++i) fa[u ^ 1][i] = frag<BM, AK>(As, ra + i * 32, s + 1, lane);
+          for (int i = 0; i < TM; ++i) fa[u ^ 1][i] = frag<BM, AK, KB>(As, ra + i * 32, s + 1, lane);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) fb[u ^ 1][j] = frag<BN, BKM>(Bs, rb + j * 32, s + 1, lane);
+          for (int j = 0; j < TN; ++j) fb[u ^ 1][j] = frag<BN, BKM, KB>(Bs, rb + j * 32, s + 1, lane);
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[u][i], fb[u][j], acc[i][j], 0, 0, 0);
-        if (s == 2) {
-          __syncthreads();  // tile t+1 landed and every wave is past its reads of tile t-1
-          if (more) {
+        if (s == SS - 2) {
+          // tile t+1 landed and every wave is past its reads of tile t-1
+          if (t + 1 < nk) sync_tile(t + 1, issued);
+          else if constexpr (NS == 2) __syncthreads();
+          if (t + 1 < nk) {
+            const int nx = (t + 1) % NS;
 #pragma unroll
-            for (int i = 0; i < TM; ++i) fa[0][i] = frag<BM, AK>(lds + (cur ^ 1) * IA, ra + i * 32, 0, lane);
+            for (int i = 0; i < TM; ++i) fa[0][i] = frag<BM, AK, KB>(lds + nx * IA, ra + i * 32, 0, lane);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-              fb[0][j] = frag<BN, BKM>(lds + 2 * IA + (cur ^ 1) * IB, rb + j * 32, 0, lane);
+              fb[0][j] = frag<BN, BKM, KB>(lds + NS * IA + nx * IB, rb + j * 32, 0, lane);
           }
         }
       }
     }
+    if constexpr (NS > 2) wait_vmcnt<0>();
     __syncthreads();  // the epilogue reuses the staging array
   }
   finish_tile<BM, BN, WM, WN, EPI, OBF, PASSES>(acc, rs, do_rs, reinterpret_cast<float*>(lds), tid, m0, n0, M, N, alpha,
@@ -354,8 +403,14 @@ struct Args {
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool OBF>
 int launch_epi(int epi, dim3 grid, hipStream_t st, const Args& a) {
+  // KB = 64 x 2 stages. PG_BF16_DEEP=1 (build-time experiment): 256 x 256 tiles with KB = 32
+  // x 4 stages and counted vmcnt instead; measured slower (fwd.cat 670 us either way, 8192^3
+  // 1580 vs 1180 us): the DMA latency is not what holds this structure back.
+  constexpr bool deep = PG_BF16_DEEP && BM == 256 && BN == 256;
+  constexpr int KB = deep ? 32 : 64;
+  constexpr int NS = deep ? 4 : 2;
 #define PG_L(EPI_)                                                                                    \
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, TA, TB, EPI_, OBF>), grid, dim3(64 * WM * WN), 0, st, \
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, KB, NS, TA, TB, EPI_, OBF>), grid, dim3(64 * WM * WN), 0, st, \
                      a.M, a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb,   \
                      a.beta, a.C, a.ldc, a.bias, a.slope, a.dact, a.lddact, a.rowsum, a.ws,      \
                      a.ws_rowsum)
