@@ -15,7 +15,8 @@ import os
 from collections import defaultdict
 
 GROUPS = {
-    "gemm_f32_kernel": "gemm_f32", "splitk_reduce_kernel": "gemm_f32",
+    "gemm_f32_kernel": "gemm_f32", "gemm_dma_kernel": "gemm_f32", "splitk_reduce_kernel": "gemm_f32",
+    "gemm_bf16_kernel": "gemm_f32", "head_kernel": "head", "head_final_kernel": "head",
     "max_fwd_kernel": "spmm_max_fwd", "max_merge_kernel": "spmm_max_fwd",
     "group_pack_kernel": "spmm_max_bwd", "max_bwd_pull_kernel": "spmm_max_bwd",
     "max_bwd_kernel": "spmm_max_bwd", "sum_merge_kernel": "spmm_max_bwd",
@@ -25,8 +26,8 @@ GROUPS = {
 
 
 def group_of(name):
-    n = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("<")[0]
-    return GROUPS.get(n.strip())
+    n = name.replace("(anonymous namespace)::", "").replace("pg_gemm::", "").replace("void ", "")
+    return GROUPS.get(n.split("(")[0].split("<")[0].strip())
 
 
 def collect(root, counter):
@@ -49,7 +50,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("config")
-    ap.add_argument("--launches", default="gemm_f32=23,spmm_max_fwd=3,spmm_max_bwd=3,loss=1,adam=1")
+    ap.add_argument("--launches", default="gemm_f32=21,spmm_max_fwd=3,spmm_max_bwd=3,head=1,adam=1")
+    ap.add_argument("--gemm-group", default="gemm_f32", help="name of the GEMM group (gemm_bf16 for cfg5)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
@@ -60,7 +62,9 @@ def main():
     cfg = {}
     for g in sorted(set(fetch) | set(write)):
         per_step = (2 * fetch.get(g, 0.0) / max(s1, 1) + write.get(g, 0.0) / max(s2, 1)) * 1024
-        cfg[g] = per_step / launches.get(g, 1.0)
+        cfg[g] = per_step / launches.get(g if g != "gemm_f32" else "gemm_f32", 1.0)
+    if a.gemm_group != "gemm_f32" and "gemm_f32" in cfg:
+        cfg[a.gemm_group] = cfg.pop("gemm_f32")
     out[a.config] = cfg
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
