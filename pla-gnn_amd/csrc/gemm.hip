@@ -201,7 +201,7 @@ __device__ __forceinline__ void finish_tile(
     const f32x16 (&acc)[BM / 64][BN / 64], float rs, bool do_rs, float* __restrict__ rsred, int tid,
     int m0, int n0, int M, int N, float alpha, float beta, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias, float slope, const float* __restrict__ dact, int64_t lddact,
-    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum) {
+    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum, int kz) {
   constexpr bool SPLIT = EPI == EPI_SPLIT;
   constexpr int TM = BM / 64, TN = BN / 64;
   const int lane = tid & 63, wave = tid >> 6;
@@ -213,7 +213,7 @@ __device__ __forceinline__ void finish_tile(
     if (tid < BM && m0 + tid < M) {
       float t = 0.f;
       for (int g = 0; g < kThreads / BM; ++g) t += rsred[g * BM + tid];
-      if constexpr (SPLIT) ws_rowsum[(int64_t)blockIdx.z * M + m0 + tid] = t;
+      if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = t;
       else rowsum[m0 + tid] = t;
     }
   }
@@ -231,7 +231,7 @@ __device__ __forceinline__ void finish_tile(
         const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row >= M) continue;
         if constexpr (SPLIT) {
-          ws[((int64_t)blockIdx.z * M + row) * N + col] = acc[i][j][r];
+          ws[((int64_t)kz * M + row) * N + col] = acc[i][j][r];
         } else {
           float v = alpha * acc[i][j][r];
           if (beta != 0.f) v = v + beta * C[(int64_t)row * ldc + col];
@@ -254,7 +254,7 @@ __device__ __forceinline__ void finish_tile_lds(
     const f32x16 (&acc)[BM / 64][BN / 64], float rs, bool do_rs, float* __restrict__ lds, int tid,
     int m0, int n0, int M, int N, float alpha, float beta, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias, float slope, const float* __restrict__ dact, int64_t lddact,
-    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum) {
+    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum, int kz) {
   constexpr bool SPLIT = EPI == EPI_SPLIT;
   constexpr int TM = BM / 64, TN = BN / 64;
   const int lane = tid & 63, wave = tid >> 6;
@@ -265,7 +265,7 @@ __device__ __forceinline__ void finish_tile_lds(
     if (tid < BM && m0 + tid < M) {
       float t = 0.f;
       for (int g = 0; g < kThreads / BM; ++g) t += lds[g * BM + tid];
-      if constexpr (SPLIT) ws_rowsum[(int64_t)blockIdx.z * M + m0 + tid] = t;
+      if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = t;
       else rowsum[m0 + tid] = t;
     }
     __syncthreads();
@@ -288,7 +288,7 @@ __device__ __forceinline__ void finish_tile_lds(
     if (gr >= M || gc >= N) continue;
     float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
     if constexpr (SPLIT) {
-      *reinterpret_cast<float4*>(ws + ((int64_t)blockIdx.z * M + gr) * N + gc) = v;
+      *reinterpret_cast<float4*>(ws + ((int64_t)kz * M + gr) * N + gc) = v;
     } else {
       float* cp = C + (int64_t)gr * ldc + gc;
       float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
 #endif
 
   finish_tile<BM, BN, EPI>(acc, rs, do_rs, rsred, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
-                           slope, dact, lddact, rowsum, ws, ws_rowsum);
+                           slope, dact, lddact, rowsum, ws, ws_rowsum, blockIdx.z);
 #if PG_GEMM_STAMP
   stamp(st_rt, st_ck, tid);
 #endif
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
     float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
     const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
-    float* __restrict__ ws, float* __restrict__ ws_rowsum, int vec_out) {
+    float* __restrict__ ws, float* __restrict__ ws_rowsum, int vec_out, int n_split) {
   constexpr bool AK = TA, BKM = !TB;
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int IA = BM * BK, IB = BN * BK;  // image sizes (floats)
@@ -586,14 +586,20 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
   // the DMA at every LDS read)
   __shared__ __attribute__((aligned(16))) float lds[2 * (IA + IB)];
 
+  // XCD-aware order over the (slice, tile) items of a 1-D grid: blocks b, b + 8, ... share
+  // an XCD and take a contiguous run of slice-major item ids, so an XCD holds whole
+  // K-slices (every tile of a slice reads the same K rows of A and B: they meet in one L2)
+  // and, without split, the column tiles of a row tile (their shared A rows)
   const int b = blockIdx.x;
-  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
-  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int items = tiles * n_split;
+  const int q8 = items / 8, r8 = items % 8, x8 = b % 8;
+  const int item = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int kz = item / tiles, tile = item % tiles;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kz0 = blockIdx.z * k_per_split;
+  const int kz0 = kz * k_per_split;
   const int kz1 = min(K, kz0 + k_per_split);
   const bool do_rs = rowsum != nullptr && tn == 0;
 #if PG_GEMM_STAMP
@@ -685,10 +691,10 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
 #endif
   if (vec_out)
     finish_tile_lds<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
-                                 slope, dact, lddact, rowsum, ws, ws_rowsum);
+                                 slope, dact, lddact, rowsum, ws, ws_rowsum, kz);
   else
     finish_tile<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
-                             slope, dact, lddact, rowsum, ws, ws_rowsum);
+                             slope, dact, lddact, rowsum, ws, ws_rowsum, kz);
 #if PG_GEMM_STAMP
   stamp(st_rt, st_ck, tid);
 #endif
@@ -738,10 +744,10 @@ int launch_epi(int epi, dim3 grid, hipStream_t st, const Args& a) {
 template <int BM, int BN, bool TA, bool TB>
 int launch_dma(int epi, dim3 grid, hipStream_t st, const Args& a) {
 #define PG_L(EPI_)                                                                          \
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, EPI_>), grid, dim3(kThreads), 0, st, a.M, \
-                     a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb,     \
-                     a.beta, a.C, a.ldc, a.bias, a.slope, a.dact, a.lddact, a.rowsum, a.ws,    \
-                     a.ws_rowsum, a.vec_out)
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, EPI_>), dim3(grid.x * grid.z), dim3(kThreads), \
+                     0, st, a.M, a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B,  \
+                     a.ldb, a.beta, a.C, a.ldc, a.bias, a.slope, a.dact, a.lddact, a.rowsum,     \
+                     a.ws, a.ws_rowsum, a.vec_out, (int)grid.z)
   switch (epi) {
     case EPI_NONE: PG_L(EPI_NONE); break;
     case EPI_RELU: PG_L(EPI_RELU); break;
