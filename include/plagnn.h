@@ -156,12 +156,17 @@ int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, f
 /* Deterministic backward (gather over the transposed CSR gt of g; gt->epos required):
  *   dx[u,f] = sum_{(v,j) in gt row u, ascending v} [argpos[v,f] == j - g.ptr[v]] * ew[j] * dout[v,f]
  * then, if mask_src != NULL, dx[u,f] *= (mask_src[u,f] > 0)  (relu' of fc_pool).
+ * fwd_out (optional, needs mask_src = the forward's input X): the forward's output. An
+ * entry (v, f) with fwd_out[v,f] == 0 is skipped: its winner u has X[u,f] * w == 0, so it
+ * is either masked (X[u,f] = 0) or weighted 0 — the result is unchanged, and the dead
+ * features whose ties all sit at position 0 no longer crowd one list. (A +-inf maximum,
+ * stored as 0, is skipped too.)
  * Every dx element is written (no zero-fill needed). */
 size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F);
 int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
                     int arg_kind, const float* dout, int64_t ldd, int64_t F,
-                    const float* mask_src, int64_t ldm, float* dx, int64_t ldx, void* ws,
-                    size_t ws_bytes, pg_stream_t stream);
+                    const float* mask_src, int64_t ldm, const float* fwd_out, int64_t ldf,
+                    float* dx, int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream);
 
 /* DGL-form backward: dx = 0; dx[src(argpos[v,f]), f] += ew * dout[v,f] with f32
  * atomics (summation order not reproducible). The callee zero-fills dx. */
@@ -288,8 +293,8 @@ int pg_spmm_max_fwd_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t 
                          size_t ws_bytes, pg_stream_t stream);
 int pg_spmm_max_bwd_bf16(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
                          int arg_kind, const void* dout, int64_t ldd, int64_t F,
-                         const void* mask_src, int64_t ldm, void* dx, int64_t ldx, void* ws,
-                         size_t ws_bytes, pg_stream_t stream);
+                         const void* mask_src, int64_t ldm, const void* fwd_out, int64_t ldf,
+                         void* dx, int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream);
 /* dst[i] = bf16(src[map ? map[i] : i]) (map[i] < 0: 0), round to nearest even: the bf16
  * weight copies of the f32 master parameters, in any layout the GEMMs want. */
 int pg_cast_f32_bf16(const float* src, const int32_t* map, int64_t n, void* dst, pg_stream_t stream);
@@ -373,7 +378,7 @@ int pg_perturb_fill(const double* xc_normal, const double* xc_inter, const doubl
 
 /* ---------------- misc ---------------- */
 const char* pg_last_error_string(void);
-int pg_version(void); /* 2: pg_csr_t.einv */
+int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out */
 
 #ifdef __cplusplus
 }

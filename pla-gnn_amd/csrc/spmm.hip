@@ -425,8 +425,8 @@ template <typename A, typename T>
 __device__ __forceinline__ void pack_short_row(
     int v, int wave, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    uint16_t* __restrict__ gfeat, int2* __restrict__ glist, float* __restrict__ dpack,
-    int* __restrict__ lds) {
+    const T* __restrict__ fout, int64_t ldf, uint16_t* __restrict__ gfeat, int2* __restrict__ glist,
+    float* __restrict__ dpack, int* __restrict__ lds) {
   constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
   const int lane = lane_id();
   // every independent load first: the row bounds, the argmax record and the upstream
@@ -442,6 +442,15 @@ __device__ __forceinline__ void pack_short_row(
     const int f = lane + i * kWave;
     a[i] = f < F ? (int)ar[f] : arg_none<A>();
     d[i] = f < F ? to_f(dr[f]) : 0.f;
+  }
+  if (fout) {  // a zero maximum: its winner's relu mask is 0, the entry contributes nothing
+    const T* fr = fout + (int64_t)v * ldf;
+    float m[MAXW];
+#pragma unroll
+    for (int i = 0; i < MAXW; ++i) m[i] = to_f(fr[min(lane + i * kWave, F - 1)]);
+#pragma unroll
+    for (int i = 0; i < MAXW; ++i)
+      if (m[i] == 0.f) a[i] = arg_none<A>();
   }
   const int deg = re - rs;
   if (deg > kPackWaveMax || deg == 0) return;
@@ -499,8 +508,8 @@ template <typename A, typename T>
 __device__ __forceinline__ void pack_long_row(
     int v, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    uint16_t* __restrict__ gfeat, int2* __restrict__ glist, float* __restrict__ dpack,
-    int* __restrict__ lds) {
+    const T* __restrict__ fout, int64_t ldf, uint16_t* __restrict__ gfeat, int2* __restrict__ glist,
+    float* __restrict__ dpack, int* __restrict__ lds) {
   int* hist = lds;
   uint16_t* feats = reinterpret_cast<uint16_t*>(lds + kHistMax + 8);
   int* wsum = lds + kHistMax + 8 + kGroupMaxF / 2;
@@ -522,6 +531,15 @@ __device__ __forceinline__ void pack_long_row(
       const int f = threadIdx.x + i * kBlock;
       a[i] = f < F ? (int)ar[f] : arg_none<A>();
       d[i] = f < F ? to_f(dr[f]) : 0.f;
+    }
+    if (fout) {  // zero maxima contribute nothing (their winner's relu mask is 0)
+      const T* fr = fout + (int64_t)v * ldf;
+      float m[FPT];
+#pragma unroll
+      for (int i = 0; i < FPT; ++i) m[i] = to_f(fr[min((int)threadIdx.x + i * kBlock, F - 1)]);
+#pragma unroll
+      for (int i = 0; i < FPT; ++i)
+        if (m[i] == 0.f) a[i] = arg_none<A>();
     }
     for (int p = threadIdx.x; p < deg; p += kBlock) hist[p] = 0;
     __syncthreads();
@@ -565,7 +583,8 @@ __device__ __forceinline__ void pack_long_row(
       uint32_t key = 0xFFFFFFFFu;
       if (i < F) {
         const int a = (int)ar[i];
-        if (a != arg_none<A>()) key = ((uint32_t)a << 16) | (uint32_t)i;
+        const bool live = !fout || to_f(fout[(int64_t)v * ldf + i]) != 0.f;
+        if (a != arg_none<A>() && live) key = ((uint32_t)a << 16) | (uint32_t)i;
       }
       keys[i] = key;
     }
@@ -622,16 +641,19 @@ template <typename A, typename T = float>
 __global__ __launch_bounds__(kBlock) void group_pack_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
     const int32_t* __restrict__ einv, const A* __restrict__ arg, int64_t lda, int F,
-    const T* __restrict__ dout, int64_t ldd, uint16_t* __restrict__ gfeat,
+    const T* __restrict__ dout, int64_t ldd, const T* __restrict__ fout, int64_t ldf,
+    uint16_t* __restrict__ gfeat,
     int2* __restrict__ glist, float* __restrict__ dpack) {
   __shared__ __attribute__((aligned(16))) int lds[kPackLds];
   const int b = blockIdx.x;
   if (b < n_long) {
-    pack_long_row<A, T>(rows ? rows[b].x : b, ptr, einv, arg, lda, F, dout, ldd, gfeat, glist, dpack, lds);
+    pack_long_row<A, T>(rows ? rows[b].x : b, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gfeat, glist,
+                        dpack, lds);
   } else {
     const int wave = wave_id_uniform();
     const int v = (b - n_long) * kWavesPerBlock + wave;
-    if (v < n_rows) pack_short_row<A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, gfeat, glist, dpack, lds);
+    if (v < n_rows)
+      pack_short_row<A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gfeat, glist, dpack, lds);
   }
 }
 
@@ -1131,7 +1153,8 @@ namespace {
 template <typename T>
 int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
                   int arg_kind, const T* dout, int64_t ldd, int64_t F, const T* mask_src,
-                  int64_t ldm, T* dx, int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream) {
+                  int64_t ldm, const T* fwd_out, int64_t ldf, T* dx, int64_t ldx, void* ws,
+                  size_t ws_bytes, pg_stream_t stream) {
   PG_TRY(pg::check_csr(g, "pg_spmm_max_bwd", false));
   PG_TRY(pg::check_csr(gt, "pg_spmm_max_bwd", true));
   if (!pg::valid_arg_kind(arg_kind))
@@ -1140,8 +1163,10 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: gt is not the transpose of g");
   if (gt->nnz > 0 && (!gt->epos || !gt->eslot))
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: gt needs eslot and epos");
-  if (F < 0 || ldd < F || ldx < F || lda < F || (mask_src && ldm < F))
+  if (F < 0 || ldd < F || ldx < F || lda < F || (mask_src && ldm < F) || (fwd_out && ldf < F))
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: bad F/leading dims");
+  if (fwd_out && !mask_src)
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: fwd_out (skip zero maxima) needs mask_src");
   if (F == 0 || gt->n_rows == 0) return pg::ok();
   if (!argpos || !dout || !dx) return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: NULL buffer");
   const size_t need = pg_spmm_max_bwd_workspace(gt, F);
@@ -1180,7 +1205,7 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     const int n_short_blocks = (int)((N + kWavesPerBlock - 1) / kWavesPerBlock);
     hipLaunchKernelGGL((group_pack_kernel<uint16_t, T>), dim3((unsigned)(n_long + n_short_blocks)),
                        dim3(kBlock), 0, st, listed ? (const int4*)g->merges : nullptr, n_long,
-                       (int)N, g->ptr, einv, arg16, lda, (int)F, dout, ldd, gfeat, glist, dpack);
+                       (int)N, g->ptr, einv, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, gfeat, glist, dpack);
     const int blocks = grid_for(gt->n_items);
     if (g->ew)
       hipLaunchKernelGGL((max_bwd_pull_kernel<true, T>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
@@ -1215,19 +1240,19 @@ extern "C" {
 
 int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
                     int arg_kind, const float* dout, int64_t ldd, int64_t F,
-                    const float* mask_src, int64_t ldm, float* dx, int64_t ldx, void* ws,
-                    size_t ws_bytes, pg_stream_t stream) {
-  return max_bwd_entry<float>(g, gt, argpos, lda, arg_kind, dout, ldd, F, mask_src, ldm, dx, ldx,
-                              ws, ws_bytes, stream);
+                    const float* mask_src, int64_t ldm, const float* fwd_out, int64_t ldf,
+                    float* dx, int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream) {
+  return max_bwd_entry<float>(g, gt, argpos, lda, arg_kind, dout, ldd, F, mask_src, ldm, fwd_out, ldf,
+                              dx, ldx, ws, ws_bytes, stream);
 }
 
 int pg_spmm_max_bwd_bf16(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
                          int arg_kind, const void* dout, int64_t ldd, int64_t F,
-                         const void* mask_src, int64_t ldm, void* dx, int64_t ldx, void* ws,
-                         size_t ws_bytes, pg_stream_t stream) {
+                         const void* mask_src, int64_t ldm, const void* fwd_out, int64_t ldf,
+                         void* dx, int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream) {
   return max_bwd_entry<uint16_t>(g, gt, argpos, lda, arg_kind, (const uint16_t*)dout, ldd, F,
-                                 (const uint16_t*)mask_src, ldm, (uint16_t*)dx, ldx, ws, ws_bytes,
-                                 stream);
+                                 (const uint16_t*)mask_src, ldm, (const uint16_t*)fwd_out, ldf,
+                                 (uint16_t*)dx, ldx, ws, ws_bytes, stream);
 }
 
 int pg_spmm_max_bwd_scatter(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,

@@ -79,7 +79,7 @@ SIGNATURES = {
     "pg_spmm_max_fwd_workspace": (_sz, [_csr, _i64, _i]),
     "pg_spmm_max_fwd": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i, _vp, _sz, _vp]),
     "pg_spmm_max_bwd_workspace": (_sz, [_csr, _i64]),
-    "pg_spmm_max_bwd": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
+    "pg_spmm_max_bwd": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                              _vp, _sz, _vp]),
     "pg_spmm_max_bwd_scatter": (_i, [_csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "pg_spmm_sum_workspace": (_sz, [_csr, _i64]),
@@ -116,8 +116,8 @@ SIGNATURES = {
     "pg_gemm_bf16": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _i, _ep,
                           _i, _vp, _sz, _vp]),
     "pg_spmm_max_fwd_bf16": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i, _vp, _sz, _vp]),
-    "pg_spmm_max_bwd_bf16": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
-                                  _vp, _sz, _vp]),
+    "pg_spmm_max_bwd_bf16": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
+                                  _i64, _vp, _sz, _vp]),
     "pg_cast_f32_bf16": (_i, [_vp, _vp, _i64, _vp, _vp]),
     "pg_cast_bf16_f32": (_i, [_vp, _i64, _vp, _vp]),
     "pg_spmm_max_fwd_cpu": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i]),

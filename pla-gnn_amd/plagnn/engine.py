@@ -385,11 +385,11 @@ class TrainEngine:
                 self._gemm(dY, P[p + "Wcat"], dHM, tag=f"gemm.dgrad.cat.l{l + 1}")
             else:
                 self._gemm(dY, P[p + "Wcat"][:, Fi:], dHM[:, Fi:], tag=f"gemm.dgrad.cat.l{l + 1}")
-            # max backward with relu' of fc_pool fused
+            # max backward with relu' of fc_pool fused; zero maxima (M = 0) are skipped
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
                 call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
-                     dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(self.dP[l]), Fi, ptr(self.ws),
-                     self.ws_bytes, st)
+                     dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(self.dP[l]), Fi,
+                     ptr(self.ws), self.ws_bytes, st)
             # d Wpool = dP^T H, d bpool = sum_nodes dP
             self._wgrad(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
                         tag=f"gemm.wgrad.pool.l{l + 1}")

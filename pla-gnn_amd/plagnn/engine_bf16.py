@@ -178,7 +178,8 @@ class TrainEngineBF16(TrainEngine):
             self._gemm(dY, W[p + "Wcat"][:, Fi:], self.dM[l], tag=f"gemm.dgrad.neigh.l{l + 1}")
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
                 call("pg_spmm_max_bwd_bf16", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.dM[l]),
-                     Fi, Fi, ptr(self.Pl[l]), Fi, ptr(dP), DYP.stride(0), ptr(self.ws), self.ws_bytes, st)
+                     Fi, Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(dP), DYP.stride(0),
+                     ptr(self.ws), self.ws_bytes, st)
             self._gemm(dP, HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
                        tag=f"gemm.wgrad.pool.l{l + 1}")
             if l > 0:

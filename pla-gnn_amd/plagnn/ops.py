@@ -80,10 +80,12 @@ def spmm_max(dg: DeviceGraph, X: torch.Tensor, ew_slots: Optional[torch.Tensor] 
 
 def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
                       ew_slots: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
-                      dx: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      dx: Optional[torch.Tensor] = None, fwd_out: Optional[torch.Tensor] = None
+                      ) -> torch.Tensor:
     """dX of the max aggregation (DGL GSpMM.backward: scatter_add_ through argX),
     gathered per source in ascending destination order; optional fused relu' mask
-    (mask[u,f] > 0)."""
+    (mask[u,f] > 0). With `fwd_out` (the forward's output; needs mask = the forward's
+    input) entries whose maximum is 0 are skipped: they contribute nothing."""
     _check_device(dg, argpos, dout, ew_slots, mask)
     bf = dout.dtype == torch.bfloat16
     if bf and ((mask is not None and mask.dtype != torch.bfloat16) or not dg.is_cuda):
@@ -97,8 +99,9 @@ def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
     if dg.is_cuda:
         ws_n = _lib.lib().pg_spmm_max_bwd_workspace(gt, F)
         ws = _workspace(ws_n, dout.device)
+        ldf = _ld(fwd_out) if fwd_out is not None else 0
         call("pg_spmm_max_bwd_bf16" if bf else "pg_spmm_max_bwd", g, gt, ptr(argpos), _ld(argpos), dg.arg_kind, ptr(dout), _ld(dout),
-             F, ptr(mask), ldm, ptr(dx), _ld(dx), ptr(ws), ws_n, _stream(dout))
+             F, ptr(mask), ldm, ptr(fwd_out), ldf, ptr(dx), _ld(dx), ptr(ws), ws_n, _stream(dout))
     else:
         call("pg_spmm_max_bwd_cpu", g, gt, ptr(argpos), _ld(argpos), dg.arg_kind, ptr(dout),
              _ld(dout), F, ptr(mask), ldm, ptr(dx), _ld(dx))

@@ -299,3 +299,33 @@ def test_gemm_fused_activation_backward():
         full = A.double() @ B.double() + C0.double()
         ref = torch.where(Y > 0, full, full * slope)
         torch.testing.assert_close(Cd.cpu().double(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("F,weighted", [(256, False), (512, True), (64, False)])
+def test_spmm_max_bwd_skip_zero_maxima_is_exact(F, weighted):
+    """fwd_out = the forward's output: entries whose maximum is 0 are skipped (their winner is
+    relu-masked or weighted 0), and dx is bitwise unchanged — hub rows and dead features
+    (all-zero columns, whose ties all sit at position 0) included."""
+    from plagnn import ops
+
+    n = 800
+    src, dst = hub_graph(n, 3000, seed=F)
+    g = _graph(src, dst, n)
+    dg = g.on(DEV)
+    gen = torch.Generator().manual_seed(F + 1)
+    P = torch.relu(torch.randn(n, F, generator=gen))
+    P[:, ::3] = 0.0  # dead features
+    P = P.to(DEV)
+    ew = dg.edge_weight_slots(torch.rand(g.num_edges, generator=gen)) if weighted else None
+    if weighted:
+        ew[::7] = 0.0  # zero weights: max 0 with a live winner
+    out, arg = ops.spmm_max(dg, P, ew)
+    dZ = torch.randn(n, F, generator=gen).to(DEV)
+    a = ops.spmm_max_backward(dg, arg, dZ, ew, mask=P)
+    b = ops.spmm_max_backward(dg, arg, dZ, ew, mask=P, fwd_out=out)
+    assert torch.equal(a, b)
+    bf = P.to(torch.bfloat16)
+    outb, argb = ops.spmm_max(dg, bf, ew)
+    dZb = dZ.to(torch.bfloat16)
+    assert torch.equal(ops.spmm_max_backward(dg, argb, dZb, ew, mask=bf),
+                       ops.spmm_max_backward(dg, argb, dZb, ew, mask=bf, fwd_out=outb))
