@@ -196,7 +196,11 @@ class TrainEngine:
         # SpMM backward -> dgrad ...), with their own split-K workspace. Off by default: on
         # one MI355X the captured step measured 2.125 ms with it vs 2.092 ms without (the
         # GEMMs already fill the chip and crowd the latency-bound SpMM kernels).
-        self.overlap = os.environ.get("PLAGNN_OVERLAP", "0") == "1"
+        # PLAGNN_OVERLAP=<prefix>: only the weight gradients whose tag starts with
+        # gemm.wgrad.<prefix> (e.g. "cat": dW_cat beside the SpMM backward of its layer)
+        ov = os.environ.get("PLAGNN_OVERLAP", "0")
+        self.overlap = ov not in ("0", "")
+        self.overlap_prefix = "gemm.wgrad." + ("" if ov == "1" else ov)
         self.side = torch.cuda.Stream(dev) if self.overlap else None
         need2 = 256
         for (M_, N_, K_), sk in self._gemm_plans.items():
@@ -311,7 +315,7 @@ class TrainEngine:
     def _wgrad(self, *args, **kw):
         """A weight-gradient GEMM: forked onto the side stream at this point of the main
         stream (it sees everything issued so far), joined back before Adam (_join)."""
-        if not self.overlap:
+        if not self.overlap or not kw.get("tag", "").startswith(self.overlap_prefix):
             self._gemm(*args, **kw)
             return
         main = torch.cuda.current_stream(self.device)
