@@ -69,6 +69,10 @@ __device__ unsigned long long pg_gemm_kphase[64][4];   // start, prologue done, 
 #ifndef PG_GEMM_PRIO
 #define PG_GEMM_PRIO 0  // 1 = s_setprio(1) around each MFMA cluster
 #endif
+#ifndef PG_GEMM_XP
+#define PG_GEMM_XP 0  // experiment only (wrong results): 1 no in-loop DMA, 2 no MFMA, 4 no epilogue;
+                      // 8 / 16: stagger co-resident workgroups by 1024 / 512 cycles per slot
+#endif
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
@@ -615,6 +619,10 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nk = kz1 > kz0 ? (kz1 - kz0 + BK - 1) / BK : 0;
+  if constexpr ((PG_GEMM_XP & 24) != 0) {  // experiment: stagger co-resident workgroups
+    const int slot = (b / 256) % 8;
+    for (int i = 0; i < slot; ++i) __builtin_amdgcn_s_sleep((PG_GEMM_XP & 8) ? 16 : 8);
+  }
   // issue the DMA of K tile t into LDS image `buf`
   auto issue = [&](int t, int buf) {
     const int k0 = kz0 + t * BK;
@@ -642,7 +650,7 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     for (int t = 0; t < nk; ++t) {
       const int cur = t & 1;
       const bool more = t + 1 < nk;
-      if (more) issue(t + 1, cur ^ 1);
+      if (more && !(PG_GEMM_XP & 1)) issue(t + 1, cur ^ 1);
       const float* As = lds + cur * IA;
       const float* Bs = lds + 2 * IA + cur * IB;
       if (do_rs) rs += img_rowsum<BM, AK>(As, tid);
@@ -660,8 +668,10 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][i][s], fb[u][j][s], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TN; ++j) {
+              if constexpr (PG_GEMM_XP & 2) acc[i][j][s] += fa[u][i][s] * fb[u][j][s];
+              else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][i][s], fb[u][j][s], acc[i][j], 0, 0, 0);
+            }
         if (q == 2) {
 #if PG_GEMM_SCHED
           __builtin_amdgcn_sched_barrier(0);  // keep chunk 2's MFMAs ahead of the barrier
@@ -689,6 +699,17 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     pg_gemm_kphase[blockIdx.x][2] = __builtin_amdgcn_s_memtime();
   }
 #endif
+  if constexpr (PG_GEMM_XP & 4) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+    if (t == 1234.5f) C[tid] = t;
+    return;
+  }
   if (vec_out)
     finish_tile_lds<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
                                  slope, dact, lddact, rowsum, ws, ws_rowsum, kz);

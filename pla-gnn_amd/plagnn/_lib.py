@@ -81,6 +81,15 @@ SIGNATURES = {
     "pg_spmm_max_bwd_workspace": (_sz, [_csr, _i64]),
     "pg_spmm_max_bwd": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                              _vp, _sz, _vp]),
+    "pg_spmm_group_tiles": (_i64, [_i64]),
+    "pg_spmm_max_fwd_grouped": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "pg_spmm_max_fwd_grouped_bf16": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz,
+                                          _vp]),
+    "pg_spmm_max_bwd_grouped_workspace": (_sz, [_csr, _i64]),
+    "pg_spmm_max_bwd_grouped": (_i, [_csr, _csr, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _sz,
+                                     _vp]),
+    "pg_spmm_max_bwd_grouped_bf16": (_i, [_csr, _csr, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
+                                          _sz, _vp]),
     "pg_spmm_max_bwd_scatter": (_i, [_csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "pg_spmm_sum_workspace": (_sz, [_csr, _i64]),
     "pg_spmm_sum": (_i, [_csr, _vp, _i64, _i64, _i, _vp, _vp, _i64, _vp, _sz, _vp]),

@@ -145,6 +145,13 @@ class TrainEngine:
         self.row_set = torch.from_numpy(rs).to(dev)
         self.n_train = len(np.asarray(train_index))
         self.n_val = 0 if val_index is None else len(np.asarray(val_index))
+        # PLAGNN_GROUPED=1: the forward builds the backward's winner lists
+        # (pg_spmm_max_fwd_grouped) and the backward has no pack pass. Off by default: on cfg2
+        # the step measured 2.115 ms with it vs 2.058 ms on the argmax-record path
+        # (pg_spmm_max_fwd / pg_spmm_max_bwd with fwd_out): the forward's list building and
+        # the split rows' sorted lists cost more than the pack pass they remove
+        self.grouped = os.environ.get("PLAGNN_GROUPED", "0") == "1" and all(
+            self.dg.can_group(pd[l]) for l in range(self.L))
         self._alloc_buffers(features)
         self._alloc_workspace()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -157,12 +164,16 @@ class TrainEngine:
         N, pd, dev = self.N, self.pd, self.device
         # ---- activations ----
         f32 = dict(dtype=torch.float32, device=dev)
-        self.HM, self.Pl, self.arg = [], [], []
+        self.HM, self.Pl, self.arg, self.lists = [], [], [], []
         for l in range(self.L):
             Fi = pd[l]
             self.HM.append(torch.zeros(N, 2 * Fi, **f32))
             self.Pl.append(torch.zeros(N, Fi, **f32))
-            self.arg.append(torch.zeros(N, Fi, dtype=self.dg.arg_dtype, device=dev))
+            if self.grouped:
+                self.lists.append(ops.WinnerLists(self.dg, Fi))
+                self.arg.append(self.lists[-1].argpos)
+            else:
+                self.arg.append(torch.zeros(N, Fi, dtype=self.dg.arg_dtype, device=dev))
         self.HM[0][:, :self.dims[0]] = features.to(dev, torch.float32)
         self.A3 = torch.zeros(N, pd[-3], **f32)
         self.A4 = torch.zeros(N, pd[-2], **f32)
@@ -184,6 +195,7 @@ class TrainEngine:
             Fi = pd[l]
             need = max(need, L.pg_spmm_max_fwd_workspace(self.dg.fwd.struct(self.ews), Fi, self.dg.arg_kind))
             need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd.struct(None), Fi))
+            need = max(need, L.pg_spmm_max_bwd_grouped_workspace(self.dg.bwd.struct(None), Fi))
         self._gemm_plans = {}
         for (M_, N_, K_) in self._wgrad_shapes():
             sk = ops._split_k(M_, N_, K_)
@@ -345,8 +357,14 @@ class TrainEngine:
                        tag=f"gemm.fwd.pool.l{l + 1}")
             # M = max-aggregate(P) -> right half of HM
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
-                call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
-                     ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
+                if self.grouped:
+                    W_ = self.lists[l]
+                    call("pg_spmm_max_fwd_grouped", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
+                         ptr(W_.argpos), Fi, ptr(W_.gfeat), ptr(W_.glist), ptr(W_.rcnt), ptr(self.ws),
+                         self.ws_bytes, st)
+                else:
+                    call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
+                         ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
             # Y = [H | M] Wcat^T + b (fc_self + fc_neigh + bias), leaky_relu -> next input
             Fo = pd[l + 1]
             out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
@@ -391,9 +409,15 @@ class TrainEngine:
                 self._gemm(dY, P[p + "Wcat"][:, Fi:], dHM[:, Fi:], tag=f"gemm.dgrad.cat.l{l + 1}")
             # max backward with relu' of fc_pool fused; zero maxima (M = 0) are skipped
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
-                     dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(self.dP[l]), Fi,
-                     ptr(self.ws), self.ws_bytes, st)
+                if self.grouped:
+                    W_ = self.lists[l]
+                    call("pg_spmm_max_bwd_grouped", g, gt, ptr(W_.gfeat), ptr(W_.glist), ptr(W_.rcnt),
+                         ptr(dHM[:, Fi:]), dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(self.dP[l]), Fi,
+                         ptr(self.ws), self.ws_bytes, st)
+                else:
+                    call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
+                         dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(self.dP[l]),
+                         Fi, ptr(self.ws), self.ws_bytes, st)
             # d Wpool = dP^T H, d bpool = sum_nodes dP
             self._wgrad(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
                         tag=f"gemm.wgrad.pool.l{l + 1}")

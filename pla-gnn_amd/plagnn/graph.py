@@ -157,6 +157,11 @@ class DeviceGraph:
     def is_cuda(self) -> bool:
         return self.device.type == "cuda"
 
+    def can_group(self, F: int) -> bool:
+        """Whether pg_spmm_max_fwd_grouped takes this graph at feature width F."""
+        return (self.is_cuda and self.arg_kind == _lib.PG_ARG_U16 and 0 < self.fwd.chunk <= 256
+                and self.fwd.einv is not None and F % 4 == 0 and self.num_nodes * F < 2 ** 31 - 1)
+
     def edge_weight_slots(self, edge_weight: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
         """Edge weights given per edge id (DGL order) -> in-CSR slot order, f32 contiguous."""
         if edge_weight is None:

@@ -329,3 +329,80 @@ def test_spmm_max_bwd_skip_zero_maxima_is_exact(F, weighted):
     dZb = dZ.to(torch.bfloat16)
     assert torch.equal(ops.spmm_max_backward(dg, argb, dZb, ew, mask=bf),
                        ops.spmm_max_backward(dg, argb, dZb, ew, mask=bf, fwd_out=outb))
+
+
+@pytest.mark.parametrize("F,weighted,hub,chunk", [(64, False, 3000, 256), (256, True, 5000, 256),
+                                                  (300, False, 900, 64), (512, True, 2000, 256),
+                                                  (1000, False, 600, 128)])
+def test_spmm_max_grouped_matches_record_path(oracle_mod, F, weighted, hub, chunk):
+    """The grouped pair (the forward builds the winner lists) against the argmax-record
+    path: out and argmax-derived results bitwise equal; dx bitwise equal to
+    pg_spmm_max_bwd with fwd_out, and within 1e-6 of the oracle's scatter_add_. Covers
+    rows split by the schedule (chunk 64 / 128 / 256), a hub of 5000 in-edges (sorted
+    long-row lists), dead features, zero weights, F not a multiple of 256, and bf16."""
+    from plagnn import ops
+
+    n = 700
+    src, dst = hub_graph(n, hub, seed=F)
+    g = _graph(src, dst, n, chunk=chunk)
+    dg = g.on(DEV)
+    gen = torch.Generator().manual_seed(F + 3)
+    P = torch.relu(torch.randn(n, F, generator=gen))
+    P[:, ::5] = 0.0  # dead features: every tie at position 0
+    P = P.to(DEV)
+    ew = None
+    if weighted:
+        ew = dg.edge_weight_slots(torch.rand(g.num_edges, generator=gen))
+        ew[::7] = 0.0
+    out_r, arg = ops.spmm_max(dg, P, ew)
+    out_g, lists = ops.spmm_max_grouped(dg, P, ew)
+    assert torch.equal(out_r, out_g)
+    dZ = torch.randn(n, F, generator=gen).to(DEV)
+    dx_r = ops.spmm_max_backward(dg, arg, dZ, ew, mask=P, fwd_out=out_r)
+    dx_g = ops.spmm_max_backward_grouped(dg, lists, dZ, ew, mask=P)
+    assert torch.equal(dx_r, dx_g)
+    # every stored list entry is a live winner of its edge, and the counts add up
+    live = (out_r != 0).sum().item()
+    assert int(lists.rcnt.sum().item()) == live
+    w_np = None
+    if weighted:  # back to edge-id order for the oracle
+        w_np = torch.empty(g.num_edges)
+        w_np[dg.eid.cpu()] = ew.cpu()
+        w_np = w_np.numpy()
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False, edge_weight=w_np)
+    Pn = P.cpu().numpy()
+    ref_out, argx, arge = oracle_mod.spmm_max(og, Pn, use_weight=weighted)
+    np.testing.assert_array_equal(out_g.cpu().numpy(), ref_out)
+    ref = oracle_mod.spmm_max_bwd(og, argx, arge, dZ.cpu().numpy(), use_weight=weighted)
+    ref = np.where(Pn > 0, ref, 0.0)
+    np.testing.assert_allclose(dx_g.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    # bf16 storage
+    Pb, dZb = P.to(torch.bfloat16), dZ.to(torch.bfloat16)
+    ob_r, argb = ops.spmm_max(dg, Pb, ew)
+    ob_g, lb = ops.spmm_max_grouped(dg, Pb, ew)
+    assert torch.equal(ob_r, ob_g)
+    assert torch.equal(ops.spmm_max_backward(dg, argb, dZb, ew, mask=Pb, fwd_out=ob_r),
+                       ops.spmm_max_backward_grouped(dg, lb, dZb, ew, mask=Pb))
+
+
+def test_spmm_max_grouped_empty_rows():
+    """Rows without in-edges (no self-loops) get out = 0 and no lists; sources without
+    out-edges get dx = 0."""
+    from plagnn import ops
+
+    n = 400
+    rng = np.random.default_rng(5)
+    src = rng.integers(0, n // 2, 1500)
+    dst = rng.integers(0, n // 2, 1500)
+    g = _graph(src, dst, n)
+    dg = g.on(DEV)
+    P = torch.relu(torch.randn(n, 128)).to(DEV)
+    out_r, arg = ops.spmm_max(dg, P)
+    out_g, lists = ops.spmm_max_grouped(dg, P)
+    assert torch.equal(out_r, out_g)
+    assert torch.all(out_g[n // 2:] == 0)
+    assert torch.all(lists.rcnt[:, n // 2:] == 0)
+    dZ = torch.randn(n, 128).to(DEV)
+    dx_g = ops.spmm_max_backward_grouped(dg, lists, dZ, mask=P)
+    assert torch.equal(dx_g, ops.spmm_max_backward(dg, arg, dZ, mask=P, fwd_out=out_r))
+    assert torch.all(dx_g[n // 2:] == 0)

@@ -13,7 +13,7 @@ from conftest import ROOT, hub_graph, random_graph
 
 def _declared_symbols():
     h = open(os.path.join(ROOT, "include", "plagnn.h")).read()
-    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(pg_[a-z0-9_]+)\(", h, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|size_t|const char\*)\s+(pg_[a-z0-9_]+)\(", h, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
