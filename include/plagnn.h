@@ -279,6 +279,11 @@ typedef struct pg_gemm_epilogue {
   int64_t lddact;
   float* rowsum;     /* if not NULL: rowsum[m] = sum_k op(A)[m][k] (overwritten). For a weight
                         gradient dY^T X (transa) these are the bias gradients sum_nodes dY. */
+  uint32_t* splitk_cnt; /* pg_gemm_f32 with split_k > 1 (optional): pg_gemm_splitk_counters(M, N)
+                        u32 tile counters, zero before the first call and left zero by every call
+                        (one set per concurrently running call). With them the partial slabs are
+                        summed inside the GEMM by the last workgroup of each tile (slice order
+                        0, 1, ...: deterministic) instead of by a second launch. */
 } pg_gemm_epilogue_t;
 
 /* C[M,N] = alpha * op(A) * op(B) + beta * C, then the epilogue.
@@ -290,6 +295,7 @@ typedef struct pg_gemm_epilogue {
  * about five 64 x 64 workgroups per CU, each slice >= 96 entries of K, at most 256. */
 int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K);
 size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k);
+int64_t pg_gemm_splitk_counters(int64_t M, int64_t N);
 int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
                 int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
@@ -414,7 +420,7 @@ int pg_perturb_fill(const double* xc_normal, const double* xc_inter, const doubl
 
 /* ---------------- misc ---------------- */
 const char* pg_last_error_string(void);
-int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out */
+int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 4: epilogue splitk_cnt */
 
 #ifdef __cplusplus
 }

@@ -253,12 +253,22 @@ __device__ __forceinline__ void finish_tile(
 // (the staging images are free by now) and written out row-major with 16-B loads/stores,
 // instead of one 4-B store per lane and accumulator register. Needs N % 4 == 0 and 16-B
 // aligned C / ldc (and dact / bias when present).
+// sc1 (agent-scope) stores / loads of the split-K slabs combined inside the kernel
+// (MI355X_MICROARCH.md, inter-workgroup hand-offs: every store and load of the handed-off
+// bytes sc1, a counter add after each storing wave's vmcnt(0) wait, the last adder reads)
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+constexpr int kSc1 = 16;  // cache-policy bit SC1 of the buffer intrinsics
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
 template <int BM, int BN, int EPI>
 __device__ __forceinline__ void finish_tile_lds(
     const f32x16 (&acc)[BM / 64][BN / 64], float rs, bool do_rs, float* __restrict__ lds, int tid,
     int m0, int n0, int M, int N, float alpha, float beta, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias, float slope, const float* __restrict__ dact, int64_t lddact,
-    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum, int kz) {
+    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum, int kz,
+    bool sc1 = false) {
   constexpr bool SPLIT = EPI == EPI_SPLIT;
   constexpr int TM = BM / 64, TN = BN / 64;
   const int lane = tid & 63, wave = tid >> 6;
@@ -269,8 +279,15 @@ __device__ __forceinline__ void finish_tile_lds(
     if (tid < BM && m0 + tid < M) {
       float t = 0.f;
       for (int g = 0; g < kThreads / BM; ++g) t += lds[g * BM + tid];
-      if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = t;
-      else rowsum[m0 + tid] = t;
+      if constexpr (SPLIT) {
+        if (sc1)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, t), slab_rsrc(ws_rowsum + (int64_t)kz * M),
+                                                (m0 + tid) * 4, 0, kSc1);
+        else
+          ws_rowsum[(int64_t)kz * M + m0 + tid] = t;
+      } else {
+        rowsum[m0 + tid] = t;
+      }
     }
     __syncthreads();
   }
@@ -292,7 +309,12 @@ __device__ __forceinline__ void finish_tile_lds(
     if (gr >= M || gc >= N) continue;
     float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
     if constexpr (SPLIT) {
-      *reinterpret_cast<float4*>(ws + ((int64_t)kz * M + gr) * N + gc) = v;
+      if (sc1) {
+        const f32x4 x = {v.x, v.y, v.z, v.w};
+        __builtin_amdgcn_raw_buffer_store_b128(x, slab_rsrc(ws + (int64_t)kz * M * N), (gr * N + gc) * 4, 0, kSc1);
+      } else {
+        *reinterpret_cast<float4*>(ws + ((int64_t)kz * M + gr) * N + gc) = v;
+      }
     } else {
       float* cp = C + (int64_t)gr * ldc + gc;
       float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
@@ -576,13 +598,72 @@ __device__ __forceinline__ float img_rowsum(const float* __restrict__ As, int ti
   return s;
 }
 
+// The last-arriving workgroup of a split tile: C = alpha * sum_z slab_z (+ beta * C), the
+// slabs read with sc1 loads, 4 slices x (BM BN / 1024) float4 units in flight per thread;
+// the tile's row sums likewise (ws_rowsum != NULL on the column-0 tile).
+template <int BM, int BN>
+__device__ __forceinline__ void splitk_combine_tile(int tid, int m0, int n0, int M, int N, int S,
+                                                    float alpha, float beta, float* __restrict__ C,
+                                                    int64_t ldc, const float* __restrict__ ws,
+                                                    const float* __restrict__ ws_rowsum,
+                                                    float* __restrict__ rowsum) {
+  constexpr int UPT = BM * BN / 4 / kThreads;  // float4 units per thread
+  const __amdgpu_buffer_rsrc_t rw = slab_rsrc(ws);
+  int off[UPT];
+  bool ok[UPT];
+  f32x4 sum[UPT];
+#pragma unroll
+  for (int i = 0; i < UPT; ++i) {
+    const int u = i * kThreads + tid;
+    const int gr = m0 + u / (BN / 4), gc = n0 + (u % (BN / 4)) * 4;
+    ok[i] = gr < M && gc < N;
+    off[i] = ok[i] ? (gr * N + gc) * 4 : 0;
+    sum[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int slab = M * N * 4;  // bytes per slice (< 2^31: checked by the host)
+  for (int z0 = 0; z0 < S; z0 += 4) {
+    f32x4 v[4][UPT];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < UPT; ++i)
+        v[j][i] = (z0 + j < S) ? __builtin_amdgcn_raw_buffer_load_b128(rw, off[i] + (z0 + j) * slab, 0, kSc1)
+                               : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < UPT; ++i) sum[i] += v[j][i];
+  }
+#pragma unroll
+  for (int i = 0; i < UPT; ++i) {
+    if (!ok[i]) continue;
+    const int u = i * kThreads + tid;
+    float* cp = C + (int64_t)(m0 + u / (BN / 4)) * ldc + n0 + (u % (BN / 4)) * 4;
+    float o[4] = {alpha * sum[i].x, alpha * sum[i].y, alpha * sum[i].z, alpha * sum[i].w};
+    if (beta != 0.f) {
+      const float4 c4 = *reinterpret_cast<const float4*>(cp);
+      o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
+      o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
+    }
+    *reinterpret_cast<float4*>(cp) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  if (ws_rowsum && tid < BM && m0 + tid < M) {
+    const __amdgpu_buffer_rsrc_t rr = slab_rsrc(ws_rowsum);
+    float t = 0.f;
+    for (int z = 0; z < S; ++z)
+      t += __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rr, (z * M + m0 + tid) * 4, 0, kSc1));
+    rowsum[m0 + tid] = t;
+  }
+}
+
 template <int BM, int BN, bool TA, bool TB, int EPI>
 __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
     float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
     const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
-    float* __restrict__ ws, float* __restrict__ ws_rowsum, int vec_out, int n_split) {
+    float* __restrict__ ws, float* __restrict__ ws_rowsum, int vec_out, int n_split,
+    uint32_t* __restrict__ cnt) {
   constexpr bool AK = TA, BKM = !TB;
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int IA = BM * BK, IB = BN * BK;  // image sizes (floats)
@@ -710,6 +791,27 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     if (t == 1234.5f) C[tid] = t;
     return;
   }
+  if (EPI == EPI_SPLIT && cnt) {
+    // split-K combined here: slab stored sc1, the last of the tile's n_split workgroups to
+    // arrive (told by its counter add) sums the slabs in slice order 0, 1, ... (the same
+    // order whichever workgroup it is: deterministic) and resets the counter for the next call
+    finish_tile_lds<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
+                                 slope, dact, lddact, rowsum, ws, ws_rowsum, kz, true);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(lds);
+    if (tid == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = old == (uint32_t)(n_split - 1);
+      if (last) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    splitk_combine_tile<BM, BN>(tid, m0, n0, M, N, n_split, alpha, beta, C, ldc, ws, do_rs ? ws_rowsum : nullptr,
+                                rowsum);
+    return;
+  }
   if (vec_out)
     finish_tile_lds<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
                                  slope, dact, lddact, rowsum, ws, ws_rowsum, kz);
@@ -740,6 +842,7 @@ struct Args {
   float* ws;
   float* ws_rowsum;
   int vec_out;
+  uint32_t* cnt;  // split-K tile counters (in-kernel combine) or NULL
 };
 
 template <int BM, int BN, bool TA, bool TB, bool VA, bool VB>
@@ -768,7 +871,7 @@ int launch_dma(int epi, dim3 grid, hipStream_t st, const Args& a) {
   hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, EPI_>), dim3(grid.x * grid.z), dim3(kThreads), \
                      0, st, a.M, a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B,  \
                      a.ldb, a.beta, a.C, a.ldc, a.bias, a.slope, a.dact, a.lddact, a.rowsum,     \
-                     a.ws, a.ws_rowsum, a.vec_out, (int)grid.z)
+                     a.ws, a.ws_rowsum, a.vec_out, (int)grid.z, a.cnt)
   switch (epi) {
     case EPI_NONE: PG_L(EPI_NONE); break;
     case EPI_RELU: PG_L(EPI_RELU); break;
@@ -853,6 +956,10 @@ int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, by_k), 256));
 }
 
+int64_t pg_gemm_splitk_counters(int64_t M, int64_t N) {
+  return M > 0 && N > 0 ? ((M + 63) / 64) * ((N + 63) / 64) : 0;
+}
+
 size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k) {
   (void)K;
   if (split_k <= 1 || M <= 0 || N <= 0) return 0;
@@ -905,9 +1012,14 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
                        (split ? al16(wsf) : (al16(C) && (ldc % 4) == 0)) &&
                        (!ep->bias || al16(ep->bias)) &&
                        (!ep->dact || (al16(ep->dact) && (ep->lddact % 4) == 0));
+  // split-K partials combined inside the kernel when the caller gives tile counters, the
+  // 16-B slab path applies and every slab offset fits the buffer intrinsics' 32-bit range
+  const bool in_kernel = split && ep->splitk_cnt && vec_out && al16(C) && (ldc % 4) == 0 &&
+                         (int64_t)split_k * M * N * 4 < INT32_MAX && !getenv("PLAGNN_SPLITK_REDUCE");
   const Args a{(int)M, (int)N, (int)K, kps, tiles_n, tiles, alpha, A, lda, B, ldb, beta, C, ldc,
                ep->bias, ep->slope, ep->dact, ep->lddact, ep->rowsum, wsf,
-               split ? wsf + (int64_t)split_k * M * N : nullptr, vec_out ? 1 : 0};
+               split ? wsf + (int64_t)split_k * M * N : nullptr, vec_out ? 1 : 0,
+               in_kernel ? ep->splitk_cnt : nullptr};
   const bool ta = transa != 0, tb = transb != 0;
   const int epi = split ? EPI_SPLIT
                         : ep->dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
@@ -922,7 +1034,7 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   else
     rc = launch_trans<64, 64>(ta, tb, va, vb, epi, grid, st, a);
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_f32: dispatch failed");
-  if (split) {
+  if (split && !in_kernel) {
     const int64_t n = M * N + (ep->rowsum ? M : 0);
     // threads per output: enough slice groups that each thread sums <= ~8 slices
     const int G = splitk_groups(split_k);

@@ -57,6 +57,7 @@ class PgGemmEpilogue(ctypes.Structure):
         ("dact", ctypes.c_void_p),
         ("lddact", ctypes.c_int64),
         ("rowsum", ctypes.c_void_p),
+        ("splitk_cnt", ctypes.c_void_p),
     ]
 
 
@@ -82,6 +83,7 @@ SIGNATURES = {
     "pg_spmm_max_bwd": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                              _vp, _sz, _vp]),
     "pg_spmm_group_tiles": (_i64, [_i64]),
+    "pg_gemm_splitk_counters": (_i64, [_i64, _i64]),
     "pg_spmm_max_fwd_grouped": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pg_spmm_max_fwd_grouped_bf16": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz,
                                           _vp]),
@@ -176,7 +178,8 @@ def stream_handle(device: torch.device):
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def epilogue(bias=None, act: int = PG_ACT_NONE, slope: float = 0.01, dact=None, rowsum=None):
+def epilogue(bias=None, act: int = PG_ACT_NONE, slope: float = 0.01, dact=None, rowsum=None,
+             splitk_cnt=None):
     """pg_gemm_epilogue_t from tensors (or None)."""
     e = PgGemmEpilogue()
     e.bias = ptr(bias)
@@ -185,6 +188,7 @@ def epilogue(bias=None, act: int = PG_ACT_NONE, slope: float = 0.01, dact=None, 
     e.dact = ptr(dact)
     e.lddact = dact.stride(0) if dact is not None else 0
     e.rowsum = ptr(rowsum)
+    e.splitk_cnt = ptr(splitk_cnt)
     return e
 
 

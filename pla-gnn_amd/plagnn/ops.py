@@ -235,8 +235,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
          out: Optional[torch.Tensor] = None, alpha: float = 1.0, beta: float = 0.0,
          bias: Optional[torch.Tensor] = None, act: int = _lib.PG_ACT_NONE,
          slope: float = LEAKY_SLOPE, split_k: Optional[int] = None,
-         dact: Optional[torch.Tensor] = None, rowsum: Optional[torch.Tensor] = None
-         ) -> torch.Tensor:
+         dact: Optional[torch.Tensor] = None, rowsum: Optional[torch.Tensor] = None,
+         splitk_cnt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = alpha*op(A)@op(B) + beta*C (+bias, act) on the fp32 MFMA kernel (GPU) or
     torch-CPU (CPU device). With `dact` (an activation output) the result is instead
     multiplied by act'(dact): the fused activation backward. With `rowsum`, also
@@ -274,7 +274,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
                         or beta not in (0.0, 1.0)) else _split_k(M, N, K)
     ws_n = _lib.lib().pg_gemm_f32_workspace(M, N, K, split_k)
     ws = _workspace(ws_n, A.device)
-    ep = _lib.epilogue(bias, act, slope, dact, rowsum)
+    ep = _lib.epilogue(bias, act, slope, dact, rowsum, splitk_cnt)
     call("pg_gemm_f32", int(transa), int(transb), M, N, K, alpha, ptr(A), _ld(A), ptr(B), _ld(B),
          beta, ptr(out), _ld(out), ep, split_k, ptr(ws), ws_n, _stream(A))
     return out

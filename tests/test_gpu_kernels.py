@@ -406,3 +406,37 @@ def test_spmm_max_grouped_empty_rows():
     dx_g = ops.spmm_max_backward_grouped(dg, lists, dZ, mask=P)
     assert torch.equal(dx_g, ops.spmm_max_backward(dg, arg, dZ, mask=P, fwd_out=out_r))
     assert torch.all(dx_g[n // 2:] == 0)
+
+
+@pytest.mark.parametrize("M,N,K,ta", [(256, 1024, 24041, True), (100, 256, 24041, True),
+                                      (97, 260, 9000, False), (512, 512, 6000, True)])
+def test_gemm_split_k_in_kernel_combine(M, N, K, ta):
+    """Split-K partial slabs summed by the last workgroup of each tile (tile counters) vs the
+    separate reduce launch: both deterministic, equal to 1e-6 relative, within fp32 bounds of
+    a float64 reference; the counters are left zero, so a second call (a graph replay) is
+    again correct; the row sums (bias gradients) likewise."""
+    from plagnn import _lib, ops
+
+    gen = torch.Generator().manual_seed(M + N)
+    A = (torch.randn(K, M, generator=gen) if ta else torch.randn(M, K, generator=gen)).to(DEV)
+    B = torch.randn(K, N, generator=gen).to(DEV)
+    sk = ops._split_k(M, N, K)
+    assert sk > 1
+    cnt = torch.zeros(int(_lib.lib().pg_gemm_splitk_counters(M, N)), dtype=torch.int32, device=DEV)
+    rs_a, rs_b = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    c_ref = ops.gemm(A, B, transa=ta, split_k=sk, rowsum=rs_a)
+    c1 = ops.gemm(A, B, transa=ta, split_k=sk, rowsum=rs_b, splitk_cnt=cnt)
+    assert torch.all(cnt == 0)
+    c2 = ops.gemm(A, B, transa=ta, split_k=sk, splitk_cnt=cnt)
+    assert torch.equal(c1, c2) and torch.all(cnt == 0)
+    torch.testing.assert_close(c1, c_ref, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(rs_b, rs_a, rtol=1e-5, atol=1e-4)
+    a64 = (A.t() if ta else A).double()
+    ref = a64 @ B.double()
+    err = (c1.double() - ref).abs().max().item()
+    assert err <= 2e-6 * (a64.abs() @ B.double().abs()).max().item()
+    # beta = 1 accumulates onto C
+    C = torch.randn(M, N, generator=gen).to(DEV)
+    C0 = C.clone()
+    ops.gemm(A, B, transa=ta, out=C, beta=1.0, split_k=sk, splitk_cnt=cnt)
+    torch.testing.assert_close(C, C0 + c1, rtol=1e-5, atol=1e-4)
