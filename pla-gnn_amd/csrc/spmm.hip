@@ -146,9 +146,12 @@ __device__ __forceinline__ float bcastf(float v, int j) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
 }
 
+#ifndef PG_EDGE_U
+#define PG_EDGE_U 8  // edges in flight per wave for feature tiles of <= 8 values per lane
+#endif
 template <int W, int NC>
 struct EdgeU {
-  static constexpr int value = (NC * W <= 8) ? 8 : 4;
+  static constexpr int value = (NC * W <= 8) ? PG_EDGE_U : 4;
 };
 
 // ---- max forward ---------------------------------------------------------------------
