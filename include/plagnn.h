@@ -342,6 +342,15 @@ int pg_spmm_max_bwd_grouped_bf16(const pg_csr_t* g, const pg_csr_t* gt, const ui
 int pg_cast_f32_bf16(const float* src, const int32_t* map, int64_t n, void* dst, pg_stream_t stream);
 int pg_cast_bf16_f32(const void* src, int64_t n, float* dst, pg_stream_t stream);
 
+/* The PCA front end (code/data_preprocess.py:475-487 `pca`, scikit-learn 1.1.1
+ * PCA(n_components, random_state=42) on the ECC / GCN*PPI matrices, 528-546): its randomized
+ * SVD's products with the centred matrix, float64, as a CSR x dense SpMM with a rank-1 term:
+ *   Y[r, :] = sum_{j in row r} val[j] X[col[j], :] - (u ? u[r] : 1) * v[:]   (v NULL: no term)
+ * k <= 512 columns. Sum in CSR order (deterministic). */
+int pg_csr_spmm_f64(int64_t n_rows, const int32_t* ptr, const int32_t* col, const double* val,
+                    const double* X, int64_t ldx, int64_t k, const double* u, const double* v,
+                    double* Y, int64_t ldy, pg_stream_t stream);
+
 /* ---------------- host (_cpu): the same operations on host pointers ---------------- */
 int pg_spmm_max_fwd_cpu(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
                         int64_t ldo, void* argpos, int64_t lda, int arg_kind);

@@ -414,3 +414,43 @@ class PerturbStream:
         if m < 0:
             raise MemoryError("oracle_perturb_rows")
         return rr[:m], cc[:m], vv[:m]
+
+
+# ---------------------------------------------------------------- PCA front end
+def pca_randomized(mat, n_components: int, random_state: int = 42, n_oversamples: int = 10) -> np.ndarray:
+    """CPU restatement of ``pca(mat, components)`` (code/data_preprocess.py:475-487), i.e.
+    scikit-learn 1.1.1 (README.md:30) ``PCA(n_components, random_state=42).fit_transform``
+    on the path its svd_solver='auto' takes for the reference's matrices (N = 24 041 > 500,
+    250 < 0.8 N): ``_fit_truncated`` -> ``randomized_svd(X - mean, n_components,
+    n_oversamples=10, n_iter='auto' (7 when n_components < 0.1 min(shape), else 4),
+    power_iteration_normalizer='auto' (LU for n_iter > 2), flip_sign=True,
+    random_state=RandomState(42))``: Gaussian test matrix ``normal(size=(n_features,
+    n_components + 10))``, LU-normalised power iterations (``scipy.linalg.lu(.., permute_l=True)``),
+    economic QR, SVD of ``Q^T X``, ``U = Q Uhat``, ``svd_flip`` u-based (1.1.1's rule: each
+    column of U made positive at its largest |entry|), returned as ``U[:, :k] * S[:k]``.
+    Pinned by tests/golden/pca.npz (the reference's own pca() under scikit-learn 1.7.2, the
+    same algorithm with v-based signs)."""
+    import scipy.linalg as sla
+    import scipy.sparse as sp
+
+    X = mat.toarray() if sp.issparse(mat) else np.asarray(mat)
+    X = np.array(X, dtype=np.float64)
+    n_samples, n_features = X.shape
+    if not (max(X.shape) > 500 and 1 <= n_components < 0.8 * min(X.shape)):
+        raise ValueError("pca_randomized: sklearn 1.1.1 would take the full-SVD path here")
+    if n_samples < n_features:
+        raise ValueError("pca_randomized: transposed randomized SVD not restated")
+    X -= X.mean(axis=0)
+    rs = np.random.RandomState(random_state)
+    size = n_components + n_oversamples
+    n_iter = 7 if n_components < 0.1 * min(X.shape) else 4
+    Q = rs.normal(size=(n_features, size))
+    for _ in range(n_iter):
+        Q, _ = sla.lu(X @ Q, permute_l=True)
+        Q, _ = sla.lu(X.T @ Q, permute_l=True)
+    Q, _ = sla.qr(X @ Q, mode="economic")
+    Uhat, s, _ = sla.svd(Q.T @ X, full_matrices=False)
+    U = Q @ Uhat
+    idx = np.argmax(np.abs(U), axis=0)
+    U *= np.sign(U[idx, np.arange(U.shape[1])])
+    return U[:, :n_components] * s[:n_components]

@@ -84,6 +84,7 @@ SIGNATURES = {
                              _vp, _sz, _vp]),
     "pg_spmm_group_tiles": (_i64, [_i64]),
     "pg_gemm_splitk_counters": (_i64, [_i64, _i64]),
+    "pg_csr_spmm_f64": (_i, [_i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),
     "pg_spmm_max_fwd_grouped": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pg_spmm_max_fwd_grouped_bf16": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz,
                                           _vp]),

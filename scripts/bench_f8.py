@@ -141,6 +141,33 @@ def main():
                                                  f"rows x all columns, scaled to {n} rows"},
                       "bit_exact_vs_oracle_sample_rows": exact}))
 
+    # 8f-4b: the PCA front end on the S0 ECC matrix (data_preprocess.py:528-530: pca(ecc, 250))
+    from plagnn.pca import pca as pca_gpu
+
+    eccm = got_ecc = ecc.edge_clustering_coefficients(adj)
+    pca_gpu(eccm, 250)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    feat = pca_gpu(eccm, 250)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    # CPU: the reference densifies the matrix and runs 2 n_iter + 2 = 16 dense products
+    # X_c @ Q (24 041 x 24 041 x 260); time one with numpy (OpenBLAS threads as set) x 16
+    dense = got_ecc.toarray()
+    dense -= dense.mean(axis=0)
+    q = np.random.RandomState(42).normal(size=(n, 260))
+    t0 = time.perf_counter()
+    dense @ q
+    one = time.perf_counter() - t0
+    del dense
+    print(json.dumps({"row": "8f-4b PCA front end (pca(ecc, 250), scikit-learn 1.1.1 randomized path)",
+                      "n": n, "nnz": int(eccm.nnz), "components": 250, "gpu_call_ms": round(wall * 1e3, 1),
+                      "out_shape": list(feat.shape),
+                      "cpu_baseline": {"ms": round(16 * one * 1e3, 1), "cores": int(os.environ.get("OMP_NUM_THREADS", "0") or 0),
+                                       "kind": "port",
+                                       "sample": "one dense X_c @ Q product (numpy, 24041 x 24041 x 260) timed, x 16 "
+                                                 "products of the randomized SVD (LU / QR / SVD not counted)"}}))
+
 
 if __name__ == "__main__":
     main()

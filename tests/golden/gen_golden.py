@@ -151,10 +151,41 @@ def gen_perturb():
     np.savez_compressed(os.path.join(HERE, "perturb.npz"), **out)
 
 
+def gen_pca():
+    """The reference's own pca() (code/data_preprocess.py:475-487) on an ECC matrix made by its
+    own edge_clustering_coefficients (175-214), as at 528-530. scikit-learn here is 1.7.2
+    (the reference pins 1.1.1): the randomized SVD it runs is the same algorithm (Gaussian
+    test matrix from RandomState(42), 7 LU-normalised power iterations, QR, SVD of the
+    projection), but 1.7.2's PCA flips signs by V (u_based_decision=False) where 1.1.1 flips
+    by U; the fixture therefore pins the columns up to sign, and the stored u-based sign is
+    1.1.1's rule applied to these columns."""
+    from scipy.sparse import coo_matrix
+
+    sys.path.insert(0, REF)
+    import data_preprocess as dp  # noqa: E402
+
+    rng = np.random.default_rng(2023)
+    n, nc = 800, 30
+    a = np.triu(rng.random((n, n)) < 0.02, 1)
+    a = a | a.T
+    r, c = np.nonzero(a)
+    ppi = coo_matrix((np.ones(len(r), np.int64), (r, c)), shape=(n, n))
+    ecc = dp.edge_clustering_coefficients(ppi).tocoo()
+    feat = dp.pca(ecc.toarray(), nc)
+    np.savez_compressed(os.path.join(HERE, "pca.npz"), n=np.int64(n), nc=np.int64(nc), row=ecc.row,
+                        col=ecc.col, val=ecc.data.astype(np.float64), out=feat)
+
+
 if __name__ == "__main__":
-    ns = _train_functions()
-    gen_loss(ns)
-    gen_eval(ns)
-    gen_ecc()
-    gen_perturb()
+    only = sys.argv[1:]
+    if not only or "train" in only:
+        ns = _train_functions()
+        gen_loss(ns)
+        gen_eval(ns)
+    if not only or "ecc" in only:
+        gen_ecc()
+    if not only or "perturb" in only:
+        gen_perturb()
+    if not only or "pca" in only:
+        gen_pca()
     print("golden fixtures written to", HERE)

@@ -178,3 +178,32 @@ def test_perturb_stream_oracle_matches_reference_golden(oracle_mod, name):
     np.testing.assert_array_equal(r, ref.row)
     np.testing.assert_array_equal(c, ref.col)
     np.testing.assert_array_equal(v, ref.data)
+
+
+def _align_cols(a, g):
+    """a's columns sign-matched to g's (scikit-learn 1.7.2 flips by V, 1.1.1 by U)."""
+    s = np.sign(np.sum(a * g, axis=0))
+    s[s == 0] = 1
+    return a * s
+
+
+def test_pca_oracle_matches_reference_golden(oracle_mod):
+    """The randomized-PCA restatement (scikit-learn 1.1.1's algorithm) against the reference's
+    own pca() (code/data_preprocess.py:475-487) on its own ECC matrix (tests/golden/pca.npz):
+    every column within 1e-9 of its magnitude up to sign; the restatement's signs follow
+    1.1.1's u-based svd_flip (largest |entry| of each column positive)."""
+    import os
+
+    from scipy.sparse import coo_matrix
+
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "pca.npz"))
+    n, nc = int(z["n"]), int(z["nc"])
+    m = coo_matrix((z["val"], (z["row"], z["col"])), shape=(n, n))
+    got = oracle_mod.pca_randomized(m, nc)
+    gold = z["out"]
+    assert got.shape == gold.shape == (n, nc)
+    a = _align_cols(got, gold)
+    scale = np.abs(gold).max(axis=0)
+    assert np.all(np.abs(a - gold).max(axis=0) <= 1e-9 * scale)
+    idx = np.abs(got).argmax(axis=0)
+    assert np.all(got[idx, np.arange(nc)] > 0)
