@@ -41,6 +41,8 @@
  *                           the ECC feature / edge-weight front end
  *   pg_loc_correction,   <- protein_loc_correction / performances_record
  *   pg_loc_performance      (code/train.py:19-86), the per-epoch eval
+ *   pg_csr_spmm_f64      <- the centred products of pca() (code/data_preprocess.py:475-487,
+ *                           scikit-learn 1.1.1 randomized PCA), the PCA front end
  *   pg_perturb_*         <- construct_gcn_matrix's np.corrcoef (code/data_preprocess.py:
  *                           165-170) + modify_network_topology (217-257), fused: the
  *                           N x N correlation / difference matrices are never stored
