@@ -71,7 +71,8 @@ __device__ unsigned long long pg_gemm_kphase[64][4];   // start, prologue done, 
 #endif
 #ifndef PG_GEMM_XP
 #define PG_GEMM_XP 0  // experiment only (wrong results): 1 no in-loop DMA, 2 no MFMA, 4 no epilogue;
-                      // 8 / 16: stagger co-resident workgroups by 1024 / 512 cycles per slot
+                      // 8 / 16: stagger co-resident workgroups by 1024 / 512 cycles per slot;
+                      // 32: every K tile's DMA issued twice (issue cost vs latency)
 #endif
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
@@ -731,7 +732,10 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     for (int t = 0; t < nk; ++t) {
       const int cur = t & 1;
       const bool more = t + 1 < nk;
-      if (more && !(PG_GEMM_XP & 1)) issue(t + 1, cur ^ 1);
+      if (more && !(PG_GEMM_XP & 1)) {
+        issue(t + 1, cur ^ 1);
+        if constexpr ((PG_GEMM_XP & 32) != 0) issue(t + 1, cur ^ 1);  // experiment: DMA issued twice
+      }
       const float* As = lds + cur * IA;
       const float* Bs = lds + 2 * IA + cur * IB;
       if (do_rs) rs += img_rowsum<BM, AK>(As, tid);
