@@ -911,7 +911,7 @@ int launch_trans(bool ta, bool tb, bool va, bool vb, int epi, dim3 grid, hipStre
 // Tile choice (measured on the PLA-GNN step shapes, scripts/gemm_bench.py): split-K
 // products (weight gradients) 64 x 64; outputs wider than 512 columns 128 x 128 when that
 // still gives >= 3 workgroups per CU, else 64 x 128; 129..512 columns with short K
-// 128 x 64 (again if >= 768 tiles); everything else 64 x 64 (5 workgroups per CU: long-K
+// (K <= 1024) 128 x 64 (if >= 720 tiles: ~3 workgroups per CU); everything else 64 x 64 (5 workgroups per CU: long-K
 // and small products balance best on the finest tile).
 inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& bn) {
   // tuning knob PLAGNN_GEMM_TILE = "BMxBN" (64|128 each) forces a tile
@@ -933,7 +933,7 @@ inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& 
   if (N > 512) {
     bn = 128;
     bm = tiles(128, 128) >= 3 * 256 ? 128 : 64;
-  } else if (N > 128 && K < 1024 && tiles(128, 64) >= 3 * 256) {
+  } else if (N > 128 && K <= 1024 && tiles(128, 64) >= 3 * 256 - 48) {
     bm = 128;
   }
 }
