@@ -185,10 +185,25 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
     const int32_t* __restrict__ eslot, const float* __restrict__ ew,
     const int4* __restrict__ items, int n_items, const T* __restrict__ X, int64_t ldx, int F,
     T* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
-    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, GroupOut go) {
+    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, GroupOut go,
+    int n_ftiles = 1, int ftile = 0) {
   constexpr int U = EdgeU<W, NC>::value;
   __shared__ int ghist[GROUP ? kWavesPerBlock * (kPackWaveMax + 4) : 1];
-  const int it = blockIdx.x * kWavesPerBlock + wave_id_uniform();
+  // n_ftiles > 1: all feature tiles of F in one launch, block b -> (item block b / n_ftiles,
+  // tile b % n_ftiles), so every tile's longest items start first
+  int bx = blockIdx.x;
+  if (n_ftiles > 1) {
+    const int t = bx % n_ftiles;
+    bx /= n_ftiles;
+    const int f0 = t * ftile;
+    X += f0;
+    out += f0;
+    arg += f0;
+    if (ws_val) ws_val += f0;
+    if (ws_arg) ws_arg += f0;
+    F = min(ftile, F - f0);
+  }
+  const int it = bx * kWavesPerBlock + wave_id_uniform();
   if (it >= n_items) return;
   const int4 item = items[it];
   const int row = item.x, k0 = item.y, k1 = item.z, slot = item.w;
@@ -1206,16 +1221,20 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
   if (!tp.vec) tp.tile = kFTileScalar;
   const bool has_w = g->ew != nullptr;
   const int blocks = grid_for(g->n_items);
-  for (int64_t f0 = 0; f0 < F; f0 += tp.tile) {
-    const int Ft = (int)std::min<int64_t>(tp.tile, F - f0);
+  // every feature tile in one launch (blocks interleaved over the tiles), one merge launch
+  // over the whole F
+  const int n_ft = (int)((F + tp.tile - 1) / tp.tile);
+  {
+    const int64_t f0 = 0;
+    const int Ft = (int)std::min<int64_t>(tp.tile, F);
     auto go = [&](auto nc_c, auto w_c, auto hw_c) -> int {
       constexpr int NC = decltype(nc_c)::value;
       constexpr int W = decltype(w_c)::value;
       constexpr bool HW = decltype(hw_c)::value;
-      hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T>), dim3(blocks), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T>), dim3((unsigned)blocks * n_ft), dim3(kBlock), 0, st,
                          g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
-                         X + f0, ldx, Ft, out + f0, ldo, arg + f0, lda,
-                         ws_val ? ws_val + f0 : nullptr, ws_arg ? ws_arg + f0 : nullptr, ldw, GroupOut{});
+                         X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, GroupOut{},
+                         n_ft, (int)tp.tile);
       return PG_OK;
     };
     int rc;
@@ -1231,7 +1250,7 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
     if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_max_fwd: unsupported feature tile");
     if (g->n_merges > 0) {
       hipLaunchKernelGGL((max_merge_kernel<A, T>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
-                         (const int4*)g->merges, (int)g->n_merges, Ft, ws_val + f0, ws_arg + f0,
+                         (const int4*)g->merges, (int)g->n_merges, (int)F, ws_val + f0, ws_arg + f0,
                          ldw, out + f0, ldo, arg + f0, lda);
     }
   }
