@@ -298,6 +298,26 @@ typedef struct pg_gemm_epilogue {
 int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K);
 size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k);
 int64_t pg_gemm_splitk_counters(int64_t M, int64_t N);
+/* Deferred split-K: pg_gemm_f32_partials runs the split product (C = op(A) op(B), rowsum
+ * allowed, nothing else) and leaves the partial slabs in ws (layout of pg_gemm_f32:
+ * split_used slabs of M x N, then split_used row-sum slices of M); *split_used = the slice
+ * count actually run. pg_gemm_splitk_reduce_batch then combines up to 16 such products in
+ * one launch, C = alpha * sum_z slab_z (+ beta * C, beta 0 or 1), each exactly as
+ * pg_gemm_f32's own combine (bitwise the same result). The ws regions must stay untouched
+ * between the two calls. */
+typedef struct pg_splitk_job {
+  const float* ws;  /* the partials' workspace */
+  int split_k;      /* *split_used of the partials call */
+  int64_t M, N;
+  float alpha, beta;
+  float* C;
+  int64_t ldc;
+  float* rowsum;    /* or NULL (must match the partials call's ep->rowsum != NULL) */
+} pg_splitk_job_t;
+int pg_gemm_f32_partials(int transa, int transb, int64_t M, int64_t N, int64_t K, const float* A,
+                         int64_t lda, const float* B, int64_t ldb, const pg_gemm_epilogue_t* ep,
+                         int split_k, void* ws, size_t ws_bytes, int* split_used, pg_stream_t stream);
+int pg_gemm_splitk_reduce_batch(const pg_splitk_job_t* jobs, int n_jobs, pg_stream_t stream);
 int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
                 int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,

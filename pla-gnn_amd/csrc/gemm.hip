@@ -970,10 +970,16 @@ size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k) {
   return (size_t)split_k * (size_t)M * (size_t)(N + 1) * 4;
 }
 
-int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
-                const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
-                int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
-                size_t ws_bytes, pg_stream_t stream) {
+}  // extern "C"
+
+namespace {
+
+// defer: split-K partial slabs (and row-sum slices) are left in ws for a later
+// pg_gemm_splitk_reduce_batch; *split_used = the slice count actually run.
+int gemm_f32_impl(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
+                  const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
+                  int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
+                  size_t ws_bytes, pg_stream_t stream, bool defer, int* split_used) {
   const pg_gemm_epilogue_t none{nullptr, PG_ACT_NONE, 0.f, nullptr, 0, nullptr};
   if (!ep) ep = &none;
   const int act = ep->act;
@@ -1004,6 +1010,8 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
     if (split_k < 1) split_k = 1;
   }
   const bool split = split_k > 1;
+  if (split_used) *split_used = split_k;
+  if (defer && !split) return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32_partials: needs split_k > 1");
   int bm, bn;
   pick_tile(M, N, K, split_k, bm, bn);
   const int tiles_n = (int)((N + bn - 1) / bn);
@@ -1018,7 +1026,7 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
                        (!ep->dact || (al16(ep->dact) && (ep->lddact % 4) == 0));
   // split-K partials combined inside the kernel when the caller gives tile counters, the
   // 16-B slab path applies and every slab offset fits the buffer intrinsics' 32-bit range
-  const bool in_kernel = split && ep->splitk_cnt && vec_out && al16(C) && (ldc % 4) == 0 &&
+  const bool in_kernel = split && !defer && ep->splitk_cnt && vec_out && al16(C) && (ldc % 4) == 0 &&
                          (int64_t)split_k * M * N * 4 < INT32_MAX && !getenv("PLAGNN_SPLITK_REDUCE");
   const Args a{(int)M, (int)N, (int)K, kps, tiles_n, tiles, alpha, A, lda, B, ldb, beta, C, ldc,
                ep->bias, ep->slope, ep->dact, ep->lddact, ep->rowsum, wsf,
@@ -1038,7 +1046,7 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   else
     rc = launch_trans<64, 64>(ta, tb, va, vb, epi, grid, st, a);
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_f32: dispatch failed");
-  if (split && !in_kernel) {
+  if (split && !in_kernel && !defer) {
     const int64_t n = M * N + (ep->rowsum ? M : 0);
     // threads per output: enough slice groups that each thread sums <= ~8 slices
     const int G = splitk_groups(split_k);
@@ -1056,6 +1064,120 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess)
     return pg::set_error((int)e, "pg_gemm_f32: launch failed: %s", hipGetErrorString(e));
+  return pg::ok();
+}
+
+// Several split-K combines in one launch: block ranges per job, each job reduced exactly as
+// splitk_reduce_kernel<G> does (same G, same order: bitwise the same result).
+constexpr int kMaxBatch = 16;
+struct BatchArgs {
+  pg_splitk_job_t job[kMaxBatch];
+  int G[kMaxBatch];
+  int first_block[kMaxBatch + 1];
+  int n;
+};
+
+template <int G>
+__device__ __forceinline__ void reduce_block(const pg_splitk_job_t& j, int blk, int nblk) {
+  constexpr int OPB = 256 / G;
+  __shared__ float part[256];
+  const int M = (int)j.M, N = (int)j.N, S = j.split_k;
+  const float* ws = j.ws;
+  const float* ws_rowsum = ws + (int64_t)S * M * N;
+  const int64_t n = (int64_t)M * N;
+  const int64_t total = n + (j.rowsum ? M : 0);
+  const int ol = threadIdx.x % OPB, g = threadIdx.x / OPB;
+  const int z0 = (int)((int64_t)S * g / G), z1 = (int)((int64_t)S * (g + 1) / G);
+  for (int64_t base = (int64_t)blk * OPB; base < total; base += (int64_t)nblk * OPB) {
+    const int64_t i = base + ol;
+    float s = 0.f;
+    if (i < total) {
+      if (i < n) {
+        for (int z = z0; z < z1; ++z) s += ws[(int64_t)z * n + i];
+      } else {
+        for (int z = z0; z < z1; ++z) s += ws_rowsum[(int64_t)z * M + (i - n)];
+      }
+    }
+    if constexpr (G > 1) {
+      part[threadIdx.x] = s;
+      __syncthreads();
+      if (g == 0) {
+#pragma unroll
+        for (int q = 1; q < G; ++q) s += part[q * OPB + ol];
+      }
+      __syncthreads();
+    }
+    if (g == 0 && i < total) {
+      if (i >= n) {
+        j.rowsum[i - n] = s;
+      } else {
+        const int64_t r = i / N;
+        const int c = (int)(i - r * N);
+        float v = j.alpha * s;
+        if (j.beta != 0.f) v = v + j.beta * j.C[r * j.ldc + c];
+        j.C[r * j.ldc + c] = v;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_batch_kernel(BatchArgs a) {
+  int k = 0;
+  while (k + 1 < a.n && (int)blockIdx.x >= a.first_block[k + 1]) ++k;
+  const int blk = blockIdx.x - a.first_block[k];
+  const int nblk = a.first_block[k + 1] - a.first_block[k];
+  switch (a.G[k]) {
+    case 1: reduce_block<1>(a.job[k], blk, nblk); break;
+    case 4: reduce_block<4>(a.job[k], blk, nblk); break;
+    default: reduce_block<16>(a.job[k], blk, nblk); break;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
+                const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
+                int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
+                size_t ws_bytes, pg_stream_t stream) {
+  return gemm_f32_impl(transa, transb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, ep, split_k, ws,
+                       ws_bytes, stream, false, nullptr);
+}
+
+int pg_gemm_f32_partials(int transa, int transb, int64_t M, int64_t N, int64_t K, const float* A,
+                         int64_t lda, const float* B, int64_t ldb, const pg_gemm_epilogue_t* ep,
+                         int split_k, void* ws, size_t ws_bytes, int* split_used, pg_stream_t stream) {
+  if (ep && (ep->bias || ep->act != PG_ACT_NONE || ep->dact))
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32_partials: the epilogue may only carry rowsum");
+  return gemm_f32_impl(transa, transb, M, N, K, 1.f, A, lda, B, ldb, 0.f, nullptr, N, ep, split_k, ws,
+                       ws_bytes, stream, true, split_used);
+}
+
+int pg_gemm_splitk_reduce_batch(const pg_splitk_job_t* jobs, int n_jobs, pg_stream_t stream) {
+  if (n_jobs < 0 || n_jobs > kMaxBatch || (n_jobs > 0 && !jobs))
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_splitk_reduce_batch: 0..%d jobs", kMaxBatch);
+  if (n_jobs == 0) return pg::ok();
+  BatchArgs a{};
+  a.n = n_jobs;
+  int blocks = 0;
+  for (int k = 0; k < n_jobs; ++k) {
+    const pg_splitk_job_t& j = jobs[k];
+    if (j.split_k < 1 || j.M <= 0 || j.N <= 0 || !j.ws || !j.C || j.ldc < j.N ||
+        (j.beta != 0.f && j.beta != 1.f))
+      return pg::set_error(PG_ERR_INVALID, "pg_gemm_splitk_reduce_batch: bad job %d", k);
+    a.job[k] = j;
+    a.G[k] = splitk_groups(j.split_k);
+    a.first_block[k] = blocks;
+    const int64_t n = j.M * j.N + (j.rowsum ? j.M : 0);
+    const int opb = 256 / a.G[k];
+    blocks += (int)std::min<int64_t>(8192, (n + opb - 1) / opb);
+  }
+  a.first_block[n_jobs] = blocks;
+  hipLaunchKernelGGL(splitk_reduce_batch_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return pg::set_error((int)e, "pg_gemm_splitk_reduce_batch: launch failed: %s", hipGetErrorString(e));
   return pg::ok();
 }
 

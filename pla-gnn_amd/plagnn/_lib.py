@@ -69,6 +69,22 @@ _d = ctypes.c_double
 _sz = ctypes.c_size_t
 _vp = ctypes.c_void_p
 _csr = ctypes.POINTER(PgCsr)
+class PgSplitkJob(ctypes.Structure):
+    """pg_splitk_job_t (include/plagnn.h)."""
+
+    _fields_ = [
+        ("ws", ctypes.c_void_p),
+        ("split_k", ctypes.c_int),
+        ("M", ctypes.c_int64),
+        ("N", ctypes.c_int64),
+        ("alpha", ctypes.c_float),
+        ("beta", ctypes.c_float),
+        ("C", ctypes.c_void_p),
+        ("ldc", ctypes.c_int64),
+        ("rowsum", ctypes.c_void_p),
+    ]
+
+
 _ep = ctypes.POINTER(PgGemmEpilogue)
 
 # name -> (restype, argtypes); every symbol of include/plagnn.h
@@ -84,6 +100,9 @@ SIGNATURES = {
                              _vp, _sz, _vp]),
     "pg_spmm_group_tiles": (_i64, [_i64]),
     "pg_gemm_splitk_counters": (_i64, [_i64, _i64]),
+    "pg_gemm_f32_partials": (_i, [_i, _i, _i64, _i64, _i64, _vp, _i64, _vp, _i64, ctypes.POINTER(PgGemmEpilogue),
+                                  _i, _vp, _sz, ctypes.POINTER(ctypes.c_int), _vp]),
+    "pg_gemm_splitk_reduce_batch": (_i, [ctypes.POINTER(PgSplitkJob), _i, _vp]),
     "pg_csr_spmm_f64": (_i, [_i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),
     "pg_spmm_max_fwd_grouped": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pg_spmm_max_fwd_grouped_bf16": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz,

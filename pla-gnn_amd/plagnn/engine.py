@@ -25,6 +25,7 @@ stay exactly zero through forward, backward and Adam):
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import os
 from collections import defaultdict
 from typing import Dict, List, Optional, Sequence
@@ -198,6 +199,11 @@ class TrainEngine:
             need = max(need, L.pg_spmm_max_bwd_grouped_workspace(self.dg.bwd.struct(None), Fi))
         self._gemm_plans = {}
         self._splitk_cnt: Dict[str, torch.Tensor] = {}
+        # weight gradients' split-K combines deferred to one batched launch per step
+        # (PLAGNN_SPLITK_BATCH=0: one reduce launch per product)
+        self._slabs: Dict[str, torch.Tensor] = {}
+        self._jobs: list = []
+        self.defer_splitk = os.environ.get("PLAGNN_SPLITK_BATCH", "1") != "0"
         for (M_, N_, K_) in self._wgrad_shapes():
             sk = ops._split_k(M_, N_, K_)
             self._gemm_plans[(M_, N_, K_)] = sk
@@ -334,12 +340,42 @@ class TrainEngine:
         K = A.shape[0] if transa else A.shape[1]
         N = B.shape[0] if transb else B.shape[1]
         sk = self._gemm_plans.get((M, N, K), 1) if (bias is None and act == NONE and dact is None) else 1
+        if sk > 1 and self.defer_splitk and ws is None:
+            self._gemm_partials(A, B, C, transa, transb, beta, rowsum, tag, M, N, K, sk)
+            return
         cnt = self._splitk_counters(tag, M, N) if sk > 1 else None
         ep = _lib.epilogue(bias, act, LEAKY_SLOPE, dact, rowsum, cnt)
         ws = self.ws if ws is None else ws
         with self._t(tag, 2.0 * M * N * K):
             call("pg_gemm_f32", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
                  B.stride(0), beta, ptr(C), C.stride(0), ep, sk, ptr(ws), ws.numel(), self._s())
+
+    def _gemm_partials(self, A, B, C, transa, transb, beta, rowsum, tag, M, N, K, sk) -> None:
+        """A split-K weight gradient whose combine is deferred: the partial slabs go to this
+        launch site's own workspace and one pg_gemm_splitk_reduce_batch at the end of the
+        backward combines every weight gradient of the step (_reduce_deferred)."""
+        slab = self._slabs.get(tag)
+        if slab is None:
+            slab = torch.empty(int(_lib.lib().pg_gemm_f32_workspace(M, N, K, sk)), dtype=torch.uint8,
+                               device=self.device)
+            self._slabs[tag] = slab
+        used = ctypes.c_int(0)
+        ep = _lib.epilogue(rowsum=rowsum)
+        with self._t(tag, 2.0 * M * N * K):
+            call("pg_gemm_f32_partials", int(transa), int(transb), M, N, K, ptr(A), A.stride(0), ptr(B),
+                 B.stride(0), ep, sk, ptr(slab), slab.numel(), ctypes.byref(used), self._s())
+        j = _lib.PgSplitkJob()
+        j.ws, j.split_k, j.M, j.N = ptr(slab), used.value, M, N
+        j.alpha, j.beta, j.C, j.ldc, j.rowsum = 1.0, beta, ptr(C), C.stride(0), ptr(rowsum)
+        self._jobs.append(j)
+
+    def _reduce_deferred(self) -> None:
+        jobs, self._jobs = self._jobs, []
+        for i in range(0, len(jobs), 16):
+            part = jobs[i:i + 16]
+            arr = (_lib.PgSplitkJob * len(part))(*part)
+            with self._t("gemm.splitk_reduce"):
+                call("pg_gemm_splitk_reduce_batch", arr, len(part), self._s())
 
     def _wgrad(self, *args, **kw):
         """A weight-gradient GEMM: forked onto the side stream at this point of the main
@@ -444,6 +480,7 @@ class TrainEngine:
                 self._gemm(self.dP[l], P[p + "Wpool"], dH, beta=1.0, act=LEAKY, dact=HM[:, :Fi],
                            tag=f"gemm.dgrad.pool.l{l + 1}")
                 dY = dH
+        self._reduce_deferred()
         self._join()
 
     def adam(self) -> None:

@@ -440,3 +440,44 @@ def test_gemm_split_k_in_kernel_combine(M, N, K, ta):
     C0 = C.clone()
     ops.gemm(A, B, transa=ta, out=C, beta=1.0, split_k=sk, splitk_cnt=cnt)
     torch.testing.assert_close(C, C0 + c1, rtol=1e-5, atol=1e-4)
+
+
+def test_gemm_split_k_deferred_batch_reduce_is_bitwise():
+    """pg_gemm_f32_partials + one pg_gemm_splitk_reduce_batch over several products equals
+    each product's own pg_gemm_f32 (split-K with its reduce launch) bitwise, row sums and
+    beta = 1 included (TrainEngine defers every weight gradient's combine to one launch)."""
+    import ctypes
+
+    from plagnn import _lib, ops
+    from plagnn._lib import call, ptr
+
+    gen = torch.Generator().manual_seed(11)
+    shapes = [(256, 1024, 24041), (100, 256, 24041), (12, 100, 24041), (97, 260, 9000)]
+    jobs, refs, outs, keep = [], [], [], []
+    for i, (M, N, K) in enumerate(shapes):
+        A = torch.randn(K, M, generator=gen).to(DEV)
+        B = torch.randn(K, N, generator=gen).to(DEV)
+        sk = ops._split_k(M, N, K)
+        beta = float(i % 2)
+        C0 = torch.randn(M, N, generator=gen).to(DEV)
+        ref, rs_ref = C0.clone(), torch.empty(M, device=DEV)
+        ops.gemm(A, B, transa=True, out=ref, beta=beta, split_k=sk, rowsum=rs_ref)
+        C, rs = C0.clone(), torch.empty(M, device=DEV)
+        ws = torch.empty(int(_lib.lib().pg_gemm_f32_workspace(M, N, K, sk)), dtype=torch.uint8, device=DEV)
+        used = ctypes.c_int(0)
+        call("pg_gemm_f32_partials", 1, 0, M, N, K, ptr(A), A.stride(0), ptr(B), B.stride(0),
+             _lib.epilogue(rowsum=rs), sk, ptr(ws), ws.numel(), ctypes.byref(used), _lib.stream_handle(A.device))
+        assert used.value > 1
+        j = _lib.PgSplitkJob()
+        j.ws, j.split_k, j.M, j.N, j.alpha, j.beta = ptr(ws), used.value, M, N, 1.0, beta
+        j.C, j.ldc, j.rowsum = ptr(C), C.stride(0), ptr(rs)
+        jobs.append(j)
+        refs.append((ref, rs_ref))
+        outs.append((C, rs))
+        keep += [A, B, ws]
+    arr = (_lib.PgSplitkJob * len(jobs))(*jobs)
+    call("pg_gemm_splitk_reduce_batch", arr, len(jobs), _lib.stream_handle(torch.device(DEV)))
+    torch.cuda.synchronize()
+    for (ref, rs_ref), (C, rs) in zip(refs, outs):
+        assert torch.equal(C, ref)
+        assert torch.equal(rs, rs_ref)
