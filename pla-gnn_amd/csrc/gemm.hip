@@ -1077,59 +1077,17 @@ struct BatchArgs {
   int n;
 };
 
-template <int G>
-__device__ __forceinline__ void reduce_block(const pg_splitk_job_t& j, int blk, int nblk) {
-  constexpr int OPB = 256 / G;
-  __shared__ float part[256];
-  const int M = (int)j.M, N = (int)j.N, S = j.split_k;
-  const float* ws = j.ws;
-  const float* ws_rowsum = ws + (int64_t)S * M * N;
-  const int64_t n = (int64_t)M * N;
-  const int64_t total = n + (j.rowsum ? M : 0);
-  const int ol = threadIdx.x % OPB, g = threadIdx.x / OPB;
-  const int z0 = (int)((int64_t)S * g / G), z1 = (int)((int64_t)S * (g + 1) / G);
-  for (int64_t base = (int64_t)blk * OPB; base < total; base += (int64_t)nblk * OPB) {
-    const int64_t i = base + ol;
-    float s = 0.f;
-    if (i < total) {
-      if (i < n) {
-        for (int z = z0; z < z1; ++z) s += ws[(int64_t)z * n + i];
-      } else {
-        for (int z = z0; z < z1; ++z) s += ws_rowsum[(int64_t)z * M + (i - n)];
-      }
-    }
-    if constexpr (G > 1) {
-      part[threadIdx.x] = s;
-      __syncthreads();
-      if (g == 0) {
-#pragma unroll
-        for (int q = 1; q < G; ++q) s += part[q * OPB + ol];
-      }
-      __syncthreads();
-    }
-    if (g == 0 && i < total) {
-      if (i >= n) {
-        j.rowsum[i - n] = s;
-      } else {
-        const int64_t r = i / N;
-        const int c = (int)(i - r * N);
-        float v = j.alpha * s;
-        if (j.beta != 0.f) v = v + j.beta * j.C[r * j.ldc + c];
-        j.C[r * j.ldc + c] = v;
-      }
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void splitk_reduce_batch_kernel(BatchArgs a) {
   int k = 0;
   while (k + 1 < a.n && (int)blockIdx.x >= a.first_block[k + 1]) ++k;
   const int blk = blockIdx.x - a.first_block[k];
   const int nblk = a.first_block[k + 1] - a.first_block[k];
+  const pg_splitk_job_t& j = a.job[k];
+  const float* wr = j.ws + (int64_t)j.split_k * j.M * j.N;
   switch (a.G[k]) {
-    case 1: reduce_block<1>(a.job[k], blk, nblk); break;
-    case 4: reduce_block<4>(a.job[k], blk, nblk); break;
-    default: reduce_block<16>(a.job[k], blk, nblk); break;
+    case 1: splitk_reduce_body<1>(j.ws, j.split_k, (int)j.M, (int)j.N, j.alpha, j.beta, j.C, j.ldc, wr, j.rowsum, blk, nblk); break;
+    case 4: splitk_reduce_body<4>(j.ws, j.split_k, (int)j.M, (int)j.N, j.alpha, j.beta, j.C, j.ldc, wr, j.rowsum, blk, nblk); break;
+    default: splitk_reduce_body<16>(j.ws, j.split_k, (int)j.M, (int)j.N, j.alpha, j.beta, j.C, j.ldc, wr, j.rowsum, blk, nblk); break;
   }
 }
 

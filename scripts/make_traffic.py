@@ -16,6 +16,7 @@ from collections import defaultdict
 
 GROUPS = {
     "gemm_f32_kernel": "gemm_f32", "gemm_dma_kernel": "gemm_f32", "splitk_reduce_kernel": "gemm_f32",
+    "splitk_reduce_batch_kernel": "gemm_f32",
     "gemm_bf16_kernel": "gemm_f32", "head_kernel": "head", "head_final_kernel": "head",
     "max_fwd_kernel": "spmm_max_fwd", "max_merge_kernel": "spmm_max_fwd",
     "group_pack_kernel": "spmm_max_bwd", "max_bwd_pull_kernel": "spmm_max_bwd",
@@ -50,7 +51,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("config")
-    ap.add_argument("--launches", default="gemm_f32=21,spmm_max_fwd=3,spmm_max_bwd=3,head=1,adam=1")
+    ap.add_argument("--launches", default="gemm_f32=22,spmm_max_fwd=3,spmm_max_bwd=3,head=1,adam=1")
     ap.add_argument("--gemm-group", default="gemm_f32", help="name of the GEMM group (gemm_bf16 for cfg5)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
