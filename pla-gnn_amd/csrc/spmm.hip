@@ -888,7 +888,10 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx,
     float* __restrict__ ws, int64_t ldw, int n_tiles = 1, int tile = 0, int64_t tile_stride = 0,
     const int32_t* __restrict__ tcol = nullptr, const T* __restrict__ dout = nullptr, int64_t ldd = 0) {
-  constexpr int U = 16;
+#ifndef PG_PULL_U
+#define PG_PULL_U 8  // measured on S0 (scripts/spmm_variants.sh): 4-8 best, 16 +6 %, 32 +25 %
+#endif
+  constexpr int U = PG_PULL_U;  // list segments in flight per wave
   __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
   const int wave = wave_id_uniform();
   const int it = blockIdx.x * kWavesPerBlock + wave;
