@@ -947,13 +947,15 @@ int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K) {
   int bm, bn;
   pick_tile(M, N, K, 1, bm, bn);
   if (((M + bm - 1) / bm) * ((N + bn - 1) / bn) >= 768) return 1;
-  // split products run 64 x 64 tiles: ~5 workgroups per CU (256 CUs), each slice >= 3 K
-  // steps, at most 256 slices
+  // split products run 64 x 64 tiles: ~4 workgroups per CU (256 CUs), each slice >= 3 K
+  // steps, at most 256 slices. Measured on the cfg2 step (whole step, batched combine):
+  // 1024 workgroups 1.984 ms, 768 1.992, 1280 2.022, 640 / 896 2.06 / 2.03 (not a multiple
+  // of the 256 CUs), 512 1.99, 384 2.15.
   const int64_t tiles = ((M + 63) / 64) * ((N + 63) / 64);
   static const int64_t want = [] {  // tuning knob PLAGNN_SPLIT_TARGET: workgroups aimed at
     const char* e = getenv("PLAGNN_SPLIT_TARGET");
-    const int64_t v = e ? atoll(e) : 1280;
-    return v > 0 ? v : 1280;
+    const int64_t v = e ? atoll(e) : 1024;
+    return v > 0 ? v : 1024;
   }();
   const int64_t target = (want + tiles - 1) / tiles;
   const int64_t by_k = K / (3 * BK);
