@@ -13,6 +13,7 @@ largest in-degree allows (else int32).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -21,8 +22,11 @@ import torch
 from . import _lib
 from ._lib import PgCsr, call
 
-DEFAULT_CHUNK = 256      # in-CSR entries per forward work item before a row is split
-DEFAULT_CHUNK_BWD = 128  # out-CSR entries per backward work item (its work is data-dependent)
+# in-CSR entries per forward work item before a row is split (tuning knob PLAGNN_CHUNK)
+DEFAULT_CHUNK = int(os.environ.get("PLAGNN_CHUNK", "256"))
+# out-CSR entries per backward work item, its work is data-dependent (knob PLAGNN_CHUNK_BWD;
+# measured on the cfg2 step: 64-96 best (1.97 ms), 128 1.99, 32 2.01, 256 2.11)
+DEFAULT_CHUNK_BWD = int(os.environ.get("PLAGNN_CHUNK_BWD", "64"))
 
 
 def _np_ptr(a: np.ndarray) -> int:
