@@ -25,8 +25,14 @@ from ._lib import PgCsr, call
 # in-CSR entries per forward work item before a row is split (tuning knob PLAGNN_CHUNK)
 DEFAULT_CHUNK = int(os.environ.get("PLAGNN_CHUNK", "256"))
 # out-CSR entries per backward work item, its work is data-dependent (knob PLAGNN_CHUNK_BWD;
-# measured on the cfg2 step: 64-96 best (1.97 ms), 128 1.99, 32 2.01, 256 2.11)
-DEFAULT_CHUNK_BWD = int(os.environ.get("PLAGNN_CHUNK_BWD", "64"))
+# None = by graph size). Measured whole steps: S0 (24 041 nodes) 64-96 best (1.97 ms), 128
+# 1.99, 32 2.01, 256 2.11; RMAT x16 (384 656 nodes) 128 24.3 ms vs 64 25.2 ms: finer items
+# pay off only while the graph alone does not fill the chip.
+DEFAULT_CHUNK_BWD = int(os.environ["PLAGNN_CHUNK_BWD"]) if "PLAGNN_CHUNK_BWD" in os.environ else None
+
+
+def default_chunk_bwd(num_nodes: int) -> int:
+    return 64 if num_nodes <= 65536 else 128
 
 
 def _np_ptr(a: np.ndarray) -> int:
@@ -98,7 +104,7 @@ class CSRGraph:
     """In-CSR + out-CSR of a directed graph given as COO (src -> dst), host resident."""
 
     def __init__(self, src, dst, num_nodes: int, chunk: int = DEFAULT_CHUNK,
-                 chunk_bwd: int = DEFAULT_CHUNK_BWD):
+                 chunk_bwd: Optional[int] = DEFAULT_CHUNK_BWD):
         src = np.ascontiguousarray(np.asarray(src, dtype=np.int64))
         dst = np.ascontiguousarray(np.asarray(dst, dtype=np.int64))
         if src.shape != dst.shape or src.ndim != 1:
@@ -124,6 +130,8 @@ class CSRGraph:
         einv = np.empty(max(E, 1), np.int32)
         einv[tslot[:E]] = np.arange(E, dtype=np.int32)
         self.fwd = HostCsr(ptr, col, None, n, chunk, einv=einv[:E])
+        if chunk_bwd is None:
+            chunk_bwd = default_chunk_bwd(n)
         self.bwd = HostCsr(tptr, tcol[:E], tslot[:E], n, min(chunk, chunk_bwd), epos=tpos[:E])
         # argmax records hold positions inside in-CSR rows: u16 while every row is shorter
         # than 0xFFFF entries (0xFFFF = no winner)
