@@ -95,7 +95,11 @@ def test_spmm_max_bwd(oracle_mod, F, weighted):
     split_rows = set(g.bwd.merges.reshape(-1, 4)[: g.bwd.n_merges, 0].tolist())
     exact = np.array([u not in split_rows for u in range(n)])
     np.testing.assert_array_equal(dX[exact], dX_ref[exact])
-    np.testing.assert_allclose(dX, dX_ref, rtol=1e-5, atol=1e-5)
+    # split rows: a different summation grouping, bounded by the error scale sum |terms|
+    mag = np.abs(oracle_mod.spmm_max_bwd(og, argx, arge, np.abs(dZ), use_weight=False))
+    if weighted:
+        mag = mag * np.abs(w).max()
+    assert np.all(np.abs(dX - dX_ref) <= 1e-5 * mag + 1e-6)
     # fused relu' mask
     mask = torch.from_numpy(X).to(DEV)
     dXm = ops.spmm_max_backward(dg, argpos, torch.from_numpy(dZ).to(DEV), ews, mask=mask).cpu().numpy()
@@ -375,7 +379,12 @@ def test_spmm_max_grouped_matches_record_path(oracle_mod, F, weighted, hub, chun
     np.testing.assert_array_equal(out_g.cpu().numpy(), ref_out)
     ref = oracle_mod.spmm_max_bwd(og, argx, arge, dZ.cpu().numpy(), use_weight=weighted)
     ref = np.where(Pn > 0, ref, 0.0)
-    np.testing.assert_allclose(dx_g.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    # rows split across work items sum in a different grouping: bound by the summation
+    # error scale sum |terms| (the same oracle on |dZ|)
+    mag = oracle_mod.spmm_max_bwd(og, argx, arge, np.abs(dZ.cpu().numpy()), use_weight=weighted)
+    if weighted:
+        mag = np.abs(mag)
+    assert np.all(np.abs(dx_g.cpu().numpy() - ref) <= 1e-5 * np.abs(mag) + 1e-6)
     # bf16 storage
     Pb, dZb = P.to(torch.bfloat16), dZ.to(torch.bfloat16)
     ob_r, argb = ops.spmm_max(dg, Pb, ew)
