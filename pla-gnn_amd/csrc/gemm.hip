@@ -1049,7 +1049,7 @@ int gemm_f32_impl(int transa, int transb, int64_t M, int64_t N, int64_t K, float
     rc = launch_trans<64, 64>(ta, tb, va, vb, epi, grid, st, a);
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_f32: dispatch failed");
   if (split && !in_kernel && !defer) {
-    const int64_t n = M * N + (ep->rowsum ? M : 0);
+    const int64_t n = (N % 4 == 0 ? M * N / 4 : M * N) + (ep->rowsum ? M : 0);  // work units
     // threads per output: enough slice groups that each thread sums <= ~8 slices
     const int G = splitk_groups(split_k);
     const int opb = 256 / G;
@@ -1129,7 +1129,7 @@ int pg_gemm_splitk_reduce_batch(const pg_splitk_job_t* jobs, int n_jobs, pg_stre
     a.job[k] = j;
     a.G[k] = splitk_groups(j.split_k);
     a.first_block[k] = blocks;
-    const int64_t n = j.M * j.N + (j.rowsum ? j.M : 0);
+    const int64_t n = (j.N % 4 == 0 ? j.M * j.N / 4 : j.M * j.N) + (j.rowsum ? j.M : 0);  // work units
     const int opb = 256 / a.G[k];
     blocks += (int)std::min<int64_t>(8192, (n + opb - 1) / opb);
   }

@@ -574,7 +574,7 @@ int pg_gemm_bf16(int transa, int transb, int64_t M, int64_t N, int64_t K, float 
   else rc = launch_tile<64, 64, 2, 2>(ta, tb, obf, epi, grid, st, a);
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_bf16: dispatch failed");
   if (split) {
-    const int64_t n = M * N + (ep->rowsum ? M : 0);
+    const int64_t n = (N % 4 == 0 ? M * N / 4 : M * N) + (ep->rowsum ? M : 0);  // work units
     const int G = splitk_groups(split_k);
     const int opb = 256 / G;
     const int blocks = (int)std::min<int64_t>(8192, (n + opb - 1) / opb);

@@ -12,6 +12,8 @@ namespace pg_gemm {
 // activation given its OUTPUT y (the fused backward of relu / leaky_relu), or split-K.
 enum Epi { EPI_NONE = 0, EPI_RELU = 1, EPI_LEAKY = 2, EPI_DRELU = 3, EPI_DLEAKY = 4, EPI_SPLIT = 5 };
 
+__host__ __device__ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 template <int EPI>
 __device__ __forceinline__ float epi_apply(float x, float y, float slope) {
   if constexpr (EPI == EPI_RELU) return x > 0.f ? x : 0.f;
@@ -41,39 +43,74 @@ __device__ __forceinline__ float splitk_sum(const float* __restrict__ p, int64_t
   return s;
 }
 
+__device__ __forceinline__ float4 splitk_sum4(const float* __restrict__ p, int64_t stride, int z0, int z1) {
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int z = z0; z < z1; z += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = z + e < z1 ? *reinterpret_cast<const float4*>(p + (int64_t)(z + e) * stride) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (z + e < z1) {
+        s.x += v[e].x; s.y += v[e].y; s.z += v[e].z; s.w += v[e].w;
+      }
+  }
+  return s;
+}
+
+// vec4 (N % 4 == 0, 16-B aligned slabs): a work unit is 4 consecutive outputs of one row
+// (float4 slab loads, each component summed in the same slice order: bitwise the same as
+// the scalar form), the row sums stay scalar units after them.
 template <int G>
 __device__ __forceinline__ void splitk_reduce_body(const float* __restrict__ ws, int splits, int M, int N,
                                                    float alpha, float beta, float* __restrict__ C,
                                                    int64_t ldc, const float* __restrict__ ws_rowsum,
                                                    float* __restrict__ rowsum, int blk, int nblk) {
-  constexpr int OPB = 256 / G;  // outputs per block
-  __shared__ float part[256];
+  constexpr int OPB = 256 / G;  // units per block
+  __shared__ float4 part[256];
   const int64_t n = (int64_t)M * N;
-  const int64_t total = n + (rowsum ? M : 0);
+  const bool vec = (N % 4) == 0 && al16(ws);
+  const int64_t nu = vec ? n / 4 : n;  // units of the product
+  const int64_t total = nu + (rowsum ? M : 0);
   const int ol = threadIdx.x % OPB, g = threadIdx.x / OPB;
   const int z0 = (int)((int64_t)splits * g / G), z1 = (int)((int64_t)splits * (g + 1) / G);
   for (int64_t base = (int64_t)blk * OPB; base < total; base += (int64_t)nblk * OPB) {
-    const int64_t i = base + ol;
-    float s = 0.f;
-    if (i < total) s = i < n ? splitk_sum<G>(ws + i, n, z0, z1) : splitk_sum<G>(ws_rowsum + (i - n), M, z0, z1);
+    const int64_t u = base + ol;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (u < total) {
+      if (u >= nu) s.x = splitk_sum<G>(ws_rowsum + (u - nu), M, z0, z1);
+      else if (vec) s = splitk_sum4(ws + 4 * u, n, z0, z1);
+      else s.x = splitk_sum<G>(ws + u, n, z0, z1);
+    }
     if constexpr (G > 1) {
       part[threadIdx.x] = s;
       __syncthreads();
       if (g == 0) {
 #pragma unroll
-        for (int q = 1; q < G; ++q) s += part[q * OPB + ol];
+        for (int q = 1; q < G; ++q) {
+          const float4 t = part[q * OPB + ol];
+          s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+        }
       }
       __syncthreads();
     }
-    if (g == 0 && i < total) {
-      if (i >= n) {
-        rowsum[i - n] = s;
+    if (g == 0 && u < total) {
+      if (u >= nu) {
+        rowsum[u - nu] = s.x;
       } else {
+        const int64_t i = vec ? 4 * u : u;
         const int64_t r = i / N;
         const int c = (int)(i - r * N);
-        float v = alpha * s;
-        if (beta != 0.f) v = v + beta * C[r * ldc + c];
-        C[r * ldc + c] = v;
+        float* cp = C + r * ldc + c;
+        const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (e > 0 && !vec) break;
+          float v = alpha * sv[e];
+          if (beta != 0.f) v = v + beta * cp[e];
+          cp[e] = v;
+        }
       }
     }
   }
@@ -87,8 +124,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                             float* __restrict__ rowsum) {
   splitk_reduce_body<G>(ws, splits, M, N, alpha, beta, C, ldc, ws_rowsum, rowsum, blockIdx.x, gridDim.x);
 }
-
-inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Threads per output of the split-K combine: enough slice groups that each thread sums
 // <= ~8 slices.
