@@ -992,6 +992,39 @@ __global__ __launch_bounds__(kBlock) void sum_merge_kernel(
   const int4 m = merges[blockIdx.x];
   const int row = m.x, s0 = m.y, ns = m.z;
   const float deg = divide_by_deg ? (float)(ptr[row + 1] - ptr[row]) : 1.f;
+  // 4 features per thread (float4 slot loads) when every row is 4-aligned: the same
+  // per-feature order, bitwise the same result
+  constexpr uintptr_t kTa = 4 * sizeof(T) - 1;
+  const bool vec = (F % 4) == 0 && (ldw % 4) == 0 && (ldo % 4) == 0 && ((uintptr_t)ws & 15) == 0 &&
+                   ((uintptr_t)out & kTa) == 0 && (!mask || ((ldm % 4) == 0 && ((uintptr_t)mask & kTa) == 0));
+  if (vec) {
+    for (int f = threadIdx.x * 4; f < F; f += kBlock * 4) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int s = s0; s < s0 + ns; s += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[e] = *reinterpret_cast<const float4*>(ws + (int64_t)min(s + e, s0 + ns - 1) * ldw + f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (s + e < s0 + ns) {
+            acc[0] += v[e].x; acc[1] += v[e].y; acc[2] += v[e].z; acc[3] += v[e].w;
+          }
+      }
+      if (divide_by_deg)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = acc[i] / deg;
+      if (mask) {
+        float mk[4];
+        load_tile<4, T>(mask + (int64_t)row * ldm, f, F, mk, 0.f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (!(mk[i] > 0.f)) acc[i] = 0.f;
+      }
+      store_tile<4, T>(out + (int64_t)row * ldo, f, F, acc);
+    }
+    return;
+  }
   for (int f = threadIdx.x; f < F; f += kBlock) {
     float acc = 0.f;
     for (int s = s0; s < s0 + ns; s += 8) {
