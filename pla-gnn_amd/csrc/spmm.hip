@@ -366,13 +366,18 @@ __global__ __launch_bounds__(kBlock) void max_merge_kernel(const int4* __restric
     int bp = arg_none<A>();
     for (int s = s0; s < s0 + ns; s += 8) {
       float v[8];
+      int a[8];  // loaded with the values: no dependent load behind each compare
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ws_val[(int64_t)min(s + e, s0 + ns - 1) * ldw + f];
+      for (int e = 0; e < 8; ++e) {
+        const int64_t o = (int64_t)min(s + e, s0 + ns - 1) * ldw + f;
+        v[e] = ws_val[o];
+        a[e] = (int)ws_arg[o];
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         if (s + e < s0 + ns && v[e] > best) {
           best = v[e];
-          bp = (int)ws_arg[(int64_t)(s + e) * ldw + f];
+          bp = a[e];
         }
     }
     if (__builtin_isinf(best)) best = 0.f;
@@ -784,13 +789,18 @@ __global__ __launch_bounds__(kBlock) void max_merge_group_kernel(
   if (f < F) {
     for (int s = s0; s < s0 + ns; s += 8) {
       float v[8];
+      int a[8];  // loaded with the values: no dependent load behind each compare
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ws_val[(int64_t)min(s + e, s0 + ns - 1) * ldw + f];
+      for (int e = 0; e < 8; ++e) {
+        const int64_t o = (int64_t)min(s + e, s0 + ns - 1) * ldw + f;
+        v[e] = ws_val[o];
+        a[e] = (int)ws_arg[o];
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         if (s + e < s0 + ns && v[e] > best) {
           best = v[e];
-          bp = (int)ws_arg[(int64_t)(s + e) * ldw + f];
+          bp = a[e];
         }
     }
     if (__builtin_isinf(best)) best = 0.f;
