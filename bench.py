@@ -4,14 +4,23 @@
 metric: edges aggregated / s per training epoch, full graph. One step = one full-graph
 training epoch of the reference (code/train.py:197-207: zero_grad, forward, multi_loss on
 the train rows, backward, Adam.step, val loss on the same logits); edges per step =
-L_sage * E' (E' = PPI edges + N self-loops). Workload (BASELINE configs[1]): synthetic
-PPI stand-in S0 (N = 24,041, power-law, mean degree 50, E' ~ 1.23 M), 3 SAGE-pool layers
-of hidden 256 (503 -> 256 -> 256 -> 256, MLP 256 -> 100 -> 12), fp32.
+L_sage * E' (E' = PPI edges + N self-loops). Default workload (BASELINE configs[1]):
+synthetic PPI stand-in S0 (N = 24,041, power-law, mean degree 50, E' ~ 1.23 M), 3 SAGE-pool
+layers of hidden 256 (503 -> 256 -> 256 -> 256, MLP 256 -> 100 -> 12), fp32. The other
+configs are plagnn.workload.CONFIGS (--config).
 
-Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): every rank trains a full-graph
-replica on its own graph (rank r: synthetic seed 70 + r, the perturbation-graph replicas
-of BASELINE configs[3]) with ONE all-reduce (average) of the flat gradient bucket per step
-before Adam; weak scaling. value = sum over ranks of edges / max-over-ranks time.
+Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): every rank holds a full-graph
+replica and starts from the same parameters; each step ends with ONE all-reduce (average)
+of the flat gradient bucket before Adam. Rank r trains the rows train_index[r::world] of
+the fold (cfg4: every rank its own perturbation graph, all train rows). Weak scaling:
+value = sum over ranks of edges / max-over-ranks time.
+
+Beside the engine's number (`value`), rank 0 at N = 1 also reports
+  * `dropin`: the unmodified reference loop on the dgl shim (plagnn.model + torch Adam,
+    exactly what main_normal.py -d cuda runs, code/train.py:197-207);
+  * `epoch_with_eval`: the reference-faithful epoch with its per-epoch evaluation
+    (code/train.py:210-218) on the device kernels;
+  * `cpu_baseline`: the oracle run as DGL's CPU backend runs it (OpenMP rows + torch-CPU).
 
 Prints ONE JSON line on rank 0.
 """
@@ -30,25 +39,12 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-CONFIGS = {
-    # name: (graph kind, dims, description)
-    "cfg2": ("s0", [503, 256, 256, 256, 100, 12],
-             "S0 PPI stand-in (N=24041, mean deg 50), 3x SAGE-pool hidden 256, fp32"),
-    "ref": ("s0", [503, 400, 300, 200, 100, 12],
-            "S0 PPI stand-in, reference dims GNN32(503,400,300,200,100,12), fp32"),
-    "cfg3": ("s0", [503, 512, 512, 512, 100, 12],
-             "S0 perturbed (+-3% edges), ECC edge weights (pg_ecc, u_mul_e max), hidden 512, fp32"),
-    "cfg5": ("rmat", [503, 512, 512, 512, 100, 12],
-             "RMAT x16 PPI (N=384656, a,b,c,d=.57,.19,.19,.05, mean deg 50), hidden 512, bf16 storage, f32 accumulate"),
-    "cfg5-f32": ("rmat", [503, 512, 512, 512, 100, 12],
-                 "RMAT x16 PPI (N=384656, a,b,c,d=.57,.19,.19,.05, mean deg 50), hidden 512, fp32"),
-}
-BF16_CONFIGS = {"cfg5"}  # BASELINE configs[4]: "hidden=512 bf16"
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_F32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
 # MI355X_MICROARCH.md: bf16 MFMA ~2.5 PF dense = 256 CUs x 4 SIMDs x (2*32*32*16 flops per
 # 32-cycle v_mfma_f32_32x32x16_bf16) x 2.4 GHz
 PEAK_BF16_TFLOPS = 2516.6
+ALPHA = 0.1               # main_normal.py -a default (code/main_normal.py:27)
 
 
 def _group(name: str, gemm_group: str = "gemm_f32") -> str:
@@ -57,80 +53,156 @@ def _group(name: str, gemm_group: str = "gemm_f32") -> str:
     return name.split(".")[0]
 
 
-def _cfg3_graph(ds, seed):
-    """the S0 graph perturbed (about 3 % of the undirected edges removed
-    and as many random ones added, the ΔPCC-style topology change of
-    data_preprocess.py:217-257), its edge clustering coefficients computed on the GPU
-    (pg_ecc, data_preprocess.py:175-214) as edge weights; self-loops weigh 1.0."""
-    from scipy.sparse import coo_matrix
-
-    from plagnn import ecc
-
-    rng = np.random.default_rng(seed)
-    n = ds.n
-    r, c = ds.row.astype(np.int64), ds.col.astype(np.int64)
-    up = r < c
-    ur, uc = r[up], c[up]
-    keep = rng.random(len(ur)) >= 0.03
-    na = int((~keep).sum())
-    ar, ac = rng.integers(0, n, na), rng.integers(0, n, na)
-    ok = ar != ac
-    ur = np.concatenate([ur[keep], np.minimum(ar[ok], ac[ok])])
-    uc = np.concatenate([uc[keep], np.maximum(ar[ok], ac[ok])])
-    a = coo_matrix((np.ones(2 * len(ur), np.int64), (np.concatenate([ur, uc]), np.concatenate([uc, ur]))),
-                   shape=(n, n)).tocsr()
-    a.data[:] = 1
-    a = a.tocoo()
-    e = ecc.edge_clustering_coefficients(a).tocsr()
-    src, dst = a.row.astype(np.int64), a.col.astype(np.int64)
-    w = np.asarray(e[src, dst]).ravel().astype(np.float32)
-    loops = np.arange(n, dtype=np.int64)
-    src = np.concatenate([src, loops])
-    dst = np.concatenate([dst, loops])
-    w = np.concatenate([w, np.ones(n, np.float32)])
-    return src, dst, torch.from_numpy(w)
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
-def cpu_baseline(ds, dims, train_idx, w, seconds: float = 15.0):
-    """The oracle (C restatement of DGL's CPU loops + torch-CPU fp32 dense algebra) timed
-    on this host on the same graph and dims; bounded to ~`seconds` of work."""
+def _cpu_threads() -> int:
+    """The threads this job may use: OMP_NUM_THREADS when the launcher sets it (the GPU box
+    sets it to the job's CPU share), else the CPUs in this process's affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(wl, dims, seconds: float = 20.0, min_steps: int = 5):
+    """The oracle run the way DGL's CPU backend runs the reference step: SpMM-max rows under
+    OpenMP, backward via torch-CPU scatter_add_, dense algebra in torch-CPU fp32, with every
+    CPU thread of the job; median of >= min_steps full steps (bounded by `seconds`). Also
+    the reference-faithful epoch: the step plus code/train.py:210-214's evaluation
+    (protein_loc_correction with its per-row loop, performances_record on the train and
+    val rows)."""
     import oracle
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
-    og = oracle.OracleGraph(ds.row, ds.col, ds.n)
-    x = torch.from_numpy(ds.feat)
-    labels = torch.from_numpy(ds.loc.astype(np.float32))
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    src, dst, w = wl.edges_without_loops()
+    og = oracle.OracleGraph(src, dst, wl.n, edge_weight=w)
+    use_w = w is not None
+    x = torch.from_numpy(wl.ds.feat)
+    labels = torch.from_numpy(wl.ds.loc.astype(np.float32))
     p = oracle.init_params(dims, seed=0)
     keys = list(p)
     m = [torch.zeros_like(p[k]) for k in keys]
     v = [torch.zeros_like(p[k]) for k in keys]
-    times = []
+    times, eval_times = [], []
     t_start = time.perf_counter()
     step = 0
     while True:
         t0 = time.perf_counter()
-        _, _, grads = oracle.train_step(og, x, labels, train_idx, w, p)
+        logits, _, grads = oracle.train_step(og, x, labels, wl.train_index, wl.class_weight, p, use_weight=use_w,
+                                             parallel=True)
         step += 1
         oracle.adam_step_torch110([p[k] for k in keys], [grads[k] for k in keys], m, v, step, 5e-5)
-        times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > seconds or step >= 5:
+        oracle.multi_loss(logits[wl.val_index], labels[wl.val_index], wl.class_weight)
+        t1 = time.perf_counter()
+        times.append(t1 - t0)
+        if step <= 2:  # the reference-faithful epoch's evaluation, timed on two epochs
+            pred = oracle.protein_loc_correction(logits, ALPHA, rowwise=True)
+            oracle.performances_record(labels[wl.train_index], pred[wl.train_index])
+            oracle.performances_record(labels[wl.val_index], pred[wl.val_index])
+            eval_times.append(time.perf_counter() - t1)
+        if step >= min_steps and time.perf_counter() - t_start > seconds:
+            break
+        if step >= 50:
             break
     t = float(np.median(times))
+    t_eval = float(np.median(eval_times))
     L = len(dims) - 3
-    return {"value": L * og.num_edges / t, "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": f"{step} full training step(s) of the oracle on the same S0 graph and dims "
-                      f"(median {t:.2f} s/step; SpMM in single-thread C, dense in torch-CPU with "
-                      f"{threads} threads)"}
+    return {"value": round(L * og.num_edges / t, 1), "unit": "edges/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "ms_per_step": round(t * 1e3, 2),
+            "steps_timed": step, "epoch_with_eval_ms": round((t + t_eval) * 1e3, 2),
+            "sample": f"median of {step} full training steps of the oracle on the same graph and dims "
+                      f"(SpMM-max rows OpenMP-parallel C, backward torch scatter_add_, dense torch-CPU fp32, "
+                      f"{threads} threads); epoch_with_eval adds code/train.py:210-214's evaluation "
+                      f"(per-row loops, median of {len(eval_times)})"}
+
+
+def dropin_leg(wl, dims, dev, steps: int, warmup: int):
+    """What `main_normal.py -d cuda` runs per epoch (code/train.py:197-207) on the dgl shim:
+    GNN32/GNN module, multi_loss, autograd, torch.optim.Adam, val loss on the same logits."""
+    import dgl
+    from plagnn.model import GNN
+    from plagnn.train import multi_loss
+
+    if wl.edge_weight is not None:
+        return None  # the reference's SAGEConv('pool') call takes no edge weights
+    src, dst, _ = wl.edges_without_loops()
+    g = dgl.add_self_loop(dgl.graph((torch.from_numpy(src), torch.from_numpy(dst)), num_nodes=wl.n)).to(dev)
+    features = torch.from_numpy(wl.ds.feat).to(dev)
+    labels = torch.from_numpy(wl.ds.loc.astype(np.float32)).to(dev)
+    tr = torch.as_tensor(wl.train_index, device=dev)
+    va = torch.as_tensor(wl.val_index, device=dev)
+    torch.manual_seed(0)
+    model = GNN(dims).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=5e-5)
+
+    def epoch():
+        opt.zero_grad()
+        model.train()
+        logits = model(g, features)
+        train_loss = multi_loss(logits[tr], labels[tr], wl.class_weight)
+        train_loss.backward()
+        opt.step()
+        model.eval()
+        val_loss = multi_loss(logits[va], labels[va], wl.class_weight)
+        return train_loss, val_loss
+
+    for _ in range(warmup):
+        epoch()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tl, vl = epoch()
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    L = len(dims) - 3
+    return {"ms_per_step": round(ms, 4), "value": round(L * (len(wl.src)) / ms * 1e3, 1), "unit": "edges/s",
+            "loss": {"train": float(tl), "val": float(vl)},
+            "what": "unmodified reference epoch body on the dgl shim: plagnn.model + multi_loss + autograd + "
+                    "torch.optim.Adam (code/train.py:197-207)"}
+
+
+def epoch_with_eval_leg(engine, wl, dev, epochs: int = 20):
+    """The reference-faithful epoch (code/train.py:197-218): the engine's step, then
+    protein_loc_correction on all logits and performances_record on the train and val rows
+    (device kernels, plagnn.loc_eval), and the two loss values read on the host."""
+    from plagnn import loc_eval
+
+    labels = torch.from_numpy(wl.ds.loc.astype(np.float32)).to(dev)
+    tr = torch.as_tensor(wl.train_index, device=dev)
+    va = torch.as_tensor(wl.val_index, device=dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(epochs):
+        engine.step()
+        pred = loc_eval.protein_loc_correction(engine.logits(), ALPHA)
+        loc_eval.performances_record(labels[tr], pred[tr])
+        loc_eval.performances_record(labels[va], pred[va])
+        engine.losses()
+    torch.cuda.synchronize(dev)
+    return round((time.perf_counter() - t0) / epochs * 1e3, 4)
 
 
 def main():
+    from plagnn import workload as W
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="cfg2", choices=sorted(W.CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-legs", action="store_true", help="skip the drop-in and epoch-with-eval legs")
     ap.add_argument("--breakdown-reps", type=int, default=5)
     ap.add_argument("--dump-breakdown", default="", help="write the per-launch-site breakdown (JSON)")
     args = ap.parse_args()
@@ -149,29 +221,22 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     import plagnn
-    from plagnn import data
-    from plagnn.train import fold_splits, weight_cal
+    from plagnn import dist as pdist
 
-    kind, dims, desc = CONFIGS[args.config]
-    ds = data.make_dataset(kind, seed=70 + rank)
-    src, dst = ds.edges_with_self_loops()
-    graph = plagnn.CSRGraph(src, dst, ds.n)
-    label = [int(i) for i in ds.labelled]
-    train_idx, val_idx = next(fold_splits(label, 10, 12))  # round 1, fold 1 (train.py:162-178)
-    w = weight_cal(ds.loc)
-    ew = None
-    if args.config == "cfg3":
-        src, dst, ew = _cfg3_graph(ds, 70 + rank)
-        graph = plagnn.CSRGraph(src, dst, ds.n)
-    bf16 = args.config in BF16_CONFIGS
+    wl = W.build(args.config, rank=rank, device=dev)
+    if world > 1 and args.config != "cfg4":
+        wl.train_index = wl.train_index[rank::world]  # the fold's train rows sharded over ranks
+    graph = wl.graph()
+    dims, bf16 = wl.dims, wl.bf16
     Engine = plagnn.TrainEngineBF16 if bf16 else plagnn.TrainEngine
     gemm_group = "gemm_bf16" if bf16 else "gemm_f32"
-    engine = Engine(graph, torch.from_numpy(ds.feat), torch.from_numpy(ds.loc.astype(np.float32)),
-                                dims, w, train_idx, val_idx, lr=5e-5, device=dev, edge_weight=ew,
-                                seed=rank)
+    engine = Engine(graph, torch.from_numpy(wl.ds.feat), torch.from_numpy(wl.ds.loc.astype(np.float32)),
+                    dims, wl.class_weight, wl.train_index, wl.val_index, lr=5e-5, device=dev,
+                    edge_weight=wl.edge_weight, seed=0)
     allreduce = None
     if dist is not None:
-        from plagnn.dist import allreduce_mean as allreduce
+        pdist.broadcast_([engine.flat])  # identical starting replicas (same seed as well)
+        allreduce = pdist.allreduce_mean
 
     n_cap_warm = min(2, args.warmup)
     engine.capture(warmup=n_cap_warm, allreduce=allreduce)
@@ -199,13 +264,23 @@ def main():
     loss_tr, loss_va = engine.losses()
     if not (np.isfinite(loss_tr) and np.isfinite(loss_va)):
         raise SystemExit(f"non-finite loss after training: {loss_tr}, {loss_va}")
+    if dist is not None:
+        # every rank must hold the same parameters after the timed steps
+        probe = engine.flat[:4096].double().sum().reshape(1)
+        lo, hi = probe.clone(), probe.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        if lo.item() != hi.item():
+            raise SystemExit("replicas diverged")
+        dist.barrier()
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
 
-    # per-kernel HIP-event breakdown (eager diagnostic steps, after the timed region)
+    # per-kernel HIP-event breakdown: eager diagnostic steps after the timed region, on rank 0
+    # only, so without the collective
     bd = engine.kernel_breakdown(args.breakdown_reps)
     if args.dump_breakdown:
         with open(args.dump_breakdown, "w") as f:
@@ -243,9 +318,15 @@ def main():
         traffic = tj.get(args.config, {}).get(dom)
     rf["traffic"] = traffic
 
+    legs = {}
+    if world == 1 and not args.no_legs:
+        legs["epoch_with_eval_ms"] = epoch_with_eval_leg(engine, wl, dev)
+        if not bf16:
+            legs["dropin"] = dropin_leg(wl, dims, dev, steps=min(args.steps, 20), warmup=3)
+
     cpu = None
-    if world == 1 and not args.no_cpu_baseline and args.config in ("cfg2", "ref"):
-        cpu = cpu_baseline(ds, dims, train_idx, w)
+    if world == 1 and not args.no_cpu_baseline and not args.config.startswith("cfg5"):
+        cpu = cpu_baseline(wl, dims)
 
     out = {
         "metric": "edges aggregated/sec per training epoch, full PPI graph",
@@ -260,12 +341,14 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16" if bf16 else "f32",
         "data": "synthetic (seeded power-law PPI stand-in; real PPI/GEO/UniProt inputs are not shipped)",
-        "config": {"workload": f"{args.config}: {desc}", "nodes": ds.n, "edges_with_self_loops": graph.num_edges,
-                   "sage_layers": len(dims) - 3, "dims": dims, "edges_per_step": engine.edges_per_step,
+        "config": {"workload": f"{args.config}: {wl.desc}", "nodes": wl.n, "edges_with_self_loops": graph.num_edges,
+                   "graph_variant_rank0": wl.variant, "sage_layers": len(dims) - 3, "dims": dims,
+                   "edges_per_step": engine.edges_per_step,
                    "parallelism": f"replicas{world}+grad-allreduce" if world > 1 else "single"},
         "roofline": rf,
         "spmm_roofline": {k: roof(k) for k in ("spmm_max_fwd", "spmm_max_bwd") if k in groups},
         "kernels_ms_per_step": {k: round(v["ms"], 4) for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])},
+        **legs,
         "cpu_baseline": cpu,
         "loss": {"train": loss_tr, "val": loss_va},
     }

@@ -19,7 +19,9 @@ CPU restatement of the reference's training hot path:
 * ``torch.optim.Adam`` step as torch 1.10.0 computes it (code/train.py:180, 205).
 
 Dense algebra runs in torch-CPU float32 (the "plain PyTorch fp32 reference"); the
-message passing runs in the C restatement, single-threaded, in DGL's loop order.
+message passing runs in the C restatement, single-threaded, in DGL's loop order. With
+``parallel=True`` (bench.py's CPU baseline) the forward loop runs row-parallel under
+OpenMP and the backward is torch-CPU ``scatter_add_``, as DGL's CPU backend runs them.
 
 Pinning: ``multi_loss``/``weight_cal`` are checked against golden vectors produced by the
 reference's own functions (tests/golden/gen_golden.py). The DGL message-passing
@@ -63,6 +65,8 @@ def lib():
         L.oracle_spmm_max.argtypes = [_i64p, _i64p, _i64p, _f32p, _f32p, ctypes.c_int64, ctypes.c_int64,
                                       _f32p, _i64p, _i64p]
         L.oracle_spmm_max.restype = None
+        L.oracle_spmm_max_omp.argtypes = L.oracle_spmm_max.argtypes
+        L.oracle_spmm_max_omp.restype = None
         L.oracle_spmm_max_bwd.argtypes = [_i64p, _i64p, _f32p, _f32p, _u8p, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.c_int64, _f32p]
         L.oracle_spmm_max_bwd.restype = None
@@ -125,14 +129,17 @@ class OracleGraph:
 
 
 # ---------------------------------------------------------------- message passing
-def spmm_max(g: OracleGraph, X: np.ndarray, use_weight: bool = False):
+def spmm_max(g: OracleGraph, X: np.ndarray, use_weight: bool = False, parallel: bool = False):
+    """parallel=True: the OpenMP row-parallel form of the same loop (DGL's CPU backend;
+    the timed CPU baseline), identical results."""
     X = np.ascontiguousarray(X, np.float32)
     F = X.shape[1]
     out = np.empty((g.n, F), np.float32)
     argx = np.empty((g.n, F), np.int64)
     arge = np.empty((g.n, F), np.int64)
     w = g.ew if use_weight else None
-    lib().oracle_spmm_max(_p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p),
+    fn = lib().oracle_spmm_max_omp if parallel else lib().oracle_spmm_max
+    fn(_p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p),
                           _p(w, _f32p), _p(X, _f32p), g.n, F, _p(out, _f32p), _p(argx, _i64p),
                           _p(arge, _i64p))
     return out, argx, arge
@@ -162,15 +169,22 @@ class _MaxAggregate(torch.autograd.Function):
     """update_all(copy_u|u_mul_e, max) with DGL's GSpMM backward (scatter_add_ on argX)."""
 
     @staticmethod
-    def forward(ctx, P, g, use_weight):
-        out, argx, arge = spmm_max(g, P.detach().numpy(), use_weight)
-        ctx.g, ctx.argx, ctx.arge, ctx.use_weight = g, argx, arge, use_weight
+    def forward(ctx, P, g, use_weight, parallel=False):
+        out, argx, arge = spmm_max(g, P.detach().numpy(), use_weight, parallel)
+        ctx.g, ctx.argx, ctx.arge, ctx.use_weight, ctx.parallel = g, argx, arge, use_weight, parallel
         return torch.from_numpy(out)
 
     @staticmethod
     def backward(ctx, dZ):
+        if ctx.parallel:
+            # DGL's own form: dX = zeros; dX.scatter_add_(0, argX, dZ [* w[argE]]) in torch-CPU
+            dZ = dZ.contiguous()
+            if ctx.use_weight:
+                dZ = dZ * torch.from_numpy(ctx.g.ew)[torch.from_numpy(ctx.arge)]
+            dX = torch.zeros_like(dZ).scatter_add_(0, torch.from_numpy(ctx.argx), dZ)
+            return dX, None, None, None
         dX = spmm_max_bwd(ctx.g, ctx.argx, ctx.arge, dZ.contiguous().numpy(), ctx.use_weight)
-        return torch.from_numpy(dX), None, None
+        return torch.from_numpy(dX), None, None, None
 
 
 # ---------------------------------------------------------------- model (code/model.py)
@@ -179,23 +193,23 @@ def leaky_relu(x):
 
 
 def sage_pool(g: OracleGraph, h: torch.Tensor, p: Dict[str, torch.Tensor], prefix: str,
-              use_weight: bool = False) -> torch.Tensor:
+              use_weight: bool = False, parallel: bool = False) -> torch.Tensor:
     """DGL 0.8.2 SAGEConv(aggregator_type='pool', feat_drop=0, bias=True, norm=None,
     activation=None).forward(graph, feat[, edge_weight])."""
     P = torch.relu(h @ p[prefix + "fc_pool.weight"].t() + p[prefix + "fc_pool.bias"])
-    neigh = _MaxAggregate.apply(P, g, use_weight)
+    neigh = _MaxAggregate.apply(P, g, use_weight, parallel)
     h_neigh = neigh @ p[prefix + "fc_neigh.weight"].t()
     rst = h @ p[prefix + "fc_self.weight"].t() + h_neigh
     return rst + p[prefix + "bias"]
 
 
 def gnn32_forward(g: OracleGraph, x: torch.Tensor, p: Dict[str, torch.Tensor],
-                  use_weight: bool = False) -> torch.Tensor:
+                  use_weight: bool = False, parallel: bool = False) -> torch.Tensor:
     """GNN32.forward (code/model.py:19-31), generalised to any number of conv layers."""
     h = x
     i = 1
     while f"conv{i}.fc_pool.weight" in p:
-        h = leaky_relu(sage_pool(g, h, p, f"conv{i}.", use_weight))
+        h = leaky_relu(sage_pool(g, h, p, f"conv{i}.", use_weight, parallel))
         i += 1
     h = leaky_relu(h @ p["liner1.weight"].t() + p["liner1.bias"])
     h = h @ p["liner2.weight"].t() + p["liner2.bias"]
@@ -270,12 +284,13 @@ def adam_step_torch110(params, grads, exp_avg, exp_avg_sq, step: int, lr: float,
 
 # ---------------------------------------------------------------- one training step
 def train_step(g: OracleGraph, x: torch.Tensor, labels: torch.Tensor, train_index,
-               i_weight, p: Dict[str, torch.Tensor], use_weight: bool = False
-               ) -> Tuple[torch.Tensor, torch.Tensor, Dict[str, torch.Tensor]]:
+               i_weight, p: Dict[str, torch.Tensor], use_weight: bool = False,
+               parallel: bool = False) -> Tuple[torch.Tensor, torch.Tensor, Dict[str, torch.Tensor]]:
     """zero_grad -> forward -> multi_loss(train rows) -> backward (code/train.py:197-204).
-    Returns (logits, loss, grads)."""
+    Returns (logits, loss, grads). parallel=True runs the message passing as DGL's CPU
+    backend does (OpenMP rows forward, torch scatter_add_ backward): the CPU baseline."""
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
-    logits = gnn32_forward(g, x, leaves, use_weight)
+    logits = gnn32_forward(g, x, leaves, use_weight, parallel)
     loss = multi_loss(logits[train_index], labels[train_index], i_weight)
     loss.backward()
     return logits.detach(), loss.detach(), {k: v.grad.detach() for k, v in leaves.items()}
@@ -302,9 +317,11 @@ def edge_clustering_coefficients(ppi_net, epsilon: float = 0.0):
     return coo_matrix((vals[:m], (rows[:m], cols[:m])), shape=csr.shape)
 
 
-def protein_loc_correction(loc_proba: torch.Tensor, alpha: float) -> torch.Tensor:
-    """code/train.py:19-39, the same torch-CPU float32 operations (rows vectorised; the
-    per-row threshold loop of the reference is a row-wise comparison)."""
+def protein_loc_correction(loc_proba: torch.Tensor, alpha: float, rowwise: bool = False) -> torch.Tensor:
+    """code/train.py:19-39, the same torch-CPU float32 operations. By default the per-row
+    threshold loop of the reference is one row-wise comparison; rowwise=True keeps the
+    reference's Python loop over the rows (train.py:36-38: same result, its cost), which
+    bench.py times for the reference-faithful epoch."""
     loc_proba = loc_proba.detach().cpu().float()
     min_proba = loc_proba.min(dim=0).values
     max_proba = loc_proba.max(dim=0).values
@@ -314,6 +331,11 @@ def protein_loc_correction(loc_proba: torch.Tensor, alpha: float) -> torch.Tenso
     rmax = new_proba.max(dim=1).values
     rmin = new_proba.min(dim=1).values
     thresholds = rmax - (rmax - rmin) * alpha
+    if rowwise:
+        loc_pred = torch.zeros(loc_proba.shape)
+        for row in range(len(loc_proba)):
+            loc_pred[row][new_proba[row] > thresholds[row]] = 1.
+        return loc_pred.double()
     return (new_proba > thresholds.reshape(-1, 1)).double()
 
 

@@ -138,3 +138,37 @@ void oracle_spmm_sum(const int64_t* indptr, const int64_t* indices, const int64_
       for (int64_t f = 0; f < F; ++f) o[f] = o[f] / (float)d;
   }
 }
+
+/* The same SpMMCmpCsr<copy_lhs|u_mul_e, Max> loop, row-parallel with OpenMP as DGL's CPU
+ * backend runs it (runtime::parallel_for over destination rows): the CPU BASELINE timed
+ * by bench.py's cpu_baseline leg. Each row is computed exactly as in oracle_spmm_max, so
+ * the results are identical. */
+void oracle_spmm_max_omp(const int64_t* indptr, const int64_t* indices, const int64_t* eids,
+                         const float* w, const float* X, int64_t n_dst, int64_t F, float* out,
+                         int64_t* argx, int64_t* arge) {
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t v = 0; v < n_dst; ++v) {
+    float* o = out + v * F;
+    int64_t* ax = argx + v * F;
+    int64_t* ae = arge + v * F;
+    for (int64_t f = 0; f < F; ++f) {
+      o[f] = -INFINITY;
+      ax[f] = 0;
+      ae[f] = 0;
+    }
+    for (int64_t j = indptr[v]; j < indptr[v + 1]; ++j) {
+      const int64_t u = indices[j];
+      const int64_t e = eids[j];
+      for (int64_t f = 0; f < F; ++f) {
+        const float val = w ? X[u * F + f] * w[e] : X[u * F + f];
+        if (o[f] < val) {
+          o[f] = val;
+          ax[f] = u;
+          ae[f] = e;
+        }
+      }
+    }
+    for (int64_t f = 0; f < F; ++f)
+      if (isinf(o[f])) o[f] = 0.f;
+  }
+}

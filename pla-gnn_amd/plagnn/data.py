@@ -170,6 +170,41 @@ def make_dataset(kind: str = "s0", n: Optional[int] = None, seed: int = 70,
     return Dataset(n, row, col, expr, gcn, ecc, labels(n, seed))
 
 
+def random_perturbation(ds: Dataset, seed: int, frac: float = 0.03):
+    """SURVEY.md §8d cfg3 topology: about `frac` of the undirected edges removed and as many
+    random ones added (the size of a ΔPCC-style change, code/data_preprocess.py:217-257).
+    Returns the symmetric (row, col) int64 edge list, no self-loops, no duplicates."""
+    rng = np.random.default_rng(seed)
+    n = ds.n
+    r, c = ds.row.astype(np.int64), ds.col.astype(np.int64)
+    up = r < c
+    ur, uc = r[up], c[up]
+    keep = rng.random(len(ur)) >= frac
+    na = int((~keep).sum())
+    ar, ac = rng.integers(0, n, na), rng.integers(0, n, na)
+    lo, hi = _symmetrize_unique(np.concatenate([ur[keep], ar]), np.concatenate([uc[keep], ac]), n)
+    return np.concatenate([lo, hi]), np.concatenate([hi, lo])
+
+
+# The three drug datasets of the reference and their ΔPCC thresholds
+# (code/data_preprocess.py:498, 511, 520); main_inter.py trains on <GSE>/PPI_inter.npz.
+GSE_THRESHOLDS = {"GSE30931": 2.75, "GSE27182": 2.99, "GSE74572": 2.91}
+
+
+def intervention_expression(ds: Dataset, gse: str, n_genes: int = 2) -> np.ndarray:
+    """Synthetic 'intervention' expression for one dataset: the normal expression with
+    `n_genes` expressed genes (seeded by the GSE number) rescaled per sample by
+    exp(N(0, 1)). With the reference's thresholds every such gene moves about 0.3 N
+    correlation pairs past mean ± thr·std, so two genes change about 2-3 % of S0's edges
+    (measured on the reference's own operations at N = 3 000)."""
+    rng = np.random.default_rng(int(gse[3:]))
+    expressed = np.nonzero(ds.expr.sum(1) > 0)[0]
+    genes = rng.choice(expressed, n_genes, replace=False)
+    inter = ds.expr.copy()
+    inter[genes] *= np.exp(rng.standard_normal((n_genes, ds.expr.shape[1])))
+    return inter
+
+
 def write_reference_layout(ds: Dataset, root: str, gse: str = "GSE30931") -> None:
     """Write ds under root/data/generate_materials/ exactly where main_normal.py /
     main_inter.py / train.py read (code/main_normal.py:57-63, code/train.py:128, 151, 154)."""

@@ -301,11 +301,13 @@ class TrainEngine:
 
     def kernel_breakdown(self, reps: int = 5) -> Dict[str, Dict[str, float]]:
         """Per-launch-site mean duration (ms) and work over `reps` eager steps, timed with
-        HIP events on the launch stream. Returns {name: {ms, work, calls}} per step."""
+        HIP events on the launch stream. Returns {name: {ms, work, calls}} per step. A
+        diagnostic of this process alone: the steps run without the gradient all-reduce
+        (the other ranks take no part in them)."""
         acc: Dict[str, List[float]] = defaultdict(lambda: [0.0, 0.0, 0])
         for _ in range(reps):
             self._timing = []
-            self.step_eager(self.allreduce)
+            self.step_eager(None)
             torch.cuda.synchronize(self.device)
             for name, work, a, b in self._timing:
                 r = acc[name]

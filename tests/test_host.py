@@ -183,3 +183,22 @@ def test_gnn32_cpu_forward_backward_matches_oracle(oracle_mod):
     torch.testing.assert_close(loss.detach(), ref_loss, rtol=1e-5, atol=1e-6)
     for name, prm in model.named_parameters():
         torch.testing.assert_close(prm.grad, ref_grads[name], rtol=1e-4, atol=1e-5, msg=name)
+
+
+def test_workload_generators():
+    """cfg3's ±3 % perturbation and cfg4's synthetic intervention expression (host side)."""
+    from plagnn import data, workload
+
+    ds = data.make_dataset("s0", n=3000, seed=70)
+    r, c = data.random_perturbation(ds, seed=1)
+    assert np.all(r != c)
+    key = np.sort(r * ds.n + c)
+    assert np.array_equal(key, np.sort(c * ds.n + r)) and len(np.unique(key)) == len(key)
+    old = set((ds.row.astype(np.int64) * ds.n + ds.col).tolist())
+    changed = len(set(key.tolist()) ^ old) / len(old)
+    assert 0.03 < changed < 0.09, changed
+    for gse in data.GSE_THRESHOLDS:
+        inter = data.intervention_expression(ds, gse)
+        diff = np.nonzero(np.any(inter != ds.expr, axis=1))[0]
+        assert len(diff) == 2 and np.all(ds.expr[diff].sum(1) > 0)
+    assert workload.CFG4_VARIANTS[0] == "normal" and len(workload.CFG4_VARIANTS) == 4

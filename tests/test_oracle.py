@@ -207,3 +207,35 @@ def test_pca_oracle_matches_reference_golden(oracle_mod):
     assert np.all(np.abs(a - gold).max(axis=0) <= 1e-9 * scale)
     idx = np.abs(got).argmax(axis=0)
     assert np.all(got[idx, np.arange(nc)] > 0)
+
+
+def test_parallel_oracle_step_equals_serial(oracle_mod):
+    """The CPU baseline's form of the oracle (OpenMP rows forward, torch scatter_add_
+    backward, as DGL's CPU backend runs them) computes the same step: the forward is a
+    selection (bit-exact), the backward sums the same terms."""
+    from conftest import random_graph
+
+    src, dst = random_graph(300, 3000, seed=5, self_loop=False)
+    dims = [20, 16, 12, 8, 6, 12]
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(rng.standard_normal((300, dims[0])).astype(np.float32))
+    labels = torch.from_numpy((rng.random((300, 12)) < 0.3).astype(np.float32))
+    w = np.linspace(0.5, 2.0, 12)
+    ew = rng.random(len(src)).astype(np.float32)
+    p = oracle_mod.init_params(dims, seed=4)
+    for weight in (None, ew):
+        og = oracle_mod.OracleGraph(src, dst, 300, edge_weight=weight)
+        a = oracle_mod.train_step(og, x, labels, list(range(0, 300, 2)), w, p, use_weight=weight is not None)
+        b = oracle_mod.train_step(og, x, labels, list(range(0, 300, 2)), w, p, use_weight=weight is not None,
+                                  parallel=True)
+        assert torch.equal(a[0], b[0])
+        for k in a[2]:
+            torch.testing.assert_close(a[2][k], b[2][k], rtol=1e-5, atol=1e-7)
+
+
+def test_rowwise_loc_correction_equals_vectorised(oracle_mod):
+    rng = np.random.default_rng(0)
+    proba = torch.from_numpy(rng.random((500, 12)).astype(np.float32))
+    for alpha in (0.1, 0.5):
+        assert torch.equal(oracle_mod.protein_loc_correction(proba, alpha),
+                           oracle_mod.protein_loc_correction(proba, alpha, rowwise=True))
