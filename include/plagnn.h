@@ -170,33 +170,6 @@ int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, i
                     const float* mask_src, int64_t ldm, const float* fwd_out, int64_t ldf,
                     float* dx, int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream);
 
-/* Grouped mode (what TrainEngine runs): the forward also builds the backward's winner
- * lists, so the backward needs no argmax pass of its own. Same out[] as pg_spmm_max_fwd.
- * Features go in tiles of 256 columns; T = pg_spmm_group_tiles(F) tiles. For every row v,
- * tile t (columns f0 = 256 t ...) and in-row position p, the features f - f0 whose winner is
- * p and whose stored maximum out[v,f] is not 0 form one list:
- *   gfeat[v F + f0 + ...]          the lists of row v in tile t, grouped by p (u16, N x F),
- *   glist[2 (t nnz + einv[ptr[v] + p]) + {0, 1}] = {offset into gfeat, length},
- *   rcnt[t N + v]                  the row's entry count in tile t.
- * A zero maximum is left out (its winner u has X[u,f] * w == 0: with the relu' mask of
- * pg_spmm_max_bwd_grouped it contributes nothing; pg_spmm_max_bwd's fwd_out rule).
- * argpos (u16, N x F) is scratch here: only rows split by the schedule write it.
- * Needs g->einv, a schedule chunk <= 256, max degree < 65535, N F < 2^31, F and the
- * leading dims multiples of 4, X / out 16-B aligned; else PG_ERR_UNSUPPORTED.
- * Workspace: pg_spmm_max_fwd_workspace(g, F, PG_ARG_U16). */
-int64_t pg_spmm_group_tiles(int64_t F);
-int pg_spmm_max_fwd_grouped(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
-                            int64_t ldo, void* argpos, int64_t lda, uint16_t* gfeat, int32_t* glist,
-                            int32_t* rcnt, void* ws, size_t ws_bytes, pg_stream_t stream);
-/* dx[u,f] = sum over the lists of u's out-edges (ascending destination v) of ew * dout[v,f],
- * then dx *= (mask_src > 0) when mask_src != NULL (it must be, for lists that left zero
- * maxima out, unless X has no zeros). Bitwise the same as pg_spmm_max_bwd with fwd_out. */
-size_t pg_spmm_max_bwd_grouped_workspace(const pg_csr_t* gt, int64_t F);
-int pg_spmm_max_bwd_grouped(const pg_csr_t* g, const pg_csr_t* gt, const uint16_t* gfeat,
-                            const int32_t* glist, const int32_t* rcnt, const float* dout, int64_t ldd,
-                            int64_t F, const float* mask_src, int64_t ldm, float* dx, int64_t ldx,
-                            void* ws, size_t ws_bytes, pg_stream_t stream);
-
 /* DGL-form backward: dx = 0; dx[src(argpos[v,f]), f] += ew * dout[v,f] with f32
  * atomics (summation order not reproducible). The callee zero-fills dx. */
 int pg_spmm_max_bwd_scatter(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,
@@ -281,11 +254,6 @@ typedef struct pg_gemm_epilogue {
   int64_t lddact;
   float* rowsum;     /* if not NULL: rowsum[m] = sum_k op(A)[m][k] (overwritten). For a weight
                         gradient dY^T X (transa) these are the bias gradients sum_nodes dY. */
-  uint32_t* splitk_cnt; /* pg_gemm_f32 with split_k > 1 (optional): pg_gemm_splitk_counters(M, N)
-                        u32 tile counters, zero before the first call and left zero by every call
-                        (one set per concurrently running call). With them the partial slabs are
-                        summed inside the GEMM by the last workgroup of each tile (slice order
-                        0, 1, ...: deterministic) instead of by a second launch. */
 } pg_gemm_epilogue_t;
 
 /* C[M,N] = alpha * op(A) * op(B) + beta * C, then the epilogue.
@@ -297,7 +265,6 @@ typedef struct pg_gemm_epilogue {
  * about five 64 x 64 workgroups per CU, each slice >= 96 entries of K, at most 256. */
 int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K);
 size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k);
-int64_t pg_gemm_splitk_counters(int64_t M, int64_t N);
 /* Deferred split-K: pg_gemm_f32_partials runs the split product (C = op(A) op(B), rowsum
  * allowed, nothing else) and leaves the partial slabs in ws (layout of pg_gemm_f32:
  * split_used slabs of M x N, then split_used row-sum slices of M); *split_used = the slice
@@ -350,15 +317,6 @@ int pg_spmm_max_bwd_bf16(const pg_csr_t* g, const pg_csr_t* gt, const void* argp
                          int arg_kind, const void* dout, int64_t ldd, int64_t F,
                          const void* mask_src, int64_t ldm, const void* fwd_out, int64_t ldf,
                          void* dx, int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream);
-/* The grouped pair on bf16 features (lists as above; dx accumulated in f32, rounded once). */
-int pg_spmm_max_fwd_grouped_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t F, void* out,
-                                 int64_t ldo, void* argpos, int64_t lda, uint16_t* gfeat,
-                                 int32_t* glist, int32_t* rcnt, void* ws, size_t ws_bytes,
-                                 pg_stream_t stream);
-int pg_spmm_max_bwd_grouped_bf16(const pg_csr_t* g, const pg_csr_t* gt, const uint16_t* gfeat,
-                                 const int32_t* glist, const int32_t* rcnt, const void* dout,
-                                 int64_t ldd, int64_t F, const void* mask_src, int64_t ldm, void* dx,
-                                 int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream);
 /* dst[i] = bf16(src[map ? map[i] : i]) (map[i] < 0: 0), round to nearest even: the bf16
  * weight copies of the f32 master parameters, in any layout the GEMMs want. */
 int pg_cast_f32_bf16(const float* src, const int32_t* map, int64_t n, void* dst, pg_stream_t stream);
@@ -451,7 +409,8 @@ int pg_perturb_fill(const double* xc_normal, const double* xc_inter, const doubl
 
 /* ---------------- misc ---------------- */
 const char* pg_last_error_string(void);
-int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 4: epilogue splitk_cnt */
+int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-kernel split-K
+                         (epilogue without splitk_cnt), no grouped SpMM pair */
 
 #ifdef __cplusplus
 }

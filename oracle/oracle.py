@@ -67,6 +67,17 @@ def lib():
         L.oracle_spmm_max.restype = None
         L.oracle_spmm_max_omp.argtypes = L.oracle_spmm_max.argtypes
         L.oracle_spmm_max_omp.restype = None
+        _d = ctypes.POINTER(ctypes.c_double)
+        L.oracle_spmm_max_f64.argtypes = [_i64p, _i64p, _i64p, _d, _d, ctypes.c_int64, ctypes.c_int64, _d, _i64p,
+                                          _i64p]
+        L.oracle_spmm_max_f64.restype = None
+        _i32p = ctypes.POINTER(ctypes.c_int32)
+        L.oracle_spmm_max_align.argtypes = [_i64p, _i64p, _i64p, _f32p, _f32p, ctypes.c_int64, ctypes.c_int64,
+                                            _i32p, ctypes.c_double, _f32p, _i64p, _i64p]
+        L.oracle_spmm_max_align.restype = ctypes.c_int64
+        L.oracle_spmm_max_align_f64.argtypes = [_i64p, _i64p, _i64p, _d, _d, ctypes.c_int64, ctypes.c_int64, _i32p,
+                                                ctypes.c_double, _d, _i64p, _i64p]
+        L.oracle_spmm_max_align_f64.restype = ctypes.c_int64
         L.oracle_spmm_max_bwd.argtypes = [_i64p, _i64p, _f32p, _f32p, _u8p, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.c_int64, _f32p]
         L.oracle_spmm_max_bwd.restype = None
@@ -132,6 +143,17 @@ class OracleGraph:
 def spmm_max(g: OracleGraph, X: np.ndarray, use_weight: bool = False, parallel: bool = False):
     """parallel=True: the OpenMP row-parallel form of the same loop (DGL's CPU backend;
     the timed CPU baseline), identical results."""
+    if X.dtype == np.float64:  # the exact-arithmetic yardstick (row-parallel)
+        X = np.ascontiguousarray(X)
+        F = X.shape[1]
+        out = np.empty((g.n, F), np.float64)
+        argx = np.empty((g.n, F), np.int64)
+        arge = np.empty((g.n, F), np.int64)
+        w = g.ew.astype(np.float64) if use_weight else None
+        d = ctypes.POINTER(ctypes.c_double)
+        lib().oracle_spmm_max_f64(_p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p), _p(w, d),
+                                  _p(X, d), g.n, F, _p(out, d), _p(argx, _i64p), _p(arge, _i64p))
+        return out, argx, arge
     X = np.ascontiguousarray(X, np.float32)
     F = X.shape[1]
     out = np.empty((g.n, F), np.float32)
@@ -165,26 +187,50 @@ def spmm_sum(g: OracleGraph, X: np.ndarray, mean: bool = False, use_weight: bool
     return out
 
 
+def spmm_max_align(g: OracleGraph, X: np.ndarray, use_weight: bool, hint: np.ndarray, tol: float,
+                   out, argx, arge) -> int:
+    """In place: entries where `hint` (another computation's winning in-row positions,
+    -1 = none) names a candidate within tol * max|out| of the maximum take it (see
+    oracle_spmm_max_align). Returns the number of changed entries."""
+    hint = np.ascontiguousarray(hint, np.int32)
+    F = X.shape[1]
+    tol = float(tol) * float(np.abs(out).max(initial=0.0))
+    if X.dtype == np.float64:
+        d = ctypes.POINTER(ctypes.c_double)
+        w = g.ew.astype(np.float64) if use_weight else None
+        return int(lib().oracle_spmm_max_align_f64(
+            _p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p), _p(w, d), _p(X, d), g.n, F,
+            _p(hint, ctypes.POINTER(ctypes.c_int32)), tol, _p(out, d), _p(argx, _i64p), _p(arge, _i64p)))
+    w = g.ew if use_weight else None
+    return int(lib().oracle_spmm_max_align(
+        _p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p), _p(w, _f32p), _p(X, _f32p), g.n, F,
+        _p(hint, ctypes.POINTER(ctypes.c_int32)), tol, _p(out, _f32p), _p(argx, _i64p), _p(arge, _i64p)))
+
+
 class _MaxAggregate(torch.autograd.Function):
     """update_all(copy_u|u_mul_e, max) with DGL's GSpMM backward (scatter_add_ on argX)."""
 
     @staticmethod
-    def forward(ctx, P, g, use_weight, parallel=False):
-        out, argx, arge = spmm_max(g, P.detach().numpy(), use_weight, parallel)
+    def forward(ctx, P, g, use_weight, parallel=False, align=None):
+        Xn = np.ascontiguousarray(P.detach().numpy())
+        out, argx, arge = spmm_max(g, Xn, use_weight, parallel)
+        if align is not None:  # (hint positions, tol, signs dict for the count)
+            hint, tol, counts = align
+            counts["_ties"] = counts.get("_ties", 0) + spmm_max_align(g, Xn, use_weight, hint, tol, out, argx, arge)
         ctx.g, ctx.argx, ctx.arge, ctx.use_weight, ctx.parallel = g, argx, arge, use_weight, parallel
         return torch.from_numpy(out)
 
     @staticmethod
     def backward(ctx, dZ):
-        if ctx.parallel:
+        if ctx.parallel or dZ.dtype == torch.float64:
             # DGL's own form: dX = zeros; dX.scatter_add_(0, argX, dZ [* w[argE]]) in torch-CPU
             dZ = dZ.contiguous()
             if ctx.use_weight:
-                dZ = dZ * torch.from_numpy(ctx.g.ew)[torch.from_numpy(ctx.arge)]
+                dZ = dZ * torch.from_numpy(ctx.g.ew).to(dZ.dtype)[torch.from_numpy(ctx.arge)]
             dX = torch.zeros_like(dZ).scatter_add_(0, torch.from_numpy(ctx.argx), dZ)
-            return dX, None, None, None
+            return dX, None, None, None, None
         dX = spmm_max_bwd(ctx.g, ctx.argx, ctx.arge, dZ.contiguous().numpy(), ctx.use_weight)
-        return torch.from_numpy(dX), None, None, None
+        return torch.from_numpy(dX), None, None, None, None
 
 
 # ---------------------------------------------------------------- model (code/model.py)
@@ -192,26 +238,57 @@ def leaky_relu(x):
     return torch.nn.functional.leaky_relu(x)  # negative_slope 0.01 (model.py:21,23,25,27)
 
 
+# Winner alignment band (spmm_max_align): a fraction of the aggregation's largest |value|.
+# Float32 GEMM rounding moves P by ~1e-7 of that scale; near-ties seen differing between the
+# engine and this oracle sat within 4e-8 of it.
+WINNER_TOL = 1e-6
+
+
+def _act(pre, slope, site, signs, sign_tol):
+    """relu (slope 0) / leaky_relu of `pre`. With `signs` (site -> the other computation's
+    "output > 0" mask), entries whose pre-activation lies within sign_tol * max|pre| of zero
+    take that decision instead of their own: there the derivative (1 or slope) is decided by
+    float32 rounding, not by the algorithm. signs["_flips"] counts the entries whose decision
+    changed."""
+    if signs is None or site not in signs:
+        return torch.relu(pre) if slope == 0.0 else torch.nn.functional.leaky_relu(pre, slope)
+    with torch.no_grad():
+        own = pre > 0
+        tiny = pre.abs() <= sign_tol * pre.abs().max()
+        pos = torch.where(tiny, signs[site].to(own.device), own)
+        signs["_flips"] = signs.get("_flips", 0) + int((pos != own).sum())
+    return torch.where(pos, pre, pre * slope)
+
+
 def sage_pool(g: OracleGraph, h: torch.Tensor, p: Dict[str, torch.Tensor], prefix: str,
-              use_weight: bool = False, parallel: bool = False) -> torch.Tensor:
+              use_weight: bool = False, parallel: bool = False, signs=None, sign_tol: float = 0.0
+              ) -> torch.Tensor:
     """DGL 0.8.2 SAGEConv(aggregator_type='pool', feat_drop=0, bias=True, norm=None,
     activation=None).forward(graph, feat[, edge_weight])."""
-    P = torch.relu(h @ p[prefix + "fc_pool.weight"].t() + p[prefix + "fc_pool.bias"])
-    neigh = _MaxAggregate.apply(P, g, use_weight, parallel)
+    P = _act(h @ p[prefix + "fc_pool.weight"].t() + p[prefix + "fc_pool.bias"], 0.0, prefix + "pool", signs,
+             sign_tol)
+    align = None
+    if signs is not None and prefix + "argpos" in signs:
+        align = (signs[prefix + "argpos"], WINNER_TOL, signs)
+    neigh = _MaxAggregate.apply(P, g, use_weight, parallel, align)
     h_neigh = neigh @ p[prefix + "fc_neigh.weight"].t()
     rst = h @ p[prefix + "fc_self.weight"].t() + h_neigh
     return rst + p[prefix + "bias"]
 
 
 def gnn32_forward(g: OracleGraph, x: torch.Tensor, p: Dict[str, torch.Tensor],
-                  use_weight: bool = False, parallel: bool = False) -> torch.Tensor:
-    """GNN32.forward (code/model.py:19-31), generalised to any number of conv layers."""
+                  use_weight: bool = False, parallel: bool = False, signs=None,
+                  sign_tol: float = 0.0) -> torch.Tensor:
+    """GNN32.forward (code/model.py:19-31), generalised to any number of conv layers.
+    Activation sites for `signs`: conv<i>.pool (relu of fc_pool), conv<i>.out (the layer's
+    leaky_relu), liner1."""
     h = x
     i = 1
     while f"conv{i}.fc_pool.weight" in p:
-        h = leaky_relu(sage_pool(g, h, p, f"conv{i}.", use_weight, parallel))
+        h = _act(sage_pool(g, h, p, f"conv{i}.", use_weight, parallel, signs, sign_tol), 0.01, f"conv{i}.out",
+                 signs, sign_tol)
         i += 1
-    h = leaky_relu(h @ p["liner1.weight"].t() + p["liner1.bias"])
+    h = _act(h @ p["liner1.weight"].t() + p["liner1.bias"], 0.01, "liner1", signs, sign_tol)
     h = h @ p["liner2.weight"].t() + p["liner2.bias"]
     return torch.sigmoid(h)
 
@@ -285,12 +362,22 @@ def adam_step_torch110(params, grads, exp_avg, exp_avg_sq, step: int, lr: float,
 # ---------------------------------------------------------------- one training step
 def train_step(g: OracleGraph, x: torch.Tensor, labels: torch.Tensor, train_index,
                i_weight, p: Dict[str, torch.Tensor], use_weight: bool = False,
-               parallel: bool = False) -> Tuple[torch.Tensor, torch.Tensor, Dict[str, torch.Tensor]]:
+               parallel: bool = False, dtype=torch.float32, signs=None, sign_tol: float = 1e-5
+               ) -> Tuple[torch.Tensor, torch.Tensor, Dict[str, torch.Tensor]]:
     """zero_grad -> forward -> multi_loss(train rows) -> backward (code/train.py:197-204).
     Returns (logits, loss, grads). parallel=True runs the message passing as DGL's CPU
-    backend does (OpenMP rows forward, torch scatter_add_ backward): the CPU baseline."""
+    backend does (OpenMP rows forward, torch scatter_add_ backward): the CPU baseline.
+    dtype=torch.float64 computes the same step in double precision (the yardstick the
+    full-size tests use to judge two float32 results that differ by more than 1e-4).
+    signs: see _act — the activation decisions of another computation at pre-activations
+    within sign_tol * max|pre| of zero; "conv<i>.argpos" entries (N x F int32 in-row
+    positions) do the same for the max aggregation's winners (spmm_max_align)."""
+    if dtype != torch.float32:  # the float64 yardstick: every tensor and product in double
+        x = x.to(dtype)
+        p = {k: v.to(dtype) for k, v in p.items()}
+        labels = labels.to(dtype)
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
-    logits = gnn32_forward(g, x, leaves, use_weight, parallel)
+    logits = gnn32_forward(g, x, leaves, use_weight, parallel, signs, sign_tol)
     loss = multi_loss(logits[train_index], labels[train_index], i_weight)
     loss.backward()
     return logits.detach(), loss.detach(), {k: v.grad.detach() for k, v in leaves.items()}

@@ -172,3 +172,93 @@ void oracle_spmm_max_omp(const int64_t* indptr, const int64_t* indices, const in
       if (isinf(o[f])) o[f] = 0.f;
   }
 }
+
+/* float64 form of the same loop (copy_lhs|u_mul_e, Max): the exact-arithmetic yardstick
+ * the full-size parity tests use where two float32 computations differ by more than the
+ * 1e-4 bar. Row-parallel; each row is independent. */
+void oracle_spmm_max_f64(const int64_t* indptr, const int64_t* indices, const int64_t* eids,
+                         const double* w, const double* X, int64_t n_dst, int64_t F, double* out,
+                         int64_t* argx, int64_t* arge) {
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t v = 0; v < n_dst; ++v) {
+    double* o = out + v * F;
+    int64_t* ax = argx + v * F;
+    int64_t* ae = arge + v * F;
+    for (int64_t f = 0; f < F; ++f) {
+      o[f] = -INFINITY;
+      ax[f] = 0;
+      ae[f] = 0;
+    }
+    for (int64_t j = indptr[v]; j < indptr[v + 1]; ++j) {
+      const int64_t u = indices[j];
+      const int64_t e = eids[j];
+      for (int64_t f = 0; f < F; ++f) {
+        const double val = w ? X[u * F + f] * w[e] : X[u * F + f];
+        if (o[f] < val) {
+          o[f] = val;
+          ax[f] = u;
+          ae[f] = e;
+        }
+      }
+    }
+    for (int64_t f = 0; f < F; ++f)
+      if (isinf(o[f])) o[f] = 0.0;
+  }
+}
+
+/* Decision alignment for parity tests: after oracle_spmm_max[_f64] has run, entries where
+ * another computation picked a different winning edge (`hint`: in-row positions of the
+ * in-CSR, n_dst x F, -1 = none) whose value is within `tol` of the maximum (an absolute
+ * band: the caller passes a fraction of the layer's largest |value|, the scale of the
+ * float32 rounding of the values compared) take that winner instead. Which of two
+ * candidates this close wins is decided by that rounding, not by the algorithm. Returns
+ * the number of changed entries. */
+int64_t oracle_spmm_max_align(const int64_t* indptr, const int64_t* indices, const int64_t* eids,
+                              const float* w, const float* X, int64_t n_dst, int64_t F,
+                              const int32_t* hint, double tol, float* out, int64_t* argx,
+                              int64_t* arge) {
+  int64_t changed = 0;
+  for (int64_t v = 0; v < n_dst; ++v) {
+    for (int64_t f = 0; f < F; ++f) {
+      const int32_t p = hint[v * F + f];
+      if (p < 0 || p >= indptr[v + 1] - indptr[v]) continue;
+      const int64_t j = indptr[v] + p;
+      const int64_t u = indices[j], e = eids[j];
+      if (u == argx[v * F + f] && e == arge[v * F + f]) continue;
+      const float val = w ? X[u * F + f] * w[e] : X[u * F + f];
+      const float m = out[v * F + f];
+      if ((double)m - (double)val <= tol) {
+        out[v * F + f] = val;
+        argx[v * F + f] = u;
+        arge[v * F + f] = e;
+        ++changed;
+      }
+    }
+  }
+  return changed;
+}
+
+int64_t oracle_spmm_max_align_f64(const int64_t* indptr, const int64_t* indices, const int64_t* eids,
+                                  const double* w, const double* X, int64_t n_dst, int64_t F,
+                                  const int32_t* hint, double tol, double* out, int64_t* argx,
+                                  int64_t* arge) {
+  int64_t changed = 0;
+  for (int64_t v = 0; v < n_dst; ++v) {
+    for (int64_t f = 0; f < F; ++f) {
+      const int32_t p = hint[v * F + f];
+      if (p < 0 || p >= indptr[v + 1] - indptr[v]) continue;
+      const int64_t j = indptr[v] + p;
+      const int64_t u = indices[j], e = eids[j];
+      if (u == argx[v * F + f] && e == arge[v * F + f]) continue;
+      const double val = w ? X[u * F + f] * w[e] : X[u * F + f];
+      const double m = out[v * F + f];
+      if (m - val <= tol) {
+        out[v * F + f] = val;
+        argx[v * F + f] = u;
+        arge[v * F + f] = e;
+        ++changed;
+      }
+    }
+  }
+  return changed;
+}

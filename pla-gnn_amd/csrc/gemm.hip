@@ -45,15 +45,15 @@ constexpr int BK = 32;
 constexpr int HK = BK / 2;  // k-values per lane half per K step
 constexpr int kThreads = 256;
 constexpr int KPAD = BK + 4;  // [row][k] image row stride (floats)
-#ifndef PG_GEMM_DB
-#define PG_GEMM_DB 0
+// Compile-time tuning knobs (variant builds only: make variant VFLAGS=-D...; the shipped
+// library reads nothing from the environment):
+//   PG_GEMM_TILE_FORCE = BM * 1000 + BN forces one tile (64|128 each), 0 = the heuristic;
+//   PG_SPLIT_TARGET    = workgroups a split-K product aims at (measured best: 1024).
+#ifndef PG_GEMM_TILE_FORCE
+#define PG_GEMM_TILE_FORCE 0
 #endif
-#ifndef PG_GEMM_PIPE
-#define PG_GEMM_PIPE 0
-#endif
-constexpr int kBufs = (PG_GEMM_DB || PG_GEMM_PIPE) ? 2 : 1;  // LDS images per operand
-#ifndef PG_GEMM_X
-#define PG_GEMM_X 0  // experiment only: 1 = no in-loop staging (wrong results; timing ceiling)
+#ifndef PG_SPLIT_TARGET
+#define PG_SPLIT_TARGET 1024
 #endif
 #ifndef PG_GEMM_STAMP
 #define PG_GEMM_STAMP 0  // probe builds only: per-workgroup clock stamps (scripts/probes)
@@ -62,17 +62,6 @@ constexpr int kBufs = (PG_GEMM_DB || PG_GEMM_PIPE) ? 2 : 1;  // LDS images per o
 __device__ unsigned long long pg_gemm_stamp[65536][4];
 __device__ unsigned long long pg_gemm_kstamp[64][64];  // shader clock at each K-step barrier
 __device__ unsigned long long pg_gemm_kphase[64][4];   // start, prologue done, loop done, end
-#endif
-#ifndef PG_GEMM_SCHED
-#define PG_GEMM_SCHED 0
-#endif
-#ifndef PG_GEMM_PRIO
-#define PG_GEMM_PRIO 0  // 1 = s_setprio(1) around each MFMA cluster
-#endif
-#ifndef PG_GEMM_XP
-#define PG_GEMM_XP 0  // experiment only (wrong results): 1 no in-loop DMA, 2 no MFMA, 4 no epilogue;
-                      // 8 / 16: stagger co-resident workgroups by 1024 / 512 cycles per slot;
-                      // 32: every K tile's DMA issued twice (issue cost vs latency)
 #endif
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
@@ -171,27 +160,16 @@ __device__ __forceinline__ void read_frag(const float* __restrict__ S, int rc, i
   }
 }
 
-// 4 k-values (chunk q of lane half h: k = 16 h + 4 q + 0..3) for row/col `rc`.
-template <int ROWS, bool KMAJ>
-__device__ __forceinline__ void read_chunk(const float* __restrict__ S, int rc, int h, int q,
-                                           float (&f)[4]) {
-  const int kb = h * HK + 4 * q;
-  if constexpr (!KMAJ) {
-    const float4 t = *reinterpret_cast<const float4*>(S + rc * KPAD + kb);
-    f[0] = t.x; f[1] = t.y; f[2] = t.z; f[3] = t.w;
-  } else {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) f[s] = S[(kb + s) * (ROWS + 4) + rc];
-  }
-}
-
 // Row sums of the A tile in LDS over its BK k-values: thread t owns row t % BM and the
-// k-values k = t / BM, t / BM + G, ... (G = 256 / BM groups).
+// k-values k = t / BM, t / BM + G, ... (G = 256 / BM groups). The row sums are bias
+// gradients, sums over all nodes whose terms largely cancel: they accumulate in float64
+// (a float32 running sum over a K-slice of ~1000 nodes measured up to 1e-4 of the result
+// off), rounded to float32 once per slice.
 template <int BM, bool AK>
-__device__ __forceinline__ float tile_rowsum(const float* __restrict__ As, int tid) {
+__device__ __forceinline__ double tile_rowsum(const float* __restrict__ As, int tid) {
   constexpr int G = kThreads / BM;
   const int m = tid % BM, g = tid / BM;
-  float s = 0.f;
+  double s = 0.0;
 #pragma unroll
   for (int i = 0; i < BK / G; ++i) {
     const int k = g + i * G;
@@ -203,7 +181,7 @@ __device__ __forceinline__ float tile_rowsum(const float* __restrict__ As, int t
 // Row sums of op(A) (combined over the k-groups in order) and the epilogue of one tile.
 template <int BM, int BN, int EPI>
 __device__ __forceinline__ void finish_tile(
-    const f32x16 (&acc)[BM / 64][BN / 64], float rs, bool do_rs, float* __restrict__ rsred, int tid,
+    const f32x16 (&acc)[BM / 64][BN / 64], double rs, bool do_rs, double* __restrict__ rsred, int tid,
     int m0, int n0, int M, int N, float alpha, float beta, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias, float slope, const float* __restrict__ dact, int64_t lddact,
     float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum, int kz) {
@@ -216,10 +194,10 @@ __device__ __forceinline__ void finish_tile(
     rsred[tid] = rs;
     __syncthreads();
     if (tid < BM && m0 + tid < M) {
-      float t = 0.f;
+      double t = 0.0;
       for (int g = 0; g < kThreads / BM; ++g) t += rsred[g * BM + tid];
-      if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = t;
-      else rowsum[m0 + tid] = t;
+      if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = (float)t;
+      else rowsum[m0 + tid] = (float)t;
     }
   }
 
@@ -254,41 +232,25 @@ __device__ __forceinline__ void finish_tile(
 // (the staging images are free by now) and written out row-major with 16-B loads/stores,
 // instead of one 4-B store per lane and accumulator register. Needs N % 4 == 0 and 16-B
 // aligned C / ldc (and dact / bias when present).
-// sc1 (agent-scope) stores / loads of the split-K slabs combined inside the kernel
-// (MI355X_MICROARCH.md, inter-workgroup hand-offs: every store and load of the handed-off
-// bytes sc1, a counter add after each storing wave's vmcnt(0) wait, the last adder reads)
-using f32x4 = __attribute__((ext_vector_type(4))) float;
-constexpr int kSc1 = 16;  // cache-policy bit SC1 of the buffer intrinsics
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const float* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff, 0x00020000);
-}
-
 template <int BM, int BN, int EPI>
 __device__ __forceinline__ void finish_tile_lds(
-    const f32x16 (&acc)[BM / 64][BN / 64], float rs, bool do_rs, float* __restrict__ lds, int tid,
+    const f32x16 (&acc)[BM / 64][BN / 64], double rs, bool do_rs, float* __restrict__ lds, int tid,
     int m0, int n0, int M, int N, float alpha, float beta, float* __restrict__ C, int64_t ldc,
     const float* __restrict__ bias, float slope, const float* __restrict__ dact, int64_t lddact,
-    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum, int kz,
-    bool sc1 = false) {
+    float* __restrict__ rowsum, float* __restrict__ ws, float* __restrict__ ws_rowsum, int kz) {
   constexpr bool SPLIT = EPI == EPI_SPLIT;
   constexpr int TM = BM / 64, TN = BN / 64;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
   if (do_rs) {
-    lds[tid] = rs;
+    double* rsred = reinterpret_cast<double*>(lds);
+    rsred[tid] = rs;
     __syncthreads();
     if (tid < BM && m0 + tid < M) {
-      float t = 0.f;
-      for (int g = 0; g < kThreads / BM; ++g) t += lds[g * BM + tid];
-      if constexpr (SPLIT) {
-        if (sc1)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, t), slab_rsrc(ws_rowsum + (int64_t)kz * M),
-                                                (m0 + tid) * 4, 0, kSc1);
-        else
-          ws_rowsum[(int64_t)kz * M + m0 + tid] = t;
-      } else {
-        rowsum[m0 + tid] = t;
-      }
+      double t = 0.0;
+      for (int g = 0; g < kThreads / BM; ++g) t += rsred[g * BM + tid];
+      if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = (float)t;
+      else rowsum[m0 + tid] = (float)t;
     }
     __syncthreads();
   }
@@ -310,12 +272,7 @@ __device__ __forceinline__ void finish_tile_lds(
     if (gr >= M || gc >= N) continue;
     float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
     if constexpr (SPLIT) {
-      if (sc1) {
-        const f32x4 x = {v.x, v.y, v.z, v.w};
-        __builtin_amdgcn_raw_buffer_store_b128(x, slab_rsrc(ws + (int64_t)kz * M * N), (gr * N + gc) * 4, 0, kSc1);
-      } else {
-        *reinterpret_cast<float4*>(ws + ((int64_t)kz * M + gr) * N + gc) = v;
-      }
+      *reinterpret_cast<float4*>(ws + ((int64_t)kz * M + gr) * N + gc) = v;
     } else {
       float* cp = C + (int64_t)gr * ldc + gc;
       float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
@@ -353,6 +310,9 @@ __device__ __forceinline__ void stamp(unsigned long long st_rt, unsigned long lo
 }
 #endif
 
+// Fallback kernel for operands the LDS-DMA kernel cannot take (a row stride or extent that
+// is not a multiple of 4 floats, or a base address that is not 16-B aligned: the drop-in
+// path's 503-wide inputs): K tiles go global -> registers -> LDS, one image per operand.
 // TA: A stored K x M (use A^T). TB: B stored N x K (use B^T).
 template <int BM, int BN, bool TA, bool TB, bool VA, bool VB, int EPI>
 __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
@@ -364,9 +324,9 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
   constexpr bool AK = TA;    // A image k-major ([k][m]) when A is stored transposed
   constexpr bool BKM = !TB;  // B image k-major ([k][n]) when B is stored K x N
   constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
-  __shared__ __attribute__((aligned(16))) float As_[kBufs][image_floats<BM, AK>()];
-  __shared__ __attribute__((aligned(16))) float Bs_[kBufs][image_floats<BN, BKM>()];
-  __shared__ float rsred[kThreads];
+  __shared__ __attribute__((aligned(16))) float As_[image_floats<BM, AK>()];
+  __shared__ __attribute__((aligned(16))) float Bs_[image_floats<BN, BKM>()];
+  __shared__ double rsred[kThreads];
 
   // XCD-aware tile order: blocks b, b+8, ... share an XCD; give each such group a
   // contiguous run of tile ids (row-major over [tile_m][tile_n]).
@@ -379,9 +339,6 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-#if PG_GEMM_STAMP
-  unsigned long long st_rt = __builtin_amdgcn_s_memrealtime(), st_ck = __builtin_amdgcn_s_memtime();
-#endif
   const int m0 = tm * BM;
   const int n0 = tn * BN;
   const int kz0 = blockIdx.z * k_per_split;
@@ -389,7 +346,7 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
   const int h = lane >> 5;
   const int l32 = lane & 31;
   const bool do_rs = rowsum != nullptr && tn == 0;
-  float rs = 0.f;
+  double rs = 0.0;
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -401,92 +358,26 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
 
   TileLoader<BM, AK, VA> la;
   TileLoader<BN, BKM, VB> lb;
-
-#if PG_GEMM_PIPE
-  // Software pipeline: fragments are read in chunks of 4 k-values (one ds_read_b128 per
-  // 32-row tile) one chunk ahead of the MFMAs that use them, across K steps as well; the
-  // next K tile is staged into the other LDS image behind the third chunk's MFMAs, so one
-  // barrier per K step and the next step's first chunk read is covered by chunk 3.
   if (kz0 < kz1) {
     la.load(A, lda, m0, M, kz0, kz1, tid);
     lb.load(B, ldb, n0, N, kz0, kz1, tid);
-    la.store(As_[0], tid);
-    lb.store(Bs_[0], tid);
+    la.store(As_, tid);
+    lb.store(Bs_, tid);
     __syncthreads();
-    float fa[2][TM][4], fb[2][TN][4];
-    const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) read_chunk<BM, AK>(As_[0], ra + i * 32, h, 0, fa[0][i]);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) read_chunk<BN, BKM>(Bs_[0], rb + j * 32, h, 0, fb[0][j]);
-    int cur = 0;
     for (int k0 = kz0; k0 < kz1; k0 += BK) {
       const bool more = k0 + BK < kz1;
-      if (more) {
+      if (more) {  // the next tile's global loads overlap this tile's MFMAs
         la.load(A, lda, m0, M, k0 + BK, kz1, tid);
         lb.load(B, ldb, n0, N, k0 + BK, kz1, tid);
       }
-      const float* As = As_[cur];
-      const float* Bs = Bs_[cur];
-      if (do_rs) rs += tile_rowsum<BM, AK>(As, tid);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int u = q & 1;
-        if (q < 3) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i) read_chunk<BM, AK>(As, ra + i * 32, h, q + 1, fa[u ^ 1][i]);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) read_chunk<BN, BKM>(Bs, rb + j * 32, h, q + 1, fb[u ^ 1][j]);
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][i][s], fb[u][j][s], acc[i][j], 0, 0, 0);
-        if (q == 2) {
-          if (more) {
-            la.store(As_[cur ^ 1], tid);
-            lb.store(Bs_[cur ^ 1], tid);
-          }
-          __syncthreads();
-          if (more) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) read_chunk<BM, AK>(As_[cur ^ 1], ra + i * 32, h, 0, fa[0][i]);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) read_chunk<BN, BKM>(Bs_[cur ^ 1], rb + j * 32, h, 0, fb[0][j]);
-          }
-        }
-      }
-      cur ^= 1;
-    }
-  }
-#else
-  if (kz0 < kz1) {
-    la.load(A, lda, m0, M, kz0, kz1, tid);
-    lb.load(B, ldb, n0, N, kz0, kz1, tid);
-    la.store(As_[0], tid);
-    lb.store(Bs_[0], tid);
-    __syncthreads();
-    int cur = 0;
-    for (int k0 = kz0; k0 < kz1; k0 += BK) {
-      const bool more = !PG_GEMM_X && k0 + BK < kz1;
-      if (more) {
-        la.load(A, lda, m0, M, k0 + BK, kz1, tid);
-        lb.load(B, ldb, n0, N, k0 + BK, kz1, tid);
-      }
-      const float* As = As_[cur];
-      const float* Bs = Bs_[cur];
-      if (do_rs) rs += tile_rowsum<BM, AK>(As, tid);
+      if (do_rs) rs += tile_rowsum<BM, AK>(As_, tid);
 #pragma unroll
       for (int c = 0; c < HK / 16; ++c) {
         float fa[TM][16], fb[TN][16];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) read_frag<BM, AK>(As, wm * (BM / 2) + i * 32 + l32, h, c, fa[i]);
+        for (int i = 0; i < TM; ++i) read_frag<BM, AK>(As_, wm * (BM / 2) + i * 32 + l32, h, c, fa[i]);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) read_frag<BN, BKM>(Bs, wn * (BN / 2) + j * 32 + l32, h, c, fb[j]);
-        if (PG_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
+        for (int j = 0; j < TN; ++j) read_frag<BN, BKM>(Bs_, wn * (BN / 2) + j * 32 + l32, h, c, fb[j]);
 #pragma unroll
         for (int s = 0; s < 16; ++s)
 #pragma unroll
@@ -494,35 +385,17 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
-        if (PG_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
       }
-      if constexpr (kBufs == 2) {
-        // double buffer: stage into the other image, one barrier per K step (every wave
-        // finished reading that image before the previous barrier)
-        if (more) {
-          la.store(As_[cur ^ 1], tid);
-          lb.store(Bs_[cur ^ 1], tid);
-        }
+      __syncthreads();
+      if (more) {
+        la.store(As_, tid);
+        lb.store(Bs_, tid);
         __syncthreads();
-        cur ^= 1;
-      } else {
-        __syncthreads();
-        if (more) {
-          la.store(As_[0], tid);
-          lb.store(Bs_[0], tid);
-          __syncthreads();
-        }
       }
     }
   }
-
-#endif
-
   finish_tile<BM, BN, EPI>(acc, rs, do_rs, rsred, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
                            slope, dact, lddact, rowsum, ws, ws_rowsum, blockIdx.z);
-#if PG_GEMM_STAMP
-  stamp(st_rt, st_ck, tid);
-#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -590,71 +463,13 @@ __device__ __forceinline__ void frag_chunk(const float* __restrict__ S, int rc, 
 }
 
 template <int BM, bool AK>
-__device__ __forceinline__ float img_rowsum(const float* __restrict__ As, int tid) {
+__device__ __forceinline__ double img_rowsum(const float* __restrict__ As, int tid) {
   constexpr int G = kThreads / BM;
   const int m = tid % BM, g = tid / BM;
-  float s = 0.f;
+  double s = 0.0;
 #pragma unroll
   for (int i = 0; i < BK / G; ++i) s += As[img_off<BM, AK>(m, g + i * G)];
   return s;
-}
-
-// The last-arriving workgroup of a split tile: C = alpha * sum_z slab_z (+ beta * C), the
-// slabs read with sc1 loads, 4 slices x (BM BN / 1024) float4 units in flight per thread;
-// the tile's row sums likewise (ws_rowsum != NULL on the column-0 tile).
-template <int BM, int BN>
-__device__ __forceinline__ void splitk_combine_tile(int tid, int m0, int n0, int M, int N, int S,
-                                                    float alpha, float beta, float* __restrict__ C,
-                                                    int64_t ldc, const float* __restrict__ ws,
-                                                    const float* __restrict__ ws_rowsum,
-                                                    float* __restrict__ rowsum) {
-  constexpr int UPT = BM * BN / 4 / kThreads;  // float4 units per thread
-  const __amdgpu_buffer_rsrc_t rw = slab_rsrc(ws);
-  int off[UPT];
-  bool ok[UPT];
-  f32x4 sum[UPT];
-#pragma unroll
-  for (int i = 0; i < UPT; ++i) {
-    const int u = i * kThreads + tid;
-    const int gr = m0 + u / (BN / 4), gc = n0 + (u % (BN / 4)) * 4;
-    ok[i] = gr < M && gc < N;
-    off[i] = ok[i] ? (gr * N + gc) * 4 : 0;
-    sum[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const int slab = M * N * 4;  // bytes per slice (< 2^31: checked by the host)
-  for (int z0 = 0; z0 < S; z0 += 4) {
-    f32x4 v[4][UPT];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < UPT; ++i)
-        v[j][i] = (z0 + j < S) ? __builtin_amdgcn_raw_buffer_load_b128(rw, off[i] + (z0 + j) * slab, 0, kSc1)
-                               : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < UPT; ++i) sum[i] += v[j][i];
-  }
-#pragma unroll
-  for (int i = 0; i < UPT; ++i) {
-    if (!ok[i]) continue;
-    const int u = i * kThreads + tid;
-    float* cp = C + (int64_t)(m0 + u / (BN / 4)) * ldc + n0 + (u % (BN / 4)) * 4;
-    float o[4] = {alpha * sum[i].x, alpha * sum[i].y, alpha * sum[i].z, alpha * sum[i].w};
-    if (beta != 0.f) {
-      const float4 c4 = *reinterpret_cast<const float4*>(cp);
-      o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
-      o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
-    }
-    *reinterpret_cast<float4*>(cp) = make_float4(o[0], o[1], o[2], o[3]);
-  }
-  if (ws_rowsum && tid < BM && m0 + tid < M) {
-    const __amdgpu_buffer_rsrc_t rr = slab_rsrc(ws_rowsum);
-    float t = 0.f;
-    for (int z = 0; z < S; ++z)
-      t += __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rr, (z * M + m0 + tid) * 4, 0, kSc1));
-    rowsum[m0 + tid] = t;
-  }
 }
 
 template <int BM, int BN, bool TA, bool TB, int EPI>
@@ -663,8 +478,7 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
     float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
     const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
-    float* __restrict__ ws, float* __restrict__ ws_rowsum, int vec_out, int n_split,
-    uint32_t* __restrict__ cnt) {
+    float* __restrict__ ws, float* __restrict__ ws_rowsum, int vec_out, int n_split) {
   constexpr bool AK = TA, BKM = !TB;
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int IA = BM * BK, IB = BN * BK;  // image sizes (floats)
@@ -691,7 +505,7 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
 #if PG_GEMM_STAMP
   unsigned long long st_rt = __builtin_amdgcn_s_memrealtime(), st_ck = __builtin_amdgcn_s_memtime();
 #endif
-  float rs = 0.f;
+  double rs = 0.0;
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -701,10 +515,6 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nk = kz1 > kz0 ? (kz1 - kz0 + BK - 1) / BK : 0;
-  if constexpr ((PG_GEMM_XP & 24) != 0) {  // experiment: stagger co-resident workgroups
-    const int slot = (b / 256) % 8;
-    for (int i = 0; i < slot; ++i) __builtin_amdgcn_s_sleep((PG_GEMM_XP & 8) ? 16 : 8);
-  }
   // issue the DMA of K tile t into LDS image `buf`
   auto issue = [&](int t, int buf) {
     const int k0 = kz0 + t * BK;
@@ -732,10 +542,7 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     for (int t = 0; t < nk; ++t) {
       const int cur = t & 1;
       const bool more = t + 1 < nk;
-      if (more && !(PG_GEMM_XP & 1)) {
-        issue(t + 1, cur ^ 1);
-        if constexpr ((PG_GEMM_XP & 32) != 0) issue(t + 1, cur ^ 1);  // experiment: DMA issued twice
-      }
+      if (more) issue(t + 1, cur ^ 1);
       const float* As = lds + cur * IA;
       const float* Bs = lds + 2 * IA + cur * IB;
       if (do_rs) rs += img_rowsum<BM, AK>(As, tid);
@@ -753,14 +560,9 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              if constexpr (PG_GEMM_XP & 2) acc[i][j][s] += fa[u][i][s] * fb[u][j][s];
-              else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][i][s], fb[u][j][s], acc[i][j], 0, 0, 0);
-            }
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][i][s], fb[u][j][s], acc[i][j], 0, 0, 0);
         if (q == 2) {
-#if PG_GEMM_SCHED
-          __builtin_amdgcn_sched_barrier(0);  // keep chunk 2's MFMAs ahead of the barrier
-#endif
           __syncthreads();  // tile t+1 landed (vmcnt) and every wave is past its reads of tile t-1
 #if PG_GEMM_STAMP
           if (tid == 0 && blockIdx.x < 64 && t < 64) pg_gemm_kstamp[blockIdx.x][t] = __builtin_amdgcn_s_memtime();
@@ -784,44 +586,12 @@ __global__ __launch_bounds__(kThreads) void gemm_dma_kernel(
     pg_gemm_kphase[blockIdx.x][2] = __builtin_amdgcn_s_memtime();
   }
 #endif
-  if constexpr (PG_GEMM_XP & 4) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
-    if (t == 1234.5f) C[tid] = t;
-    return;
-  }
-  if (EPI == EPI_SPLIT && cnt) {
-    // split-K combined here: slab stored sc1, the last of the tile's n_split workgroups to
-    // arrive (told by its counter add) sums the slabs in slice order 0, 1, ... (the same
-    // order whichever workgroup it is: deterministic) and resets the counter for the next call
-    finish_tile_lds<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
-                                 slope, dact, lddact, rowsum, ws, ws_rowsum, kz, true);
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(lds);
-    if (tid == 0) {
-      const uint32_t old = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = old == (uint32_t)(n_split - 1);
-      if (last) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = last;
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    splitk_combine_tile<BM, BN>(tid, m0, n0, M, N, n_split, alpha, beta, C, ldc, ws, do_rs ? ws_rowsum : nullptr,
-                                rowsum);
-    return;
-  }
   if (vec_out)
     finish_tile_lds<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
                                  slope, dact, lddact, rowsum, ws, ws_rowsum, kz);
   else
-    finish_tile<BM, BN, EPI>(acc, rs, do_rs, lds, tid, m0, n0, M, N, alpha, beta, C, ldc, bias,
-                             slope, dact, lddact, rowsum, ws, ws_rowsum, kz);
+    finish_tile<BM, BN, EPI>(acc, rs, do_rs, reinterpret_cast<double*>(lds), tid, m0, n0, M, N, alpha, beta, C,
+                             ldc, bias, slope, dact, lddact, rowsum, ws, ws_rowsum, kz);
 #if PG_GEMM_STAMP
   stamp(st_rt, st_ck, tid);
 #endif
@@ -846,7 +616,6 @@ struct Args {
   float* ws;
   float* ws_rowsum;
   int vec_out;
-  uint32_t* cnt;  // split-K tile counters (in-kernel combine) or NULL
 };
 
 template <int BM, int BN, bool TA, bool TB, bool VA, bool VB>
@@ -875,7 +644,7 @@ int launch_dma(int epi, dim3 grid, hipStream_t st, const Args& a) {
   hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, TA, TB, EPI_>), dim3(grid.x * grid.z), dim3(kThreads), \
                      0, st, a.M, a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B,  \
                      a.ldb, a.beta, a.C, a.ldc, a.bias, a.slope, a.dact, a.lddact, a.rowsum,     \
-                     a.ws, a.ws_rowsum, a.vec_out, (int)grid.z, a.cnt)
+                     a.ws, a.ws_rowsum, a.vec_out, (int)grid.z)
   switch (epi) {
     case EPI_NONE: PG_L(EPI_NONE); break;
     case EPI_RELU: PG_L(EPI_RELU); break;
@@ -891,9 +660,7 @@ int launch_dma(int epi, dim3 grid, hipStream_t st, const Args& a) {
 
 template <int BM, int BN, bool TA, bool TB>
 int launch_vec(bool va, bool vb, int epi, dim3 grid, hipStream_t st, const Args& a) {
-  static const bool legacy = getenv("PLAGNN_GEMM_LEGACY") != nullptr;  // A/B knob
-  if (va && vb && !legacy) return launch_dma<BM, BN, TA, TB>(epi, grid, st, a);
-  if (va && vb) return launch_epi<BM, BN, TA, TB, true, true>(epi, grid, st, a);
+  if (va && vb) return launch_dma<BM, BN, TA, TB>(epi, grid, st, a);
   if (va) return launch_epi<BM, BN, TA, TB, true, false>(epi, grid, st, a);
   if (vb) return launch_epi<BM, BN, TA, TB, false, true>(epi, grid, st, a);
   return launch_epi<BM, BN, TA, TB, false, false>(epi, grid, st, a);
@@ -914,17 +681,9 @@ int launch_trans(bool ta, bool tb, bool va, bool vb, int epi, dim3 grid, hipStre
 // (K <= 1024) 128 x 64 (if >= 720 tiles: ~3 workgroups per CU); everything else 64 x 64 (5 workgroups per CU: long-K
 // and small products balance best on the finest tile).
 inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& bn) {
-  // tuning knob PLAGNN_GEMM_TILE = "BMxBN" (64|128 each) forces a tile
-  static const int forced = [] {
-    const char* e = getenv("PLAGNN_GEMM_TILE");
-    if (!e) return 0;
-    int a = 0, b = 0;
-    if (sscanf(e, "%dx%d", &a, &b) != 2 || (a != 64 && a != 128) || (b != 64 && b != 128)) return 0;
-    return a * 1000 + b;
-  }();
-  if (forced) {
-    bm = forced / 1000;
-    bn = forced % 1000;
+  if constexpr (PG_GEMM_TILE_FORCE != 0) {  // variant builds only
+    bm = PG_GEMM_TILE_FORCE / 1000;
+    bn = PG_GEMM_TILE_FORCE % 1000;
     return;
   }
   auto tiles = [&](int tm, int tn) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
@@ -952,18 +711,9 @@ int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K) {
   // 1024 workgroups 1.984 ms, 768 1.992, 1280 2.022, 640 / 896 2.06 / 2.03 (not a multiple
   // of the 256 CUs), 512 1.99, 384 2.15.
   const int64_t tiles = ((M + 63) / 64) * ((N + 63) / 64);
-  static const int64_t want = [] {  // tuning knob PLAGNN_SPLIT_TARGET: workgroups aimed at
-    const char* e = getenv("PLAGNN_SPLIT_TARGET");
-    const int64_t v = e ? atoll(e) : 1024;
-    return v > 0 ? v : 1024;
-  }();
-  const int64_t target = (want + tiles - 1) / tiles;
+  const int64_t target = (PG_SPLIT_TARGET + tiles - 1) / tiles;
   const int64_t by_k = K / (3 * BK);
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, by_k), 256));
-}
-
-int64_t pg_gemm_splitk_counters(int64_t M, int64_t N) {
-  return M > 0 && N > 0 ? ((M + 63) / 64) * ((N + 63) / 64) : 0;
 }
 
 size_t pg_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int split_k) {
@@ -1026,14 +776,9 @@ int gemm_f32_impl(int transa, int transb, int64_t M, int64_t N, int64_t K, float
                        (split ? al16(wsf) : (al16(C) && (ldc % 4) == 0)) &&
                        (!ep->bias || al16(ep->bias)) &&
                        (!ep->dact || (al16(ep->dact) && (ep->lddact % 4) == 0));
-  // split-K partials combined inside the kernel when the caller gives tile counters, the
-  // 16-B slab path applies and every slab offset fits the buffer intrinsics' 32-bit range
-  const bool in_kernel = split && !defer && ep->splitk_cnt && vec_out && al16(C) && (ldc % 4) == 0 &&
-                         (int64_t)split_k * M * N * 4 < INT32_MAX && !getenv("PLAGNN_SPLITK_REDUCE");
   const Args a{(int)M, (int)N, (int)K, kps, tiles_n, tiles, alpha, A, lda, B, ldb, beta, C, ldc,
                ep->bias, ep->slope, ep->dact, ep->lddact, ep->rowsum, wsf,
-               split ? wsf + (int64_t)split_k * M * N : nullptr, vec_out ? 1 : 0,
-               in_kernel ? ep->splitk_cnt : nullptr};
+               split ? wsf + (int64_t)split_k * M * N : nullptr, vec_out ? 1 : 0};
   const bool ta = transa != 0, tb = transb != 0;
   const int epi = split ? EPI_SPLIT
                         : ep->dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
@@ -1048,7 +793,7 @@ int gemm_f32_impl(int transa, int transb, int64_t M, int64_t N, int64_t K, float
   else
     rc = launch_trans<64, 64>(ta, tb, va, vb, epi, grid, st, a);
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_f32: dispatch failed");
-  if (split && !in_kernel && !defer) {
+  if (split && !defer) {
     const int64_t n = (N % 4 == 0 ? M * N / 4 : M * N) + (ep->rowsum ? M : 0);  // work units
     // threads per output: enough slice groups that each thread sums <= ~8 slices
     const int G = splitk_groups(split_k);

@@ -163,32 +163,14 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Winner lists built by the forward (grouped mode, one feature tile per launch): for an
-// unsplit row v, the tile's features are grouped by their winning in-row position p and
-//   gfeat[v pitch + f0 + i]   the features (tile-relative), grouped by p,
-//   glist[einv[ptr[v] + p]]   = {v pitch + f0 + start_p, count_p}  (this tile's descriptors),
-//   rcnt[v]                   = the row's entry count in this tile.
-// Entries whose maximum is 0 (a +-inf maximum, stored as 0, too) are left out: their
-// winner contributes nothing through a relu' mask (pg_spmm_max_bwd's fwd_out rule).
-struct GroupOut {
-  uint16_t* gfeat;
-  int2* glist;
-  int32_t* rcnt;
-  const int32_t* einv;
-  int64_t pitch;
-  int f0;
-};
-
-template <int W, int NC, bool HAS_W, typename A, typename T = float, bool GROUP = false>
+template <int W, int NC, bool HAS_W, typename A, typename T = float>
 __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
     const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
     const int32_t* __restrict__ eslot, const float* __restrict__ ew,
     const int4* __restrict__ items, int n_items, const T* __restrict__ X, int64_t ldx, int F,
     T* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
-    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, GroupOut go,
-    int n_ftiles = 1, int ftile = 0) {
+    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, int n_ftiles = 1, int ftile = 0) {
   constexpr int U = EdgeU<W, NC>::value;
-  __shared__ int ghist[GROUP ? kWavesPerBlock * (kPackWaveMax + 4) : 1];
   // n_ftiles > 1: all feature tiles of F in one launch, block b -> (item block b / n_ftiles,
   // tile b % n_ftiles), so every tile's longest items start first
   int bx = blockIdx.x;
@@ -210,19 +192,6 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
   const int rs = ptr[row];
   const int lane = lane_id();
   const float ninf = -std::numeric_limits<float>::infinity();
-  // grouped mode: the row's transposed-CSR indices are loaded up front (needed at the end)
-  const int gdeg = k1 - k0;
-  const int gB = (gdeg + kWave - 1) / kWave;  // bins per lane, <= 4 (unsplit rows)
-  int ei[4] = {0, 0, 0, 0};
-  if constexpr (GROUP) {
-    if (slot < 0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int p = lane * gB + q;
-        if (q < gB && p < gdeg) ei[q] = go.einv[rs + p];
-      }
-    }
-  }
 
   float best[NC][W];
   int bpos[NC][W];
@@ -283,59 +252,7 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
     for (int c = 0; c < NC; ++c) {
       const int f = (c * kWave + lane) * W;
       store_tile<W, T>(orow, f, F, best[c]);
-      if constexpr (!GROUP) store_arg<W, A>(arow, f, F, bpos[c]);
-    }
-    if constexpr (GROUP) {
-      // wave-private LDS histogram over the row's positions, wave scan, placement
-      const int deg = gdeg, B = gB;
-      // the stored value is what the backward's relu' mask sees: 0 => no contribution
-      bool live[NC][W];
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int i = 0; i < W; ++i)
-          live[c][i] = bpos[c][i] != arg_none<A>() && to_f(from_f<T>(best[c][i])) != 0.f &&
-                       (c * kWave + lane) * W + i < F;
-      int* hist = ghist + wave_id_uniform() * (kPackWaveMax + 4);
-      for (int p = lane; p < deg; p += kWave) hist[p] = 0;
-      wave_lds_sync();
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int i = 0; i < W; ++i)
-          if (live[c][i]) atomicAdd(&hist[bpos[c][i]], 1);
-      wave_lds_sync();
-      int cq[4], local = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int p = lane * B + q;
-        cq[q] = (q < B && p < deg) ? hist[p] : 0;
-        local += cq[q];
-      }
-      int x = local;
-#pragma unroll
-      for (int o = 1; o < kWave; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-      }
-      int run = x - local;
-      const int64_t base = (int64_t)row * go.pitch + go.f0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int p = lane * B + q;
-        if (q < B && p < deg) {
-          hist[p] = run;
-          go.glist[ei[q]] = make_int2((int)(base + run), cq[q]);
-          run += cq[q];
-        }
-      }
-      if (lane == kWave - 1) go.rcnt[row] = x;
-      wave_lds_sync();
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int i = 0; i < W; ++i)
-          if (live[c][i]) go.gfeat[base + atomicAdd(&hist[bpos[c][i]], 1)] = (uint16_t)((c * kWave + lane) * W + i);
+      store_arg<W, A>(arow, f, F, bpos[c]);
     }
   } else {
     float* orow = ws_val + (int64_t)slot * ldw;
@@ -497,6 +414,9 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
 // short contiguous runs (~F/deg entries).
 constexpr int kHistMax = 4096;
 constexpr int kGroupMaxF = 1024;
+#ifndef PG_BWD_DIRECT
+#define PG_BWD_DIRECT 0
+#endif
 
 __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   const int per = (n + kBlock - 1) / kBlock;
@@ -610,23 +530,20 @@ __device__ __forceinline__ void pack_short_row(
     }
 }
 
-// LISTS: lists only (the grouped forward's split rows: no upstream gradient yet, so no
-// dpack; the row's entry count goes to rcnt[v]); the list space of row v starts at
-// v pitch + f0 (the old path: pitch = F, f0 = 0).
-template <typename A, typename T, bool LISTS = false>
+template <typename A, typename T>
 __device__ __forceinline__ void pack_long_row(
     int v, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
     const T* __restrict__ fout, int64_t ldf, uint16_t* __restrict__ gfeat, int2* __restrict__ glist,
-    float* __restrict__ dpack, int* __restrict__ lds, int64_t pitch, int f0, int32_t* __restrict__ rcnt) {
+    float* __restrict__ dpack, int* __restrict__ lds) {
   int* hist = lds;
   uint16_t* feats = reinterpret_cast<uint16_t*>(lds + kHistMax + 8);
   int* wsum = lds + kHistMax + 8 + kGroupMaxF / 2;
   const int rs = ptr[v];
   const int deg = ptr[v + 1] - rs;
-  if (!LISTS && deg <= kPackWaveMax) return;  // (LISTS: every split row, whatever its chunk)
+  if (deg <= kPackWaveMax) return;
   const A* ar = arg + (int64_t)v * lda;
-  const int64_t vF = (int64_t)v * pitch + f0;
+  const int64_t vF = (int64_t)v * F;
   int total;
   if (deg <= kHistMax) {
     // independent loads first (each thread its own features), placement straight to the
@@ -639,7 +556,7 @@ __device__ __forceinline__ void pack_long_row(
     for (int i = 0; i < FPT; ++i) {
       const int f = threadIdx.x + i * kBlock;
       a[i] = f < F ? (int)ar[f] : arg_none<A>();
-      if constexpr (!LISTS) d[i] = f < F ? to_f(dr[f]) : 0.f;
+      d[i] = f < F ? to_f(dr[f]) : 0.f;
     }
     if (fout) {  // zero maxima contribute nothing (their winner's relu mask is 0)
       const T* fr = fout + (int64_t)v * ldf;
@@ -674,14 +591,13 @@ __device__ __forceinline__ void pack_long_row(
         }
       }
     }
-    if (LISTS && threadIdx.x == 0) rcnt[v] = total;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < FPT; ++i)
       if (a[i] != arg_none<A>()) {
         const int64_t pos = vF + atomicAdd(&hist[a[i]], 1);
         gfeat[pos] = (uint16_t)(threadIdx.x + i * kBlock);
-        if constexpr (!LISTS) dpack[pos] = d[i];
+        dpack[pos] = d[i];
       }
     return;
   } else {
@@ -729,7 +645,6 @@ __device__ __forceinline__ void pack_long_row(
     if (threadIdx.x == 0) wsum[0] = lower(0xFFFFFFFFu);
     __syncthreads();
     total = wsum[0];
-    if (LISTS && threadIdx.x == 0) rcnt[v] = total;
     for (int i = threadIdx.x; i < total; i += kBlock) feats[i] = (uint16_t)(keys[i] & 0xFFFFu);
     __syncthreads();
   }
@@ -737,7 +652,7 @@ __device__ __forceinline__ void pack_long_row(
   for (int i = threadIdx.x; i < total; i += kBlock) {
     const int f = feats[i];
     gfeat[vF + i] = (uint16_t)f;
-    if constexpr (!LISTS) dpack[vF + i] = to_f(dr[f]);
+    dpack[vF + i] = to_f(dr[f]);
   }
 }
 
@@ -759,124 +674,12 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
   const int b = blockIdx.x;
   if (b < n_long) {
     pack_long_row<A, T>(rows ? rows[b].x : b, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gfeat, glist,
-                        dpack, lds, F, 0, nullptr);
+                        dpack, lds);
   } else {
     const int wave = wave_id_uniform();
     const int v = (b - n_long) * kWavesPerBlock + wave;
     if (v < n_rows)
       pack_short_row<A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gfeat, glist, dpack, lds);
-  }
-}
-
-// Grouped forward, rows split across work items: combine the partial maxima in chunk order
-// (earlier chunk wins ties, as max_merge_kernel) and build the row's lists in the same
-// block: one thread per feature of the tile (F <= kBlock), the live (p << 16 | f) keys
-// bitonic-sorted in LDS, descriptors by binary search for every position p of the row.
-template <typename T>
-__global__ __launch_bounds__(kBlock) void max_merge_group_kernel(
-    const int4* __restrict__ merges, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
-    int F, const float* __restrict__ ws_val, const uint16_t* __restrict__ ws_arg, int64_t ldw,
-    T* __restrict__ out, int64_t ldo, uint16_t* __restrict__ gfeat, int2* __restrict__ glist,
-    int64_t pitch, int f0, int32_t* __restrict__ rcnt) {
-  __shared__ uint32_t keys[kBlock];
-  const int4 m = merges[blockIdx.x];
-  const int row = m.x, s0 = m.y, ns = m.z;
-  const int f = threadIdx.x;
-  const int rs = ptr[row];
-  const int deg = ptr[row + 1] - rs;
-  float best = -std::numeric_limits<float>::infinity();
-  int bp = 0xFFFF;
-  if (f < F) {
-    for (int s = s0; s < s0 + ns; s += 8) {
-      float v[8];
-      int a[8];  // loaded with the values: no dependent load behind each compare
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int64_t o = (int64_t)min(s + e, s0 + ns - 1) * ldw + f;
-        v[e] = ws_val[o];
-        a[e] = (int)ws_arg[o];
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (s + e < s0 + ns && v[e] > best) {
-          best = v[e];
-          bp = a[e];
-        }
-    }
-    if (__builtin_isinf(best)) best = 0.f;
-    out[(int64_t)row * ldo + f] = from_f<T>(best);
-  }
-  const bool live = f < F && bp != 0xFFFF && to_f(from_f<T>(best)) != 0.f;
-  keys[f] = live ? ((uint32_t)bp << 16) | (uint32_t)f : 0xFFFFFFFFu;
-  const int total = __syncthreads_count(live);
-  for (int k = 2; k <= kBlock; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int ixj = f ^ j;
-      if (ixj > f) {
-        const uint32_t x = keys[f], y = keys[ixj];
-        if ((x > y) == ((f & k) == 0)) {
-          keys[f] = y;
-          keys[ixj] = x;
-        }
-      }
-      __syncthreads();
-    }
-  auto lower = [&](uint32_t key) {
-    int lo = 0, hi = total;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (keys[mid] < key) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-  };
-  const int64_t base = (int64_t)row * pitch + f0;
-  for (int p0 = f; p0 < deg; p0 += 8 * kBlock) {  // 8 positions' einv loads in flight
-    int e[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) e[j] = p0 + j * kBlock < deg ? einv[rs + p0 + j * kBlock] : 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int p = p0 + j * kBlock;
-      if (p < deg) {
-        const int st = lower((uint32_t)p << 16);
-        const int en = lower((uint32_t)(p + 1) << 16);
-        glist[e[j]] = make_int2((int)(base + st), en - st);
-      }
-    }
-  }
-  if (f < total) gfeat[base + f] = (uint16_t)(keys[f] & 0xFFFFu);
-  if (f == 0) rcnt[row] = total;
-}
-
-// Grouped backward, pass 1: the upstream gradient in list order, one wave per row v over
-// every feature tile t: dpack[i] = dout[v, f0_t + gfeat[i]] over the row's entries.
-template <typename T>
-__global__ __launch_bounds__(kBlock) void group_gather_kernel(
-    int n_rows, int F, int tile, const int32_t* __restrict__ rcnt, const uint16_t* __restrict__ gfeat,
-    const T* __restrict__ dout, int64_t ldd, float* __restrict__ dpack) {
-  const int v = blockIdx.x * kWavesPerBlock + wave_id_uniform();
-  if (v >= n_rows) return;
-  const int lane = lane_id();
-  const T* dr = dout + (int64_t)v * ldd;
-  const int nt = (F + tile - 1) / tile;
-  for (int t = 0; t < nt; ++t) {
-    const int f0 = t * tile;
-    const int cnt = rcnt[(int64_t)t * n_rows + v];
-    const int64_t base = (int64_t)v * F + f0;
-    for (int i0 = 0; i0 < cnt; i0 += 4 * kWave) {
-      int f[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int i = i0 + j * kWave + lane;
-        f[j] = i < cnt ? (int)gfeat[base + i] : -1;
-      }
-      float d[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) d[j] = f[j] >= 0 ? to_f(dr[f0 + f[j]]) : 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (f[j] >= 0) dpack[base + i0 + j * kWave + lane] = d[j];
-    }
   }
 }
 
@@ -886,18 +689,13 @@ __global__ __launch_bounds__(kBlock) void invert_slots_kernel(const int32_t* __r
     einv[tslot[t]] = (int32_t)t;
 }
 
-// Lists of several feature tiles (the grouped mode): tile k's descriptors start at
-// glist + k * tile_stride and its list entries are features relative to f0 = k * tile.
-// DIRECT: no dpack; the upstream gradient is read from dout[v, f0 + gfeat[...]] (v = the
-// edge's destination, tcol), one dependent load after the list's feature ids.
-template <bool HAS_W, typename T = float, bool DIRECT = false>
+template <bool HAS_W, typename T = float>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const float* __restrict__ ew, const int32_t* __restrict__ tslot,
-    const int4* __restrict__ items, int n_items, const int2* __restrict__ glist0,
+    const int4* __restrict__ items, int n_items, const int2* __restrict__ glist,
     const uint16_t* __restrict__ gfeat, const float* __restrict__ dpack, int F,
     const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx,
-    float* __restrict__ ws, int64_t ldw, int n_tiles = 1, int tile = 0, int64_t tile_stride = 0,
-    const int32_t* __restrict__ tcol = nullptr, const T* __restrict__ dout = nullptr, int64_t ldd = 0) {
+    float* __restrict__ ws, int64_t ldw) {
 #ifndef PG_PULL_U
 #define PG_PULL_U 8  // measured on S0 (scripts/spmm_variants.sh): 4-8 best, 16 +6 %, 32 +25 %
 #endif
@@ -906,14 +704,11 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   const int wave = wave_id_uniform();
   const int it = blockIdx.x * kWavesPerBlock + wave;
   if (it >= n_items) return;
-  float* acc0 = accs[wave];
+  float* acc = accs[wave];
   const int4 item = items[it];
   const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
   const int lane = lane_id();
-  for (int f = lane; f < F; f += kWave) acc0[f] = 0.f;
-  for (int tk = 0; tk < n_tiles; ++tk) {
-  const int2* __restrict__ glist = glist0 + tk * tile_stride;
-  float* acc = acc0 + tk * tile;
+  for (int f = lane; f < F; f += kWave) acc[f] = 0.f;
 
   // Each window of 64 out-edges is flattened into "segments" (64-entry pieces of the
   // edges' lists, edge-major; empty lists have none) and the segments are processed U at
@@ -930,8 +725,6 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     if (tw + kWave < t1) gl_next = glist[tw + kWave + min(lane, t1 - tw - kWave - 1)];
     float wv = 1.f;
     if constexpr (HAS_W) wv = ew[tslot[tl]];
-    int vv = 0;
-    if constexpr (DIRECT) vv = tcol[tl];
     const int nseg = lane < nw ? (gl.y + kWave - 1) / kWave : 0;
     int incl = nseg;
 #pragma unroll
@@ -956,14 +749,7 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
         ne[u] = n;
         const bool on = lane < n;
         fe[u] = on ? (int)gfeat[base + lane] : 0;
-        if constexpr (!DIRECT) de[u] = on ? dpack[base + lane] : 0.f;
-      }
-      if constexpr (DIRECT) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const T* dr = dout + (int64_t)bcast(vv, ie[u]) * ldd + tk * tile;
-          de[u] = lane < ne[u] ? to_f(dr[fe[u]]) : 0.f;
-        }
+        de[u] = on ? dpack[base + lane] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -975,8 +761,6 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
       }
     }
   }
-  }  // feature tiles
-  float* acc = acc0;
   wave_lds_sync();
   if (slot < 0) {
     T* xr = dx + (int64_t)row * ldx;
@@ -1233,18 +1017,14 @@ struct TilePlan {
   int64_t tile;
 };
 
-// Feature columns per launch on the vector path (tuning knob PLAGNN_SPMM_FTILE, a
-// multiple of 256 up to 1024): narrower tiles mean fewer registers per wave (higher
-// occupancy) at the price of re-reading the column ids once per tile.
-inline int64_t vec_ftile() {
-  static const int64_t t = [] {
-    const char* e = getenv("PLAGNN_SPMM_FTILE");
-    int64_t v = e ? atoll(e) : 256;
-    if (v < 256 || v > kFTileVec || v % 256) v = kFTileVec;
-    return v;
-  }();
-  return t;
-}
+// Feature columns per launch on the vector path (a multiple of 256 up to 1024; variant
+// builds: -DPG_SPMM_FTILE=...): narrower tiles mean fewer registers per wave (higher
+// occupancy) at the price of re-reading the column ids once per tile. 256 measured best.
+#ifndef PG_SPMM_FTILE
+#define PG_SPMM_FTILE 256
+#endif
+static_assert(PG_SPMM_FTILE >= 256 && PG_SPMM_FTILE <= kFTileVec && PG_SPMM_FTILE % 256 == 0, "feature tile");
+constexpr int64_t vec_ftile() { return PG_SPMM_FTILE; }
 
 inline TilePlan plan_tiles(int64_t F, std::initializer_list<int64_t> lds,
                            std::initializer_list<const void*> ptrs) {
@@ -1279,8 +1059,8 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
       constexpr bool HW = decltype(hw_c)::value;
       hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T>), dim3((unsigned)blocks * n_ft), dim3(kBlock), 0, st,
                          g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
-                         X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, GroupOut{},
-                         n_ft, (int)tp.tile);
+                         X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, n_ft,
+                         (int)tp.tile);
       return PG_OK;
     };
     int rc;
@@ -1456,12 +1236,9 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
   hipStream_t st = (hipStream_t)stream;
   const size_t pbytes = bwd_partials_bytes(gt, F);
   float* w = pbytes ? (float*)ws : nullptr;
-  static const bool force_direct = [] {
-    const char* e = getenv("PLAGNN_BWD_PATH");  // tuning knob: "direct" = argmax-row gather
-    return e && strcmp(e, "direct") == 0;
-  }();
   const int64_t N = g->n_rows;
-  if (arg_kind == PG_ARG_U16 && F <= kGroupMaxF && N * F < INT32_MAX && !force_direct) {
+  // PG_BWD_DIRECT (variant builds): always the argmax-record gather over the transposed CSR
+  if (arg_kind == PG_ARG_U16 && F <= kGroupMaxF && N * F < INT32_MAX && !PG_BWD_DIRECT) {
     char* p = (char*)ws + pbytes;
     uint16_t* gfeat = (uint16_t*)p;
     p += round_up(N * F * 2, 256);
@@ -1657,172 +1434,6 @@ int pg_argpos_to_src(const pg_csr_t* g, const void* argpos, int64_t lda, int arg
     hipLaunchKernelGGL((argpos_to_src_kernel<int32_t>), dim3(blocks), dim3(kBlock), 0, st, g->ptr,
                        g->col, g->n_rows, (const int32_t*)argpos, lda, (int)F, argx, ldx);
   return hip_status("pg_argpos_to_src");
-}
-
-}  // extern "C"
-
-// ---- grouped forward / backward: the winner lists are built by the forward ------------
-namespace {
-
-constexpr int kGroupTile = 256;  // feature columns per grouped launch (one 64 x float4 chunk)
-
-template <typename T>
-int max_fwd_grouped_entry(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
-                          int64_t ldo, void* argpos, int64_t lda, uint16_t* gfeat, int32_t* glist,
-                          int32_t* rcnt, void* ws, size_t ws_bytes, pg_stream_t stream) {
-  const char* who = "pg_spmm_max_fwd_grouped";
-  PG_TRY(pg::check_csr(g, who, true));
-  if (F < 0 || ldx < F || ldo < F || lda < F)
-    return pg::set_error(PG_ERR_INVALID, "%s: bad F/leading dims", who);
-  if (F == 0 || g->n_rows == 0) return pg::ok();
-  if (!X || !out || !argpos || !gfeat || !glist || !rcnt)
-    return pg::set_error(PG_ERR_INVALID, "%s: NULL buffer", who);
-  if (g->nnz > 0 && !g->einv) return pg::set_error(PG_ERR_INVALID, "%s: g needs einv", who);
-  if (g->max_deg >= 0xFFFF || g->chunk <= 0 || g->chunk > kPackWaveMax ||
-      g->n_rows * F >= INT32_MAX || F % 4 || ldx % 4 || ldo % 4 || lda % 4 || !aligned16(X) ||
-      !aligned16(out) || ((uintptr_t)argpos & 7))
-    return pg::set_error(PG_ERR_UNSUPPORTED,
-                         "%s: needs max degree < 65535, a schedule chunk <= %d, N*F < 2^31 and "
-                         "16-B aligned rows (F, ld multiples of 4)", who, kPackWaveMax);
-  const size_t need = pg_spmm_max_fwd_workspace(g, F, PG_ARG_U16);
-  PG_TRY(check_ws(ws_bytes, need, who));
-  const int64_t ldw = ws_ld(F);
-  float* ws_val = need ? (float*)ws : nullptr;
-  uint16_t* ws_arg = need ? (uint16_t*)((char*)ws + round_up(g->n_slots * ldw * 4, 256)) : nullptr;
-  if (ws_val && (!aligned16(ws_val) || ((uintptr_t)ws_arg & 7)))
-    return pg::set_error(PG_ERR_INVALID, "%s: workspace must be 16-B aligned", who);
-  hipStream_t st = (hipStream_t)stream;
-  uint16_t* arg = (uint16_t*)argpos;  // (the kernels of the grouped mode leave it unwritten)
-  const int blocks = grid_for(g->n_items);
-  const int64_t N = g->n_rows;
-  for (int64_t f0 = 0; f0 < F; f0 += kGroupTile) {
-    const int Ft = (int)std::min<int64_t>(kGroupTile, F - f0);
-    const int64_t t = f0 / kGroupTile;
-    const GroupOut go{gfeat, (int2*)glist + t * g->nnz, rcnt + t * N, g->einv, F, (int)f0};
-    if (g->ew)
-      hipLaunchKernelGGL((max_fwd_kernel<4, 1, true, uint16_t, T, true>), dim3(blocks), dim3(kBlock), 0, st,
-                         g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
-                         X + f0, ldx, Ft, out + f0, ldo, arg + f0, lda,
-                         ws_val ? ws_val + f0 : nullptr, ws_arg ? ws_arg + f0 : nullptr, ldw, go);
-    else
-      hipLaunchKernelGGL((max_fwd_kernel<4, 1, false, uint16_t, T, true>), dim3(blocks), dim3(kBlock), 0, st,
-                         g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
-                         X + f0, ldx, Ft, out + f0, ldo, arg + f0, lda,
-                         ws_val ? ws_val + f0 : nullptr, ws_arg ? ws_arg + f0 : nullptr, ldw, go);
-    if (g->n_merges > 0) {
-      hipLaunchKernelGGL((max_merge_group_kernel<T>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
-                         (const int4*)g->merges, g->ptr, g->einv, Ft, ws_val + f0, ws_arg + f0, ldw,
-                         out + f0, ldo, gfeat, go.glist, (int64_t)F, (int)f0, go.rcnt);
-    }
-  }
-  return hip_status(who);
-}
-
-size_t bwd_grouped_ws(const pg_csr_t* gt, int64_t F) {
-  const size_t part = gt->n_slots > 0 ? round_up(gt->n_slots * ws_ld(F) * 4, 256) : 0;
-  return part + round_up(gt->n_cols * F * 4, 256);
-}
-
-template <typename T>
-int max_bwd_grouped_entry(const pg_csr_t* g, const pg_csr_t* gt, const uint16_t* gfeat,
-                          const int32_t* glist, const int32_t* rcnt, const T* dout, int64_t ldd,
-                          int64_t F, const T* mask_src, int64_t ldm, T* dx, int64_t ldx, void* ws,
-                          size_t ws_bytes, pg_stream_t stream) {
-  const char* who = "pg_spmm_max_bwd_grouped";
-  PG_TRY(pg::check_csr(g, who, false));
-  PG_TRY(pg::check_csr(gt, who, true));
-  if (gt->n_cols != g->n_rows || gt->nnz != g->nnz)
-    return pg::set_error(PG_ERR_INVALID, "%s: gt is not the transpose of g", who);
-  if (gt->nnz > 0 && !gt->eslot) return pg::set_error(PG_ERR_INVALID, "%s: gt needs eslot", who);
-  if (F < 0 || ldd < F || ldx < F || (mask_src && ldm < F))
-    return pg::set_error(PG_ERR_INVALID, "%s: bad F/leading dims", who);
-  if (F == 0 || gt->n_rows == 0) return pg::ok();
-  if (!gfeat || !glist || !rcnt || !dout || !dx) return pg::set_error(PG_ERR_INVALID, "%s: NULL buffer", who);
-  if (g->n_rows * F >= INT32_MAX) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: N*F >= 2^31", who);
-  PG_TRY(check_ws(ws_bytes, bwd_grouped_ws(gt, F), who));
-  hipStream_t st = (hipStream_t)stream;
-  const int64_t N = g->n_rows;
-  const size_t part = gt->n_slots > 0 ? round_up(gt->n_slots * ws_ld(F) * 4, 256) : 0;
-  float* w = part ? (float*)ws : nullptr;
-  float* dpack = (float*)((char*)ws + part);
-  const int blocks = grid_for(gt->n_items);
-  const int nt = (int)((F + kGroupTile - 1) / kGroupTile);
-  if (F > kGroupMaxF) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: F > %d", who, kGroupMaxF);
-  static const bool gather = [] {  // tuning knob: 1 = dpack gather pass + plain pull
-    const char* e = getenv("PLAGNN_GROUP_GATHER");
-    return e && e[0] == '1';
-  }();
-  if (!gather) {
-    if (g->ew)
-      hipLaunchKernelGGL((max_bwd_pull_kernel<true, T, true>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
-                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, (const int2*)glist, gfeat,
-                         nullptr, (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F), nt, kGroupTile, g->nnz,
-                         gt->col, dout, ldd);
-    else
-      hipLaunchKernelGGL((max_bwd_pull_kernel<false, T, true>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
-                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, (const int2*)glist, gfeat,
-                         nullptr, (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F), nt, kGroupTile, g->nnz,
-                         gt->col, dout, ldd);
-  } else {
-  hipLaunchKernelGGL((group_gather_kernel<T>), dim3((unsigned)grid_for(N)), dim3(kBlock), 0, st, (int)N,
-                     (int)F, kGroupTile, rcnt, gfeat, dout, ldd, dpack);
-  if (g->ew)
-    hipLaunchKernelGGL((max_bwd_pull_kernel<true, T>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
-                       gt->eslot, (const int4*)gt->items, (int)gt->n_items, (const int2*)glist, gfeat,
-                       dpack, (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F), nt, kGroupTile, g->nnz);
-  else
-    hipLaunchKernelGGL((max_bwd_pull_kernel<false, T>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
-                       gt->eslot, (const int4*)gt->items, (int)gt->n_items, (const int2*)glist, gfeat,
-                       dpack, (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F), nt, kGroupTile, g->nnz);
-  }
-  if (gt->n_merges > 0)
-    hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
-                       (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
-                       mask_src, ldm, dx, ldx);
-  return hip_status(who);
-}
-
-}  // namespace
-
-extern "C" {
-
-int64_t pg_spmm_group_tiles(int64_t F) { return F > 0 ? (F + kGroupTile - 1) / kGroupTile : 0; }
-
-int pg_spmm_max_fwd_grouped(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
-                            int64_t ldo, void* argpos, int64_t lda, uint16_t* gfeat, int32_t* glist,
-                            int32_t* rcnt, void* ws, size_t ws_bytes, pg_stream_t stream) {
-  return max_fwd_grouped_entry<float>(g, X, ldx, F, out, ldo, argpos, lda, gfeat, glist, rcnt, ws,
-                                      ws_bytes, stream);
-}
-
-int pg_spmm_max_fwd_grouped_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t F, void* out,
-                                 int64_t ldo, void* argpos, int64_t lda, uint16_t* gfeat,
-                                 int32_t* glist, int32_t* rcnt, void* ws, size_t ws_bytes,
-                                 pg_stream_t stream) {
-  return max_fwd_grouped_entry<uint16_t>(g, (const uint16_t*)X, ldx, F, (uint16_t*)out, ldo, argpos,
-                                         lda, gfeat, glist, rcnt, ws, ws_bytes, stream);
-}
-
-size_t pg_spmm_max_bwd_grouped_workspace(const pg_csr_t* gt, int64_t F) {
-  if (!gt || F <= 0) return 0;
-  return bwd_grouped_ws(gt, F);
-}
-
-int pg_spmm_max_bwd_grouped(const pg_csr_t* g, const pg_csr_t* gt, const uint16_t* gfeat,
-                            const int32_t* glist, const int32_t* rcnt, const float* dout, int64_t ldd,
-                            int64_t F, const float* mask_src, int64_t ldm, float* dx, int64_t ldx,
-                            void* ws, size_t ws_bytes, pg_stream_t stream) {
-  return max_bwd_grouped_entry<float>(g, gt, gfeat, glist, rcnt, dout, ldd, F, mask_src, ldm, dx, ldx,
-                                      ws, ws_bytes, stream);
-}
-
-int pg_spmm_max_bwd_grouped_bf16(const pg_csr_t* g, const pg_csr_t* gt, const uint16_t* gfeat,
-                                 const int32_t* glist, const int32_t* rcnt, const void* dout,
-                                 int64_t ldd, int64_t F, const void* mask_src, int64_t ldm, void* dx,
-                                 int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream) {
-  return max_bwd_grouped_entry<uint16_t>(g, gt, gfeat, glist, rcnt, (const uint16_t*)dout, ldd, F,
-                                         (const uint16_t*)mask_src, ldm, (uint16_t*)dx, ldx, ws,
-                                         ws_bytes, stream);
 }
 
 }  // extern "C"

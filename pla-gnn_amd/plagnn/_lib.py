@@ -57,7 +57,6 @@ class PgGemmEpilogue(ctypes.Structure):
         ("dact", ctypes.c_void_p),
         ("lddact", ctypes.c_int64),
         ("rowsum", ctypes.c_void_p),
-        ("splitk_cnt", ctypes.c_void_p),
     ]
 
 
@@ -98,20 +97,10 @@ SIGNATURES = {
     "pg_spmm_max_bwd_workspace": (_sz, [_csr, _i64]),
     "pg_spmm_max_bwd": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                              _vp, _sz, _vp]),
-    "pg_spmm_group_tiles": (_i64, [_i64]),
-    "pg_gemm_splitk_counters": (_i64, [_i64, _i64]),
     "pg_gemm_f32_partials": (_i, [_i, _i, _i64, _i64, _i64, _vp, _i64, _vp, _i64, ctypes.POINTER(PgGemmEpilogue),
                                   _i, _vp, _sz, ctypes.POINTER(ctypes.c_int), _vp]),
     "pg_gemm_splitk_reduce_batch": (_i, [ctypes.POINTER(PgSplitkJob), _i, _vp]),
     "pg_csr_spmm_f64": (_i, [_i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),
-    "pg_spmm_max_fwd_grouped": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
-    "pg_spmm_max_fwd_grouped_bf16": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _sz,
-                                          _vp]),
-    "pg_spmm_max_bwd_grouped_workspace": (_sz, [_csr, _i64]),
-    "pg_spmm_max_bwd_grouped": (_i, [_csr, _csr, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _sz,
-                                     _vp]),
-    "pg_spmm_max_bwd_grouped_bf16": (_i, [_csr, _csr, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
-                                          _sz, _vp]),
     "pg_spmm_max_bwd_scatter": (_i, [_csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "pg_spmm_sum_workspace": (_sz, [_csr, _i64]),
     "pg_spmm_sum": (_i, [_csr, _vp, _i64, _i64, _i, _vp, _vp, _i64, _vp, _sz, _vp]),
@@ -198,8 +187,7 @@ def stream_handle(device: torch.device):
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def epilogue(bias=None, act: int = PG_ACT_NONE, slope: float = 0.01, dact=None, rowsum=None,
-             splitk_cnt=None):
+def epilogue(bias=None, act: int = PG_ACT_NONE, slope: float = 0.01, dact=None, rowsum=None):
     """pg_gemm_epilogue_t from tensors (or None)."""
     e = PgGemmEpilogue()
     e.bias = ptr(bias)
@@ -208,7 +196,6 @@ def epilogue(bias=None, act: int = PG_ACT_NONE, slope: float = 0.01, dact=None, 
     e.dact = ptr(dact)
     e.lddact = dact.stride(0) if dact is not None else 0
     e.rowsum = ptr(rowsum)
-    e.splitk_cnt = ptr(splitk_cnt)
     return e
 
 

@@ -26,7 +26,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 from collections import defaultdict
 from typing import Dict, List, Optional, Sequence
 
@@ -146,13 +145,6 @@ class TrainEngine:
         self.row_set = torch.from_numpy(rs).to(dev)
         self.n_train = len(np.asarray(train_index))
         self.n_val = 0 if val_index is None else len(np.asarray(val_index))
-        # PLAGNN_GROUPED=1: the forward builds the backward's winner lists
-        # (pg_spmm_max_fwd_grouped) and the backward has no pack pass. Off by default: on cfg2
-        # the step measured 2.115 ms with it vs 2.058 ms on the argmax-record path
-        # (pg_spmm_max_fwd / pg_spmm_max_bwd with fwd_out): the forward's list building and
-        # the split rows' sorted lists cost more than the pack pass they remove
-        self.grouped = os.environ.get("PLAGNN_GROUPED", "0") == "1" and all(
-            self.dg.can_group(pd[l]) for l in range(self.L))
         self._alloc_buffers(features)
         self._alloc_workspace()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -165,16 +157,12 @@ class TrainEngine:
         N, pd, dev = self.N, self.pd, self.device
         # ---- activations ----
         f32 = dict(dtype=torch.float32, device=dev)
-        self.HM, self.Pl, self.arg, self.lists = [], [], [], []
+        self.HM, self.Pl, self.arg = [], [], []
         for l in range(self.L):
             Fi = pd[l]
             self.HM.append(torch.zeros(N, 2 * Fi, **f32))
             self.Pl.append(torch.zeros(N, Fi, **f32))
-            if self.grouped:
-                self.lists.append(ops.WinnerLists(self.dg, Fi))
-                self.arg.append(self.lists[-1].argpos)
-            else:
-                self.arg.append(torch.zeros(N, Fi, dtype=self.dg.arg_dtype, device=dev))
+            self.arg.append(torch.zeros(N, Fi, dtype=self.dg.arg_dtype, device=dev))
         self.HM[0][:, :self.dims[0]] = features.to(dev, torch.float32)
         self.A3 = torch.zeros(N, pd[-3], **f32)
         self.A4 = torch.zeros(N, pd[-2], **f32)
@@ -196,14 +184,10 @@ class TrainEngine:
             Fi = pd[l]
             need = max(need, L.pg_spmm_max_fwd_workspace(self.dg.fwd.struct(self.ews), Fi, self.dg.arg_kind))
             need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd.struct(None), Fi))
-            need = max(need, L.pg_spmm_max_bwd_grouped_workspace(self.dg.bwd.struct(None), Fi))
         self._gemm_plans = {}
-        self._splitk_cnt: Dict[str, torch.Tensor] = {}
         # weight gradients' split-K combines deferred to one batched launch per step
-        # (PLAGNN_SPLITK_BATCH=0: one reduce launch per product)
         self._slabs: Dict[str, torch.Tensor] = {}
         self._jobs: list = []
-        self.defer_splitk = os.environ.get("PLAGNN_SPLITK_BATCH", "1") != "0"
         for (M_, N_, K_) in self._wgrad_shapes():
             sk = ops._split_k(M_, N_, K_)
             self._gemm_plans[(M_, N_, K_)] = sk
@@ -211,20 +195,6 @@ class TrainEngine:
         need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
         self.ws_bytes = self.ws.numel()
-        # PLAGNN_OVERLAP=1: weight gradients on a side stream, off the critical path (dgrad ->
-        # SpMM backward -> dgrad ...), with their own split-K workspace. Off by default: on
-        # one MI355X the captured step measured 2.125 ms with it vs 2.092 ms without (the
-        # GEMMs already fill the chip and crowd the latency-bound SpMM kernels).
-        # PLAGNN_OVERLAP=<prefix>: only the weight gradients whose tag starts with
-        # gemm.wgrad.<prefix> (e.g. "cat": dW_cat beside the SpMM backward of its layer)
-        ov = os.environ.get("PLAGNN_OVERLAP", "0")
-        self.overlap = ov not in ("0", "")
-        self.overlap_prefix = "gemm.wgrad." + ("" if ov == "1" else ov)
-        self.side = torch.cuda.Stream(dev) if self.overlap else None
-        need2 = 256
-        for (M_, N_, K_), sk in self._gemm_plans.items():
-            need2 = max(need2, L.pg_gemm_f32_workspace(M_, N_, K_, sk))
-        self.ws2 = torch.zeros(int(need2), dtype=torch.uint8, device=dev) if self.overlap else self.ws
 
     # ------------------------------------------------------------------ parameters
     def _wgrad_shapes(self):
@@ -321,33 +291,17 @@ class TrainEngine:
     def _s(self):
         return _lib.stream_handle(self.device)
 
-    def _splitk_counters(self, tag: str, M: int, N: int):
-        """This launch site's own split-K tile counters (zeroed once; every call leaves them
-        zero), so split GEMMs on different streams never share one. Only with
-        PLAGNN_SPLITK_INKERNEL=1: the in-kernel combine (last workgroup of a tile sums the
-        slabs) measured 2.25 ms/step on cfg2 against 2.06 ms with the separate reduce launch
-        (the last arrivers' slab reads form a serial tail at the end of every split GEMM)."""
-        if os.environ.get("PLAGNN_SPLITK_INKERNEL", "0") != "1":
-            return None
-        c = self._splitk_cnt.get(tag)
-        if c is None:
-            n = int(_lib.lib().pg_gemm_splitk_counters(M, N))
-            c = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
-            self._splitk_cnt[tag] = c
-        return c
-
     def _gemm(self, A, B, C, transa=False, transb=False, beta=0.0, bias=None, act=NONE, dact=None,
-              rowsum=None, tag="gemm", ws=None):
+              rowsum=None, tag="gemm"):
         M = A.shape[1] if transa else A.shape[0]
         K = A.shape[0] if transa else A.shape[1]
         N = B.shape[0] if transb else B.shape[1]
         sk = self._gemm_plans.get((M, N, K), 1) if (bias is None and act == NONE and dact is None) else 1
-        if sk > 1 and self.defer_splitk and ws is None:
+        if sk > 1:
             self._gemm_partials(A, B, C, transa, transb, beta, rowsum, tag, M, N, K, sk)
             return
-        cnt = self._splitk_counters(tag, M, N) if sk > 1 else None
-        ep = _lib.epilogue(bias, act, LEAKY_SLOPE, dact, rowsum, cnt)
-        ws = self.ws if ws is None else ws
+        ep = _lib.epilogue(bias, act, LEAKY_SLOPE, dact, rowsum)
+        ws = self.ws
         with self._t(tag, 2.0 * M * N * K):
             call("pg_gemm_f32", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
                  B.stride(0), beta, ptr(C), C.stride(0), ep, sk, ptr(ws), ws.numel(), self._s())
@@ -379,25 +333,6 @@ class TrainEngine:
             with self._t("gemm.splitk_reduce"):
                 call("pg_gemm_splitk_reduce_batch", arr, len(part), self._s())
 
-    def _wgrad(self, *args, **kw):
-        """A weight-gradient GEMM: forked onto the side stream at this point of the main
-        stream (it sees everything issued so far), joined back before Adam (_join)."""
-        if not self.overlap or not kw.get("tag", "").startswith(self.overlap_prefix):
-            self._gemm(*args, **kw)
-            return
-        main = torch.cuda.current_stream(self.device)
-        ev = torch.cuda.Event()
-        ev.record(main)
-        self.side.wait_event(ev)
-        with torch.cuda.stream(self.side):
-            self._gemm(*args, ws=self.ws2, **kw)
-
-    def _join(self):
-        if self.overlap:
-            ev = torch.cuda.Event()
-            ev.record(self.side)
-            torch.cuda.current_stream(self.device).wait_event(ev)
-
     def forward(self) -> None:
         """Logits (self.prob) and both losses; dZ = d train_loss / d z."""
         st = self._s()
@@ -412,14 +347,8 @@ class TrainEngine:
                        tag=f"gemm.fwd.pool.l{l + 1}")
             # M = max-aggregate(P) -> right half of HM
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
-                if self.grouped:
-                    W_ = self.lists[l]
-                    call("pg_spmm_max_fwd_grouped", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
-                         ptr(W_.argpos), Fi, ptr(W_.gfeat), ptr(W_.glist), ptr(W_.rcnt), ptr(self.ws),
-                         self.ws_bytes, st)
-                else:
-                    call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
-                         ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
+                call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
+                     ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
             # Y = [H | M] Wcat^T + b (fc_self + fc_neigh + bias), leaky_relu -> next input
             Fo = pd[l + 1]
             out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
@@ -446,9 +375,9 @@ class TrainEngine:
         g = self.dg.fwd.struct(self.ews)
         gt = self.dg.bwd.struct(None)
         # liner2: dW2 = dZ^T A4 (+ db2 = row sums of dZ^T); dA4 came from the fused head
-        self._wgrad(self.dZ, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
+        self._gemm(self.dZ, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
         # liner1
-        self._wgrad(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
+        self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
         self._gemm(self.dA4, P["liner1.W"], self.dA3, act=LEAKY, dact=self.A3, tag="gemm.dgrad.liner1")
         dY = self.dA3
         for l in reversed(range(self.L)):
@@ -456,7 +385,7 @@ class TrainEngine:
             Fi = pd[l]
             HM, dHM = self.HM[l], self.dHM[l]
             # d Wcat = dY^T [H | M], d b = sum_nodes dY
-            self._wgrad(dY, HM, G[p + "Wcat"], transa=True, rowsum=G[p + "b"], tag=f"gemm.wgrad.cat.l{l + 1}")
+            self._gemm(dY, HM, G[p + "Wcat"], transa=True, rowsum=G[p + "b"], tag=f"gemm.wgrad.cat.l{l + 1}")
             # d[H | M] = dY Wcat   (layer 1: only dM is needed)
             if l > 0:
                 self._gemm(dY, P[p + "Wcat"], dHM, tag=f"gemm.dgrad.cat.l{l + 1}")
@@ -464,17 +393,11 @@ class TrainEngine:
                 self._gemm(dY, P[p + "Wcat"][:, Fi:], dHM[:, Fi:], tag=f"gemm.dgrad.cat.l{l + 1}")
             # max backward with relu' of fc_pool fused; zero maxima (M = 0) are skipped
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                if self.grouped:
-                    W_ = self.lists[l]
-                    call("pg_spmm_max_bwd_grouped", g, gt, ptr(W_.gfeat), ptr(W_.glist), ptr(W_.rcnt),
-                         ptr(dHM[:, Fi:]), dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(self.dP[l]), Fi,
-                         ptr(self.ws), self.ws_bytes, st)
-                else:
-                    call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
-                         dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(self.dP[l]),
-                         Fi, ptr(self.ws), self.ws_bytes, st)
+                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
+                     dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(self.dP[l]),
+                     Fi, ptr(self.ws), self.ws_bytes, st)
             # d Wpool = dP^T H, d bpool = sum_nodes dP
-            self._wgrad(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
+            self._gemm(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
                         tag=f"gemm.wgrad.pool.l{l + 1}")
             if l > 0:
                 # dH = (dH_self + dP Wpool) * leaky'(H): H is the previous layer's output
@@ -483,7 +406,6 @@ class TrainEngine:
                            tag=f"gemm.dgrad.pool.l{l + 1}")
                 dY = dH
         self._reduce_deferred()
-        self._join()
 
     def adam(self) -> None:
         st = self._s()

@@ -112,16 +112,14 @@ class TrainEngineBF16(TrainEngine):
             sk = int(L.pg_gemm_bf16_split_k(M_, N_, K_))
             self._gemm_plans[(M_, N_, K_)] = sk
             need = max(need, L.pg_gemm_bf16_workspace(M_, N_, K_, sk))
-        need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C))
+        # the fused head (pg_mlp_head, run by forward()) and the standalone loss kernel
+        need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
         self.ws_bytes = self.ws.numel()
-        self.overlap = False
-        self.side = None
-        self.ws2 = self.ws
 
     # ------------------------------------------------------------------ kernels
     def _gemm(self, A, B, C, transa=False, transb=False, beta=0.0, bias=None, act=NONE, dact=None,
-              rowsum=None, tag="gemm", ws=None):
+              rowsum=None, tag="gemm"):
         M = A.shape[1] if transa else A.shape[0]
         K = A.shape[0] if transa else A.shape[1]
         N = B.shape[0] if transb else B.shape[1]

@@ -13,7 +13,6 @@ largest in-degree allows (else int32).
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -22,13 +21,13 @@ import torch
 from . import _lib
 from ._lib import PgCsr, call
 
-# in-CSR entries per forward work item before a row is split (tuning knob PLAGNN_CHUNK)
-DEFAULT_CHUNK = int(os.environ.get("PLAGNN_CHUNK", "256"))
-# out-CSR entries per backward work item, its work is data-dependent (knob PLAGNN_CHUNK_BWD;
+# in-CSR entries per forward work item before a row is split (CSRGraph(chunk=...))
+DEFAULT_CHUNK = 256
+# out-CSR entries per backward work item, its work is data-dependent (CSRGraph(chunk_bwd=...);
 # None = by graph size). Measured whole steps: S0 (24 041 nodes) 64-96 best (1.97 ms), 128
 # 1.99, 32 2.01, 256 2.11; RMAT x16 (384 656 nodes) 128 24.3 ms vs 64 25.2 ms: finer items
 # pay off only while the graph alone does not fill the chip.
-DEFAULT_CHUNK_BWD = int(os.environ["PLAGNN_CHUNK_BWD"]) if "PLAGNN_CHUNK_BWD" in os.environ else None
+DEFAULT_CHUNK_BWD = None
 
 
 def default_chunk_bwd(num_nodes: int) -> int:
@@ -168,11 +167,6 @@ class DeviceGraph:
     @property
     def is_cuda(self) -> bool:
         return self.device.type == "cuda"
-
-    def can_group(self, F: int) -> bool:
-        """Whether pg_spmm_max_fwd_grouped takes this graph at feature width F."""
-        return (self.is_cuda and self.arg_kind == _lib.PG_ARG_U16 and 0 < self.fwd.chunk <= 256
-                and self.fwd.einv is not None and F % 4 == 0 and self.num_nodes * F < 2 ** 31 - 1)
 
     def edge_weight_slots(self, edge_weight: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
         """Edge weights given per edge id (DGL order) -> in-CSR slot order, f32 contiguous."""

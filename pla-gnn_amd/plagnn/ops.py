@@ -108,74 +108,6 @@ def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
     return dx
 
 
-class WinnerLists:
-    """The grouped forward's winner lists (pg_spmm_max_fwd_grouped): gfeat [N, F] u16,
-    glist [tiles, nnz, 2] int32, rcnt [tiles, N] int32, plus the u16 argmax scratch the
-    schedule's split rows use. Allocated once per (graph, F) and reused every step."""
-
-    def __init__(self, dg: DeviceGraph, F: int):
-        n, dev = dg.num_nodes, dg.device
-        t = int(_lib.lib().pg_spmm_group_tiles(F))
-        self.F = F
-        self.gfeat = torch.empty(n, F, dtype=torch.int16, device=dev)
-        self.glist = torch.empty(t, max(dg.num_edges, 1), 2, dtype=torch.int32, device=dev)
-        self.rcnt = torch.empty(t, n, dtype=torch.int32, device=dev)
-        self.argpos = torch.empty(n, F, dtype=torch.int16, device=dev)
-
-
-def spmm_max_grouped(dg: DeviceGraph, X: torch.Tensor, ew_slots: Optional[torch.Tensor] = None,
-                     out: Optional[torch.Tensor] = None, lists: Optional[WinnerLists] = None,
-                     ws: Optional[torch.Tensor] = None):
-    """spmm_max that also builds the backward's winner lists (GPU, u16 records)."""
-    if X.dtype not in (torch.float32, torch.bfloat16):
-        raise TypeError("spmm_max_grouped: float32 or bfloat16 features expected")
-    if not dg.is_cuda:
-        raise TypeError("spmm_max_grouped runs on the GPU only")
-    bf = X.dtype == torch.bfloat16
-    _check_device(dg, X, ew_slots)
-    n, F = dg.num_nodes, X.shape[1]
-    if out is None:
-        out = torch.empty(n, F, dtype=X.dtype, device=X.device)
-    if lists is None:
-        lists = WinnerLists(dg, F)
-    g = dg.fwd.struct(ew_slots)
-    ws_n = _lib.lib().pg_spmm_max_fwd_workspace(g, F, _lib.PG_ARG_U16)
-    if ws is None:
-        ws = _workspace(ws_n, X.device)
-    else:
-        ws_n = ws.numel()
-    call("pg_spmm_max_fwd_grouped_bf16" if bf else "pg_spmm_max_fwd_grouped", g, ptr(X), _ld(X), F,
-         ptr(out), _ld(out), ptr(lists.argpos), _ld(lists.argpos), ptr(lists.gfeat), ptr(lists.glist),
-         ptr(lists.rcnt), ptr(ws), ws_n, _stream(X))
-    return out, lists
-
-
-def spmm_max_backward_grouped(dg: DeviceGraph, lists: WinnerLists, dout: torch.Tensor,
-                              ew_slots: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
-                              dx: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None
-                              ) -> torch.Tensor:
-    """dX from the winner lists of spmm_max_grouped; the relu' mask (the forward's input)
-    is required because the lists leave zero maxima out."""
-    _check_device(dg, dout, ew_slots, mask)
-    if mask is None:
-        raise ValueError("spmm_max_backward_grouped: mask (the forward's input) is required")
-    bf = dout.dtype == torch.bfloat16
-    n, F = dg.num_nodes, dout.shape[1]
-    if dx is None:
-        dx = torch.empty(n, F, dtype=dout.dtype, device=dout.device)
-    g = dg.fwd.struct(ew_slots)
-    gt = dg.bwd.struct(None)
-    ws_n = _lib.lib().pg_spmm_max_bwd_grouped_workspace(gt, F)
-    if ws is None:
-        ws = _workspace(ws_n, dout.device)
-    else:
-        ws_n = ws.numel()
-    call("pg_spmm_max_bwd_grouped_bf16" if bf else "pg_spmm_max_bwd_grouped", g, gt, ptr(lists.gfeat),
-         ptr(lists.glist), ptr(lists.rcnt), ptr(dout), _ld(dout), F, ptr(mask), _ld(mask), ptr(dx), _ld(dx),
-         ptr(ws), ws_n, _stream(dout))
-    return dx
-
-
 def spmm_max_backward_scatter(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
                               ew_slots: Optional[torch.Tensor] = None) -> torch.Tensor:
     """DGL-form backward with float atomics (non-deterministic summation order)."""
@@ -235,8 +167,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
          out: Optional[torch.Tensor] = None, alpha: float = 1.0, beta: float = 0.0,
          bias: Optional[torch.Tensor] = None, act: int = _lib.PG_ACT_NONE,
          slope: float = LEAKY_SLOPE, split_k: Optional[int] = None,
-         dact: Optional[torch.Tensor] = None, rowsum: Optional[torch.Tensor] = None,
-         splitk_cnt: Optional[torch.Tensor] = None) -> torch.Tensor:
+         dact: Optional[torch.Tensor] = None, rowsum: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = alpha*op(A)@op(B) + beta*C (+bias, act) on the fp32 MFMA kernel (GPU) or
     torch-CPU (CPU device). With `dact` (an activation output) the result is instead
     multiplied by act'(dact): the fused activation backward. With `rowsum`, also
@@ -274,7 +205,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
                         or beta not in (0.0, 1.0)) else _split_k(M, N, K)
     ws_n = _lib.lib().pg_gemm_f32_workspace(M, N, K, split_k)
     ws = _workspace(ws_n, A.device)
-    ep = _lib.epilogue(bias, act, slope, dact, rowsum, splitk_cnt)
+    ep = _lib.epilogue(bias, act, slope, dact, rowsum)
     call("pg_gemm_f32", int(transa), int(transb), M, N, K, alpha, ptr(A), _ld(A), ptr(B), _ld(B),
          beta, ptr(out), _ld(out), ep, split_k, ptr(ws), ws_n, _stream(A))
     return out

@@ -239,3 +239,26 @@ def test_rowwise_loc_correction_equals_vectorised(oracle_mod):
     for alpha in (0.1, 0.5):
         assert torch.equal(oracle_mod.protein_loc_correction(proba, alpha),
                            oracle_mod.protein_loc_correction(proba, alpha, rowwise=True))
+
+
+def test_decision_alignment(oracle_mod):
+    """spmm_max_align takes another computation's winner only when it is within tol of the
+    maximum; _act takes another computation's sign only at near-zero pre-activations."""
+    src = np.array([1, 2, 3], np.int64)
+    dst = np.array([0, 0, 0], np.int64)
+    og = oracle_mod.OracleGraph(src, dst, 4, self_loop=False)
+    X = np.array([[0.0, 0.0], [1.0, 5.0], [1.0 - 1e-7, 4.0], [0.5, 5.0]], np.float32)
+    out, ax, ae = oracle_mod.spmm_max(og, X)
+    assert ax[0].tolist() == [1, 1]
+    hint = np.full((4, 2), -1, np.int32)
+    hint[0] = [1, 1]  # positions: edge 1->0 is 0, 2->0 is 1, 3->0 is 2
+    n = oracle_mod.spmm_max_align(og, X, False, hint, 1e-7, out, ax, ae)  # band 1e-7 * max|out| = 5e-7
+    assert n == 1 and ax[0].tolist() == [2, 1] and out[0, 0] == np.float32(1.0 - 1e-7)
+    hint[0] = [2, 2]
+    n = oracle_mod.spmm_max_align(og, X, False, hint, 1e-7, out, ax, ae)
+    assert n == 1 and ax[0].tolist() == [2, 3]  # 0.5 is far from the max; the tie at 5.0 is taken
+    pre = torch.tensor([1e-9, -1e-9, 1.0, -1.0])
+    signs = {"s": torch.tensor([False, True, False, True])}
+    y = oracle_mod._act(pre, 0.01, "s", signs, 1e-5)
+    assert signs["_flips"] == 2
+    torch.testing.assert_close(y, torch.tensor([1e-11, -1e-9, 1.0, -0.01]), rtol=1e-6, atol=0)
