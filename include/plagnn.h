@@ -8,7 +8,7 @@
  *
  *   pg_csr_from_coo      <- dgl.graph((start, end), num_nodes=N) + dgl.add_self_loop
  *                           and DGL's lazy COO->CSC (in-CSR) build
- *                           (code/utils.py:74-75, first update_all at code/model.py:20)
+ *                           (code/utils.py:44-45, first update_all at code/model.py:20)
  *   pg_csr_transpose     <- DGL's reverse-graph CSR used by GSpMM.backward
  *   pg_spmm_max_fwd      <- update_all(copy_u('h','m'), max('m','neigh')) inside
  *                           SAGEConv(..., 'pool')  (code/model.py:13-15, 20, 22, 24)
@@ -124,7 +124,7 @@ typedef struct pg_csr {
                             transposed CSR (the inverse permutation of its eslot) */
 } pg_csr_t;
 
-/* ---------------- host: graph construction (code/utils.py:74-75) ---------------- */
+/* ---------------- host: graph construction (code/utils.py:44-45) ---------------- */
 
 /* COO (src[e], dst[e]) -> in-CSR: ptr[n_dst+1], col[nnz] = src, eid[nnz] = edge id.
  * Stable counting sort by dst, so each row lists its edges in ascending edge id. */

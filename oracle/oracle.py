@@ -8,7 +8,7 @@ missing instead of routing here.
 CPU restatement of the reference's training hot path:
 
 * graph construction — ``dgl.graph((start, end), num_nodes)`` + ``dgl.add_self_loop``
-  (code/utils.py:71-75) with DGL's CSC in ascending edge id (C: ``oracle_csc_build``);
+  (code/utils.py:44-45) with DGL's CSC in ascending edge id (C: ``oracle_csc_build``);
 * ``SAGEConv(in, out, 'pool')`` of DGL 0.8.2.post1 (code/model.py:7, 13-15, 20-25):
   ``P = relu(fc_pool(h))``; ``update_all(copy_u('h','m'), max('m','neigh'))`` with argmax
   (C: ``oracle_spmm_max``); ``rst = fc_self(h) + fc_neigh(neigh) + bias``; backward of the
@@ -114,7 +114,7 @@ class OracleGraph:
         src = np.asarray(src, dtype=np.int64)
         dst = np.asarray(dst, dtype=np.int64)
         n = int(num_nodes)
-        if self_loop:  # dgl.add_self_loop: loops appended, edge ids E..E+N-1 (utils.py:75)
+        if self_loop:  # dgl.add_self_loop: loops appended, edge ids E..E+N-1 (utils.py:45)
             loops = np.arange(n, dtype=np.int64)
             src = np.concatenate([src, loops])
             dst = np.concatenate([dst, loops])

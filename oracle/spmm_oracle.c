@@ -8,7 +8,7 @@
  * /root/reference and not installed here) runs under the reference's call sites:
  *
  *   oracle_csc_build   dgl.graph((start, end), num_nodes) + dgl.add_self_loop
- *                      (code/utils.py:74-75) and the lazily built CSC that update_all
+ *                      (code/utils.py:44-45) and the lazily built CSC that update_all
  *                      walks (first use at code/model.py:20): in-edges of each
  *                      destination in ascending edge id, self-loop ids E..E+N-1 last.
  *   oracle_spmm_max    SpMMCmpCsr<copy_lhs|u_mul_e, Max> reached from SAGEConv('pool')'s

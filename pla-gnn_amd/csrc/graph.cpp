@@ -1,6 +1,6 @@
 // Host-side graph construction for the plagnn C-ABI.
 //
-// Replaces what DGL does below code/utils.py:74-75 (dgl.graph((start, end), N) then
+// Replaces what DGL does below code/utils.py:44-45 (dgl.graph((start, end), N) then
 // dgl.add_self_loop) and at the first update_all (code/model.py:20): the COO edge list
 // (self-loops already appended by the caller with edge ids E..E+N-1) becomes the
 // in-CSR that DGL's SpMMCmpCsr walks, each destination row listing its in-edges in

@@ -2,10 +2,10 @@
 MI355X message-passing engine (``plagnn``).
 
 The reference touches exactly this surface:
-  import dgl                                         code/utils.py:34, main_normal.py:9-15
-  dgl.graph((start, end), num_nodes=N)               code/utils.py:74
-  dgl.add_self_loop(g)                               code/utils.py:75
-  g.nodes[list(range(N))].data[key] = tensor         code/utils.py:76, 79
+  import dgl                                         code/utils.py:4, main_normal.py:9-15
+  dgl.graph((start, end), num_nodes=N)               code/utils.py:44
+  dgl.add_self_loop(g)                               code/utils.py:45
+  g.nodes[list(range(N))].data[key] = tensor         code/utils.py:46, 49
   g.ndata['feat'], g.ndata['loc']                    code/train.py:145-146, 179
   g.to(device)                                       code/main_normal.py:66
   dgl.seed(seed)                                     code/main_normal.py:15
@@ -79,7 +79,7 @@ class _NodeDataView:
         if idx is not None:
             ids = torch.as_tensor(idx, dtype=torch.int64).reshape(-1)
             if ids.numel() == n and bool((ids == torch.arange(n)).all()):
-                idx = None  # full, in order (code/utils.py:76, 79 pass list(range(N)))
+                idx = None  # full, in order (code/utils.py:46, 49 pass list(range(N)))
         if idx is None:
             self._g.ndata[key] = value
             return
@@ -266,7 +266,7 @@ def _as_ids(x) -> torch.Tensor:
 
 
 def graph(data, num_nodes: Optional[int] = None, idtype=None, device=None, **kwargs) -> DGLGraph:
-    """dgl.graph((U, V), num_nodes=N): edge i goes U[i] -> V[i] (code/utils.py:74)."""
+    """dgl.graph((U, V), num_nodes=N): edge i goes U[i] -> V[i] (code/utils.py:44)."""
     if isinstance(data, tuple) and len(data) == 2:
         src, dst = _as_ids(data[0]), _as_ids(data[1])
     else:
@@ -283,7 +283,7 @@ def graph(data, num_nodes: Optional[int] = None, idtype=None, device=None, **kwa
 
 
 def add_self_loop(g: DGLGraph, etype=None) -> DGLGraph:
-    """dgl.add_self_loop (code/utils.py:75): one loop per node appended, so the new
+    """dgl.add_self_loop (code/utils.py:45): one loop per node appended, so the new
     edges get ids E..E+N-1 (existing loops are kept; duplicates allowed). Edge features
     of the new loops are zero-filled, as DGL does."""
     n = g.num_nodes()

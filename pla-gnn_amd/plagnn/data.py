@@ -142,7 +142,7 @@ class Dataset:
 
     @property
     def feat(self) -> np.ndarray:
-        """hstack(expr, gcn, ecc) as float32: code/utils.py:77-78."""
+        """hstack(expr, gcn, ecc) as float32: code/utils.py:47-48."""
         return np.hstack((self.expr, np.hstack((self.gcn, self.ecc)))).astype(np.float32)
 
     @property
@@ -150,7 +150,7 @@ class Dataset:
         return np.nonzero(self.loc.sum(1) > 0)[0]
 
     def edges_with_self_loops(self):
-        """COO src/dst of dgl.add_self_loop(dgl.graph((row, col), N)) (utils.py:74-75)."""
+        """COO src/dst of dgl.add_self_loop(dgl.graph((row, col), N)) (utils.py:44-45)."""
         loops = np.arange(self.n)
         return (np.concatenate([self.row.astype(np.int64), loops]),
                 np.concatenate([self.col.astype(np.int64), loops]))

@@ -1,6 +1,6 @@
 """Graph storage for the message-passing engine.
 
-Host side: the COO edge list (self-loops already appended, code/utils.py:74-75) becomes
+Host side: the COO edge list (self-loops already appended, code/utils.py:44-45) becomes
 an in-CSR (DGL's CSC: rows = destinations, each row in ascending edge id) and its
 transpose (rows = sources, destinations ascending, with the in-CSR slot of every edge),
 plus the longest-first work schedules the kernels consume. All of it is built by the

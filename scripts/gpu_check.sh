@@ -17,5 +17,10 @@ fi
 if [ "${BENCH:-1}" = "1" ]; then
   timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
   rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+if [ "${PROFILE:-0}" = "1" ]; then
+  cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-legs ${BENCH_ARGS:-} > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/prof.err
+  rc=$?; cd $GRAFT_REPO_ROOT; echo "rocprof rc=$rc"; tail -2 gpurun_out/prof.err
 fi
 exit $rc

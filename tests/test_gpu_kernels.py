@@ -228,9 +228,11 @@ def test_col_sum_act_bwd():
     torch.testing.assert_close(dyd.cpu(), ref, rtol=0, atol=0)
 
 
-def test_sigmoid_multi_loss_matches_reference_golden(oracle_mod):
-    """Loss and d loss / d prob of the fused kernel vs the reference's multi_loss
-    (golden vectors from code/train.py:89-108)."""
+def test_sigmoid_multi_loss_matches_oracle_on_golden_inputs(oracle_mod):
+    """Loss and d loss / d z of the fused kernel vs the oracle's multi_loss (code/train.py:
+    89-108) on logits re-derived from the golden fixture's probabilities. The pinning to
+    the reference's own output is transitive: the oracle matches the golden loss itself in
+    tests/test_oracle.py::test_multi_loss_matches_reference_golden."""
     import os
 
     from plagnn import _lib

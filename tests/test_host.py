@@ -120,7 +120,7 @@ def test_cpu_backend_sum_mean(oracle_mod):
 
 
 def test_dgl_shim_surface_like_utils_create_graph():
-    """The exact call sequence of code/utils.py:71-79 and train.py:145-146."""
+    """The exact call sequence of code/utils.py:28-51 and train.py:145-146."""
     import dgl
     from scipy.sparse import coo_matrix
 
