@@ -170,33 +170,6 @@ int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, i
                     const float* mask_src, int64_t ldm, const float* fwd_out, int64_t ldf,
                     float* dx, int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream);
 
-/* Winner masks (what TrainEngine runs): the forward also records, for every in-CSR slot
- * s = (row v, in-row position p) and feature f, bit f of wmask[s * W ...] (W =
- * pg_spmm_winner_words(F) = ceil(F / 32) uint32 words per slot) when the edge at s wins
- * (v, f) and the stored maximum out[v, f] is not 0. Same out[] as pg_spmm_max_fwd; argpos
- * may be NULL (the records are then not written). Every slot's W words are written.
- * Workspace: pg_spmm_max_fwd_workspace(g, F, arg_kind). F <= 4096. */
-int64_t pg_spmm_winner_words(int64_t F);
-int pg_spmm_max_fwd_masks(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
-                          int64_t ldo, void* argpos, int64_t lda, int arg_kind, uint32_t* wmask,
-                          void* ws, size_t ws_bytes, pg_stream_t stream);
-int pg_spmm_max_fwd_masks_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t F, void* out,
-                               int64_t ldo, void* argpos, int64_t lda, int arg_kind, uint32_t* wmask,
-                               void* ws, size_t ws_bytes, pg_stream_t stream);
-/* Backward from the winner masks: dx[u,f] = sum over u's out-edges (u -> v, slot s) in
- * ascending v of [bit f of wmask[s]] * ew[s] * dout[v,f]; then dx *= (mask_src > 0) when
- * mask_src != NULL. With the masks' zero-maximum rule this equals pg_spmm_max_bwd with
- * fwd_out and mask_src = the forward's input X, bitwise on rows not split by gt's schedule,
- * whenever X >= 0 (a relu output: then mask_src is implied and may be NULL). Needs F <= 1024,
- * F and the leading dims multiples of 4, rows aligned to 4 elements. */
-size_t pg_spmm_max_bwd_masks_workspace(const pg_csr_t* gt, int64_t F);
-int pg_spmm_max_bwd_masks(const pg_csr_t* g, const pg_csr_t* gt, const uint32_t* wmask, int64_t F,
-                          const float* dout, int64_t ldd, const float* mask_src, int64_t ldm, float* dx,
-                          int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream);
-int pg_spmm_max_bwd_masks_bf16(const pg_csr_t* g, const pg_csr_t* gt, const uint32_t* wmask, int64_t F,
-                               const void* dout, int64_t ldd, const void* mask_src, int64_t ldm, void* dx,
-                               int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream);
-
 /* DGL-form backward: dx = 0; dx[src(argpos[v,f]), f] += ew * dout[v,f] with f32
  * atomics (summation order not reproducible). The callee zero-fills dx. */
 int pg_spmm_max_bwd_scatter(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,
@@ -437,7 +410,7 @@ int pg_perturb_fill(const double* xc_normal, const double* xc_inter, const doubl
 /* ---------------- misc ---------------- */
 const char* pg_last_error_string(void);
 int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-kernel split-K
-                         (epilogue without splitk_cnt), no grouped SpMM pair; winner masks */
+                         (epilogue without splitk_cnt), no grouped SpMM pair */
 
 #ifdef __cplusplus
 }

@@ -163,43 +163,27 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Winner masks (MASK): for every in-CSR slot s = (row v, position p) and feature f,
-// bit f of wmask[s * wtot ...] (wtot = ceil(F / 32) words per slot) is set when the edge at
-// s wins (v, f) AND the stored maximum out[v, f] is not 0. A zero maximum contributes
-// nothing to the backward when the aggregated input is nonnegative (a relu output): its
-// winner u has X[u, f] * w == 0, so X[u, f] == 0 (relu' = 0) or w == 0. The backward
-// (max_bwd_mask_kernel) reads, per out-edge of a source, the edge's mask word for each
-// lane's features and pulls only the upstream gradients it won: no argmax record, no
-// grouping pass. Unsplit rows build their masks in a wave-private LDS image, 64 positions
-// at a time; split rows get theirs from the merge kernel.
-constexpr int kMaskPosBlock = 64;
-
-template <int W, int NC, bool HAS_W, typename A, typename T = float, bool MASK = false>
+template <int W, int NC, bool HAS_W, typename A, typename T = float>
 __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
     const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
     const int32_t* __restrict__ eslot, const float* __restrict__ ew,
     const int4* __restrict__ items, int n_items, const T* __restrict__ X, int64_t ldx, int F,
     T* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
-    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, int n_ftiles = 1, int ftile = 0,
-    uint32_t* __restrict__ wmask = nullptr, int wtot = 0) {
+    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, int n_ftiles = 1, int ftile = 0) {
   constexpr int U = EdgeU<W, NC>::value;
-  constexpr int WT = NC * kWave * W / 32;  // mask words per position in this feature tile
-  __shared__ uint32_t mlds[MASK ? kWavesPerBlock * kMaskPosBlock * WT : 1];
   // n_ftiles > 1: all feature tiles of F in one launch, block b -> (item block b / n_ftiles,
   // tile b % n_ftiles), so every tile's longest items start first
   int bx = blockIdx.x;
-  int wofs = 0;  // this tile's first mask word
   if (n_ftiles > 1) {
     const int t = bx % n_ftiles;
     bx /= n_ftiles;
     const int f0 = t * ftile;
     X += f0;
     out += f0;
-    if (arg) arg += f0;
+    arg += f0;
     if (ws_val) ws_val += f0;
     if (ws_arg) ws_arg += f0;
     F = min(ftile, F - f0);
-    wofs = f0 / 32;
   }
   const int it = bx * kWavesPerBlock + wave_id_uniform();
   if (it >= n_items) return;
@@ -263,37 +247,12 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
       for (int i = 0; i < W; ++i)
         if (__builtin_isinf(best[c][i])) best[c][i] = 0.f;
     T* orow = out + (int64_t)row * ldo;
+    A* arow = arg + (int64_t)row * lda;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int f = (c * kWave + lane) * W;
       store_tile<W, T>(orow, f, F, best[c]);
-      if (arg) store_arg<W, A>(arg + (int64_t)row * lda, f, F, bpos[c]);
-    }
-    if constexpr (MASK) {
-      uint32_t* ml = mlds + wave_id_uniform() * (kMaskPosBlock * WT);
-      const int deg = k1 - k0;
-      const int wvalid = min(WT, wtot - wofs);  // words of this tile inside the row's wtot
-      for (int pb = 0; pb < deg; pb += kMaskPosBlock) {
-        const int np = min(kMaskPosBlock, deg - pb);
-        for (int i = lane; i < np * WT; i += kWave) ml[i] = 0u;
-        wave_lds_sync();
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-#pragma unroll
-          for (int i = 0; i < W; ++i) {
-            const int fl = (c * kWave + lane) * W + i;
-            const int p = bpos[c][i] - pb;
-            // the stored value decides (a bf16 maximum that rounds to 0 is a zero maximum)
-            if (fl < F && bpos[c][i] != arg_none<A>() && p >= 0 && p < np && to_f(from_f<T>(best[c][i])) != 0.f)
-              atomicOr(&ml[p * WT + (fl >> 5)], 1u << (fl & 31));
-          }
-        wave_lds_sync();
-        for (int i = lane; i < np * WT; i += kWave) {
-          const int q = i / WT, w = i - q * WT;
-          if (w < wvalid) wmask[(int64_t)(rs + pb + q) * wtot + wofs + w] = ml[i];
-        }
-        wave_lds_sync();
-      }
+      store_arg<W, A>(arow, f, F, bpos[c]);
     }
   } else {
     float* orow = ws_val + (int64_t)slot * ldw;
@@ -304,168 +263,6 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
       store_tile<W>(orow, f, F, best[c]);
       store_arg<W, A>(arow, f, F, bpos[c]);
     }
-  }
-}
-
-// Split rows with winner masks: the partial maxima combined as max_merge_kernel does, the
-// final positions kept in LDS; then the row's whole mask region is zeroed and every nonzero
-// word written once: per 32-feature group (lanes 0-31 of a wave), the leader of each
-// distinct winning position writes that position's word (a ballot of the group's features
-// it won). F <= kMergeMaskMaxF.
-constexpr int kMergeMaskMaxF = 4096;
-
-template <typename A, typename T = float>
-__global__ __launch_bounds__(kBlock) void max_merge_mask_kernel(
-    const int4* __restrict__ merges, const int32_t* __restrict__ ptr, int F, const float* __restrict__ ws_val,
-    const A* __restrict__ ws_arg, int64_t ldw, T* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
-    uint32_t* __restrict__ wmask, int wtot) {
-  __shared__ int32_t spos[kMergeMaskMaxF];
-  const int4 m = merges[blockIdx.x];
-  const int row = m.x, s0 = m.y, ns = m.z;
-  for (int f = threadIdx.x; f < F; f += kBlock) {
-    float best = -std::numeric_limits<float>::infinity();
-    int bp = arg_none<A>();
-    for (int s = s0; s < s0 + ns; s += 8) {
-      float v[8];
-      int a[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int64_t o = (int64_t)min(s + e, s0 + ns - 1) * ldw + f;
-        v[e] = ws_val[o];
-        a[e] = (int)ws_arg[o];
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (s + e < s0 + ns && v[e] > best) {
-          best = v[e];
-          bp = a[e];
-        }
-    }
-    if (__builtin_isinf(best)) best = 0.f;
-    const T bt = from_f<T>(best);
-    out[(int64_t)row * ldo + f] = bt;
-    if (arg) arg[(int64_t)row * lda + f] = (A)bp;
-    spos[f] = (bp != arg_none<A>() && to_f(bt) != 0.f) ? bp : -1;
-  }
-  const int rs = ptr[row];
-  const int64_t n_words = (int64_t)(ptr[row + 1] - rs) * wtot;
-  uint32_t* mr = wmask + (int64_t)rs * wtot;
-  for (int64_t i = threadIdx.x; i < n_words; i += kBlock) mr[i] = 0u;
-  __threadfence_block();
-  __syncthreads();
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
-  for (int g = wave; g < wtot; g += kWavesPerBlock) {
-    const int f = g * 32 + lane;
-    const int p = (lane < 32 && f < F) ? (int)spos[f] : -1;
-    uint64_t active = __ballot(p >= 0);
-    while (active) {
-      const int leader = __ffsll((long long)active) - 1;
-      const int pl = __builtin_amdgcn_readlane(p, leader);
-      const uint64_t bits = __ballot(p == pl);
-      if (lane == leader) mr[(int64_t)pl * wtot + g] = (uint32_t)bits;
-      active &= ~bits;
-    }
-  }
-}
-
-// ---- max backward from winner masks --------------------------------------------------
-// Wave per source item (u, t0, t1, slot) of the transposed CSR; lane l owns features
-// c * 256 + 4 l .. + 3 (NC 256-column tiles, accumulated in registers). For each out-edge
-// (u -> v, in-CSR slot s) in ascending v, each lane reads the nibble of wmask[s] for its
-// features; only when it is not zero does it load dout[v] for them (float4 / 4 x bf16) and
-// add (* w) the bits it won. U edges in flight: their mask words first, then their upstream
-// rows. Every feature sums its terms in ascending destination v, the order of the
-// sequential scatter_add_ (bit-exact on unsplit rows); split rows go to slots and are
-// combined in chunk order by sum_merge_kernel.
-template <int NC, bool HAS_W, typename T>
-__global__ __launch_bounds__(kBlock) void max_bwd_mask_kernel(
-    const float* __restrict__ ew, const int32_t* __restrict__ tcol, const int32_t* __restrict__ tslot,
-    const int4* __restrict__ items, int n_items, const uint32_t* __restrict__ wmask, int wtot,
-    const T* __restrict__ dout, int64_t ldd, int F, const T* __restrict__ mask, int64_t ldm,
-    T* __restrict__ dx, int64_t ldx, float* __restrict__ ws, int64_t ldw) {
-  constexpr int W = 4;
-  constexpr int U = NC <= 2 ? 8 : 4;
-  const int it = blockIdx.x * kWavesPerBlock + wave_id_uniform();
-  if (it >= n_items) return;
-  const int4 item = items[it];
-  const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
-  const int lane = lane_id();
-  int widx[NC];  // this lane's mask word in each tile (-1 past wtot)
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int wi = (c * kWave * W + lane * W) >> 5;
-    widx[c] = wi < wtot ? wi : -1;
-  }
-  const int sh = (lane * W) & 31;
-  float acc[NC][W];
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-#pragma unroll
-    for (int i = 0; i < W; ++i) acc[c][i] = 0.f;
-
-  for (int tw = t0; tw < t1; tw += kWave) {
-    const int nw = min(kWave, t1 - tw);
-    const int tl = tw + min(lane, nw - 1);
-    const int vv = tcol[tl];
-    const int sv = tslot[tl];
-    float wv = 1.f;
-    if constexpr (HAS_W) wv = ew[sv];
-    for (int j = 0; j < nw; j += U) {
-      const int nv = min(U, nw - j);
-      uint32_t mb[U][NC];
-#pragma unroll
-      for (int e = 0; e < U; ++e) {
-        const uint32_t* mr = wmask + (int64_t)bcast(sv, j + min(e, nv - 1)) * wtot;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) mb[e][c] = widx[c] >= 0 ? (mr[widx[c]] >> sh) & 0xFu : 0u;
-      }
-      float d[U][NC][W];
-#pragma unroll
-      for (int e = 0; e < U; ++e) {
-        const T* dr = dout + (int64_t)bcast(vv, j + min(e, nv - 1)) * ldd;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          if (mb[e][c]) {
-            load_tile<W, T>(dr, (c * kWave + lane) * W, F, d[e][c], 0.f);
-          } else {
-#pragma unroll
-            for (int i = 0; i < W; ++i) d[e][c][i] = 0.f;
-          }
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < U; ++e) {
-        if (e < nv) {
-          float w = 1.f;
-          if constexpr (HAS_W) w = bcastf(wv, j + e);
-#pragma unroll
-          for (int c = 0; c < NC; ++c)
-#pragma unroll
-            for (int i = 0; i < W; ++i)
-              if ((mb[e][c] >> i) & 1u) acc[c][i] += HAS_W ? w * d[e][c][i] : d[e][c][i];
-        }
-      }
-    }
-  }
-
-  if (slot < 0) {
-    T* xr = dx + (int64_t)row * ldx;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int f = (c * kWave + lane) * W;
-      if (mask) {
-        float mk[W];
-        load_tile<W, T>(mask + (int64_t)row * ldm, f, F, mk, 0.f);
-#pragma unroll
-        for (int i = 0; i < W; ++i)
-          if (!(mk[i] > 0.f)) acc[c][i] = 0.f;
-      }
-      store_tile<W, T>(xr, f, F, acc[c]);
-    }
-  } else {
-    float* wr = ws + (int64_t)slot * ldw;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) store_tile<W>(wr, (c * kWave + lane) * W, F, acc[c]);
   }
 }
 
@@ -1240,7 +1037,7 @@ inline TilePlan plan_tiles(int64_t F, std::initializer_list<int64_t> lds,
 template <typename A, typename T>
 int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
                    int64_t ldo, A* arg, int64_t lda, float* ws_val, A* ws_arg, int64_t ldw,
-                   hipStream_t st, uint32_t* wmask = nullptr) {
+                   hipStream_t st) {
   // argpos rows: u16 x4 = 8 B -> need 8-B alignment only; treat via the same 16-B check on
   // the float operands and an 8-B check on arg.
   TilePlan tp = plan_tiles(F, {ldx, ldo, lda}, {X, out, ws_val});
@@ -1256,21 +1053,14 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
   {
     const int64_t f0 = 0;
     const int Ft = (int)std::min<int64_t>(tp.tile, F);
-    const int wtot = (int)((F + 31) / 32);
     auto go = [&](auto nc_c, auto w_c, auto hw_c) -> int {
       constexpr int NC = decltype(nc_c)::value;
       constexpr int W = decltype(w_c)::value;
       constexpr bool HW = decltype(hw_c)::value;
-      if (wmask)
-        hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T, true>), dim3((unsigned)blocks * n_ft), dim3(kBlock), 0,
-                           st, g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
-                           X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, n_ft,
-                           (int)tp.tile, wmask, wtot);
-      else
-        hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T>), dim3((unsigned)blocks * n_ft), dim3(kBlock), 0, st,
-                           g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
-                           X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, n_ft,
-                           (int)tp.tile, nullptr, 0);
+      hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T>), dim3((unsigned)blocks * n_ft), dim3(kBlock), 0, st,
+                         g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
+                         X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, n_ft,
+                         (int)tp.tile);
       return PG_OK;
     };
     int rc;
@@ -1284,11 +1074,7 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
                  : dispatch_nc_scalar(nc, [&](auto n) { return go(n, std::integral_constant<int, 1>{}, std::false_type{}); });
     }
     if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_max_fwd: unsupported feature tile");
-    if (g->n_merges > 0 && wmask) {
-      hipLaunchKernelGGL((max_merge_mask_kernel<A, T>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
-                         (const int4*)g->merges, g->ptr, (int)F, ws_val, ws_arg, ldw, out, ldo, arg, lda, wmask,
-                         wtot);
-    } else if (g->n_merges > 0) {
+    if (g->n_merges > 0) {
       hipLaunchKernelGGL((max_merge_kernel<A, T>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
                          (const int4*)g->merges, (int)g->n_merges, (int)F, ws_val + f0, ws_arg + f0,
                          ldw, out + f0, ldo, arg + f0, lda);
@@ -1364,7 +1150,7 @@ namespace {
 template <typename T>
 int max_fwd_entry(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out, int64_t ldo,
                   void* argpos, int64_t lda, int arg_kind, void* ws, size_t ws_bytes,
-                  pg_stream_t stream, uint32_t* wmask = nullptr) {
+                  pg_stream_t stream) {
   PG_TRY(pg::check_csr(g, "pg_spmm_max_fwd", true));
   if (!pg::valid_arg_kind(arg_kind))
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: bad arg_kind %d", arg_kind);
@@ -1374,9 +1160,7 @@ int max_fwd_entry(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: max degree %d needs PG_ARG_I32",
                          g->max_deg);
   if (F == 0 || g->n_rows == 0) return pg::ok();
-  if (!X || !out || (!argpos && !wmask)) return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: NULL buffer");
-  if (wmask && F > kMergeMaskMaxF)
-    return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm_max_fwd_masks: F <= %d", kMergeMaskMaxF);
+  if (!X || !out || !argpos) return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: NULL buffer");
   const size_t need = pg_spmm_max_fwd_workspace(g, F, arg_kind);
   PG_TRY(check_ws(ws_bytes, need, "pg_spmm_max_fwd"));
   const int64_t ldw = ws_ld(F);
@@ -1385,9 +1169,9 @@ int max_fwd_entry(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
   hipStream_t st = (hipStream_t)stream;
   if (arg_kind == PG_ARG_U16)
     return launch_max_fwd<uint16_t, T>(g, X, ldx, F, out, ldo, (uint16_t*)argpos, lda, ws_val,
-                                       (uint16_t*)ws_arg, ldw, st, wmask);
+                                       (uint16_t*)ws_arg, ldw, st);
   return launch_max_fwd<int32_t, T>(g, X, ldx, F, out, ldo, (int32_t*)argpos, lda, ws_val,
-                                    (int32_t*)ws_arg, ldw, st, wmask);
+                                    (int32_t*)ws_arg, ldw, st);
 }
 
 }  // namespace
@@ -1405,23 +1189,6 @@ int pg_spmm_max_fwd_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t 
                          size_t ws_bytes, pg_stream_t stream) {
   return max_fwd_entry<uint16_t>(g, (const uint16_t*)X, ldx, F, (uint16_t*)out, ldo, argpos, lda,
                                  arg_kind, ws, ws_bytes, stream);
-}
-
-int64_t pg_spmm_winner_words(int64_t F) { return F > 0 ? (F + 31) / 32 : 0; }
-
-int pg_spmm_max_fwd_masks(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
-                          int64_t ldo, void* argpos, int64_t lda, int arg_kind, uint32_t* wmask,
-                          void* ws, size_t ws_bytes, pg_stream_t stream) {
-  if (!wmask && g && g->nnz > 0) return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd_masks: wmask is NULL");
-  return max_fwd_entry<float>(g, X, ldx, F, out, ldo, argpos, lda, arg_kind, ws, ws_bytes, stream, wmask);
-}
-
-int pg_spmm_max_fwd_masks_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t F, void* out,
-                               int64_t ldo, void* argpos, int64_t lda, int arg_kind, uint32_t* wmask,
-                               void* ws, size_t ws_bytes, pg_stream_t stream) {
-  if (!wmask && g && g->nnz > 0) return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd_masks: wmask is NULL");
-  return max_fwd_entry<uint16_t>(g, (const uint16_t*)X, ldx, F, (uint16_t*)out, ldo, argpos, lda,
-                                 arg_kind, ws, ws_bytes, stream, wmask);
 }
 
 // [split-row partials][grouped path: gfeat N x F u16 | glist nnz x int2 | dpack N x F f32 |
@@ -1545,75 +1312,6 @@ int pg_spmm_max_bwd_bf16(const pg_csr_t* g, const pg_csr_t* gt, const void* argp
   return max_bwd_entry<uint16_t>(g, gt, argpos, lda, arg_kind, (const uint16_t*)dout, ldd, F,
                                  (const uint16_t*)mask_src, ldm, (const uint16_t*)fwd_out, ldf,
                                  (uint16_t*)dx, ldx, ws, ws_bytes, stream);
-}
-
-}  // extern "C"
-
-namespace {
-
-template <typename T>
-int max_bwd_masks_entry(const pg_csr_t* g, const pg_csr_t* gt, const uint32_t* wmask, int64_t F, const T* dout,
-                        int64_t ldd, const T* mask_src, int64_t ldm, T* dx, int64_t ldx, void* ws, size_t ws_bytes,
-                        pg_stream_t stream) {
-  const char* who = "pg_spmm_max_bwd_masks";
-  PG_TRY(pg::check_csr(g, who, false));
-  PG_TRY(pg::check_csr(gt, who, true));
-  if (gt->n_cols != g->n_rows || gt->nnz != g->nnz)
-    return pg::set_error(PG_ERR_INVALID, "%s: gt is not the transpose of g", who);
-  if (gt->nnz > 0 && !gt->eslot) return pg::set_error(PG_ERR_INVALID, "%s: gt needs eslot", who);
-  if (F < 0 || ldd < F || ldx < F || (mask_src && ldm < F))
-    return pg::set_error(PG_ERR_INVALID, "%s: bad F/leading dims", who);
-  if (F == 0 || gt->n_rows == 0) return pg::ok();
-  if (!dout || !dx || (gt->nnz > 0 && !wmask)) return pg::set_error(PG_ERR_INVALID, "%s: NULL buffer", who);
-  constexpr uintptr_t kA = 4 * sizeof(T) - 1;
-  if (F % 4 || ldd % 4 || ldx % 4 || (mask_src && ldm % 4) || ((uintptr_t)dout & kA) || ((uintptr_t)dx & kA) ||
-      ((uintptr_t)mask_src & kA) || F > kMaxNC * kWave * 4)
-    return pg::set_error(PG_ERR_UNSUPPORTED, "%s: needs F <= %d, F and leading dims multiples of 4, aligned rows",
-                         who, kMaxNC * kWave * 4);
-  const size_t need = bwd_partials_bytes(gt, F);
-  PG_TRY(check_ws(ws_bytes, need, who));
-  float* w = need ? (float*)ws : nullptr;
-  hipStream_t st = (hipStream_t)stream;
-  const int wtot = (int)((F + 31) / 32);
-  const int blocks = grid_for(gt->n_items);
-  auto go = [&](auto nc_c, auto hw_c) -> int {
-    constexpr int NC = decltype(nc_c)::value;
-    constexpr bool HW = decltype(hw_c)::value;
-    hipLaunchKernelGGL((max_bwd_mask_kernel<NC, HW, T>), dim3(blocks), dim3(kBlock), 0, st, g->ew, gt->col,
-                       gt->eslot, (const int4*)gt->items, (int)gt->n_items, wmask, wtot, dout, ldd, (int)F,
-                       mask_src, ldm, dx, ldx, w, ws_ld(F));
-    return PG_OK;
-  };
-  const int nc = (int)((F + 255) / 256);
-  const int rc = g->ew ? dispatch_nc_vec(nc, [&](auto n) { return go(n, std::true_type{}); })
-                       : dispatch_nc_vec(nc, [&](auto n) { return go(n, std::false_type{}); });
-  if (rc != PG_OK) return pg::set_error(rc, "%s: unsupported feature count", who);
-  if (gt->n_merges > 0)
-    hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
-                       (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0, mask_src, ldm,
-                       dx, ldx);
-  return hip_status(who);
-}
-
-}  // namespace
-
-extern "C" {
-
-int pg_spmm_max_bwd_masks(const pg_csr_t* g, const pg_csr_t* gt, const uint32_t* wmask, int64_t F,
-                          const float* dout, int64_t ldd, const float* mask_src, int64_t ldm, float* dx,
-                          int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream) {
-  return max_bwd_masks_entry<float>(g, gt, wmask, F, dout, ldd, mask_src, ldm, dx, ldx, ws, ws_bytes, stream);
-}
-
-int pg_spmm_max_bwd_masks_bf16(const pg_csr_t* g, const pg_csr_t* gt, const uint32_t* wmask, int64_t F,
-                               const void* dout, int64_t ldd, const void* mask_src, int64_t ldm, void* dx,
-                               int64_t ldx, void* ws, size_t ws_bytes, pg_stream_t stream) {
-  return max_bwd_masks_entry<uint16_t>(g, gt, wmask, F, (const uint16_t*)dout, ldd, (const uint16_t*)mask_src, ldm,
-                                       (uint16_t*)dx, ldx, ws, ws_bytes, stream);
-}
-
-size_t pg_spmm_max_bwd_masks_workspace(const pg_csr_t* gt, int64_t F) {
-  return gt && F > 0 ? bwd_partials_bytes(gt, F) : 0;
 }
 
 int pg_spmm_max_bwd_scatter(const pg_csr_t* g, const void* argpos, int64_t lda, int arg_kind,

@@ -101,12 +101,6 @@ SIGNATURES = {
                                   _i, _vp, _sz, ctypes.POINTER(ctypes.c_int), _vp]),
     "pg_gemm_splitk_reduce_batch": (_i, [ctypes.POINTER(PgSplitkJob), _i, _vp]),
     "pg_csr_spmm_f64": (_i, [_i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),
-    "pg_spmm_winner_words": (_i64, [_i64]),
-    "pg_spmm_max_fwd_masks": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i, _vp, _vp, _sz, _vp]),
-    "pg_spmm_max_fwd_masks_bf16": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i, _vp, _vp, _sz, _vp]),
-    "pg_spmm_max_bwd_masks_workspace": (_sz, [_csr, _i64]),
-    "pg_spmm_max_bwd_masks": (_i, [_csr, _csr, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _sz, _vp]),
-    "pg_spmm_max_bwd_masks_bf16": (_i, [_csr, _csr, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _sz, _vp]),
     "pg_spmm_max_bwd_scatter": (_i, [_csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "pg_spmm_sum_workspace": (_sz, [_csr, _i64]),
     "pg_spmm_sum": (_i, [_csr, _vp, _i64, _i64, _i, _vp, _vp, _i64, _vp, _sz, _vp]),

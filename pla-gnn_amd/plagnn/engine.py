@@ -157,12 +157,12 @@ class TrainEngine:
         N, pd, dev = self.N, self.pd, self.device
         # ---- activations ----
         f32 = dict(dtype=torch.float32, device=dev)
-        self.HM, self.Pl = [], []
+        self.HM, self.Pl, self.arg = [], [], []
         for l in range(self.L):
             Fi = pd[l]
             self.HM.append(torch.zeros(N, 2 * Fi, **f32))
             self.Pl.append(torch.zeros(N, Fi, **f32))
-        self._alloc_winner_masks()
+            self.arg.append(torch.zeros(N, Fi, dtype=self.dg.arg_dtype, device=dev))
         self.HM[0][:, :self.dims[0]] = features.to(dev, torch.float32)
         self.A3 = torch.zeros(N, pd[-3], **f32)
         self.A4 = torch.zeros(N, pd[-2], **f32)
@@ -175,36 +175,6 @@ class TrainEngine:
         self.dHM = [torch.zeros(N, 2 * pd[l], **f32) for l in range(self.L)]
         self.dP = [torch.zeros(N, pd[l], **f32) for l in range(self.L)]
 
-    def _alloc_winner_masks(self) -> None:
-        """Per SAGE layer: the max aggregation's winner masks (pg_spmm_max_fwd_masks), one
-        row of ceil(F / 32) uint32 words per in-CSR slot. They replace the argmax records:
-        the backward pulls, per out-edge, only the upstream gradients the edge won."""
-        L = _lib.lib()
-        E = max(self.dg.num_edges, 1)
-        self.wmask = [torch.zeros(E, int(L.pg_spmm_winner_words(self.pd[l])), dtype=torch.int32, device=self.device)
-                      for l in range(self.L)]
-
-    def winner_positions(self, layer: int) -> torch.Tensor:
-        """Diagnostics / tests: the argmax records (in-row positions, int32; -1 where the
-        maximum is 0 and nothing is recorded) of `layer`'s max aggregation, reconstructed
-        from its winner masks. N x F at the true width F."""
-        F = self.dims[layer]
-        N = self.N
-        out = torch.full((N, F), -1, dtype=torch.int32, device=self.device)
-        ptr = self.dg.fwd.ptr.to(torch.int64)
-        row_of = torch.repeat_interleave(torch.arange(N, device=self.device), ptr[1:] - ptr[:-1])
-        wm = self.wmask[layer]
-        shifts = torch.arange(32, device=self.device, dtype=torch.int32)
-        step = 1 << 16
-        for s0 in range(0, self.dg.num_edges, step):
-            bits = (wm[s0:s0 + step].unsqueeze(-1) >> shifts) & 1
-            bits = bits.reshape(bits.shape[0], -1)[:, :F]
-            s_idx, f_idx = bits.nonzero(as_tuple=True)
-            s_idx = s_idx + s0
-            v = row_of[s_idx]
-            out[v, f_idx] = (s_idx - ptr[v]).to(torch.int32)
-        return out
-
     def _alloc_workspace(self) -> None:
         # ---- workspace (one buffer, sized for the largest call) ----
         N, pd, C, dev = self.N, self.pd, self.C, self.device
@@ -213,7 +183,7 @@ class TrainEngine:
         for l in range(self.L):
             Fi = pd[l]
             need = max(need, L.pg_spmm_max_fwd_workspace(self.dg.fwd.struct(self.ews), Fi, self.dg.arg_kind))
-            need = max(need, L.pg_spmm_max_bwd_masks_workspace(self.dg.bwd.struct(None), Fi))
+            need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd.struct(None), Fi))
         self._gemm_plans = {}
         # weight gradients' split-K combines deferred to one batched launch per step
         self._slabs: Dict[str, torch.Tensor] = {}
@@ -377,8 +347,8 @@ class TrainEngine:
                        tag=f"gemm.fwd.pool.l{l + 1}")
             # M = max-aggregate(P) -> right half of HM
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
-                call("pg_spmm_max_fwd_masks", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0), None,
-                     Fi, self.dg.arg_kind, ptr(self.wmask[l]), ptr(self.ws), self.ws_bytes, st)
+                call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
+                     ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
             # Y = [H | M] Wcat^T + b (fc_self + fc_neigh + bias), leaky_relu -> next input
             Fo = pd[l + 1]
             out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
@@ -421,11 +391,11 @@ class TrainEngine:
                 self._gemm(dY, P[p + "Wcat"], dHM, tag=f"gemm.dgrad.cat.l{l + 1}")
             else:
                 self._gemm(dY, P[p + "Wcat"][:, Fi:], dHM[:, Fi:], tag=f"gemm.dgrad.cat.l{l + 1}")
-            # max backward from the winner masks; relu' of fc_pool is implied by them (P >= 0:
-            # a nonzero maximum has a winner with P > 0, a zero one records no winner)
+            # max backward with relu' of fc_pool fused; zero maxima (M = 0) are skipped
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                call("pg_spmm_max_bwd_masks", g, gt, ptr(self.wmask[l]), Fi, ptr(dHM[:, Fi:]), dHM.stride(0),
-                     None, 0, ptr(self.dP[l]), Fi, ptr(self.ws), self.ws_bytes, st)
+                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
+                     dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(self.dP[l]),
+                     Fi, ptr(self.ws), self.ws_bytes, st)
             # d Wpool = dP^T H, d bpool = sum_nodes dP
             self._gemm(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
                         tag=f"gemm.wgrad.pool.l{l + 1}")

@@ -38,11 +38,12 @@ class TrainEngineBF16(TrainEngine):
         N, pd, dev, L = self.N, self.pd, self.device, self.L
         bf = dict(dtype=torch.bfloat16, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
-        self.HM, self.Pl, self.DYP, self.dM = [], [], [], []
+        self.HM, self.Pl, self.arg, self.DYP, self.dM = [], [], [], [], []
         for l in range(L):
             Fi, Fo = pd[l], pd[l + 1]
             self.HM.append(torch.zeros(N, 2 * Fi, **bf))
             self.Pl.append(torch.zeros(N, Fi, **bf))
+            self.arg.append(torch.zeros(N, Fi, dtype=self.dg.arg_dtype, device=dev))
             self.DYP.append(torch.zeros(N, Fo + Fi, **bf))  # [dY_l | dP_l]
             self.dM.append(torch.zeros(N, Fi, **bf))
         self.HM[0][:, :self.dims[0]] = features.to(dev, torch.float32).to(torch.bfloat16)
@@ -53,7 +54,6 @@ class TrainEngineBF16(TrainEngine):
         self.dZ = torch.zeros(N, pd[-1], **f32)
         self.dZb = torch.zeros(N, pd[-1], **bf)
         self.dA4 = torch.zeros(N, pd[-2], **bf)
-        self._alloc_winner_masks()
         self._build_weight_copies()
 
     def _build_weight_copies(self) -> None:
@@ -106,7 +106,7 @@ class TrainEngineBF16(TrainEngine):
         for l in range(self.L):
             Fi = pd[l]
             need = max(need, L.pg_spmm_max_fwd_workspace(self.dg.fwd.struct(self.ews), Fi, self.dg.arg_kind))
-            need = max(need, L.pg_spmm_max_bwd_masks_workspace(self.dg.bwd.struct(None), Fi))
+            need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd.struct(None), Fi))
         self._gemm_plans = {}
         for (M_, N_, K_) in self._wgrad_shapes():
             sk = int(L.pg_gemm_bf16_split_k(M_, N_, K_))
@@ -144,8 +144,8 @@ class TrainEngineBF16(TrainEngine):
             self._gemm(HM[:, :Fi], W[p + "Wpool"], self.Pl[l], transb=True, bias=P[p + "bpool"], act=RELU,
                        tag=f"gemm.fwd.pool.l{l + 1}")
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
-                call("pg_spmm_max_fwd_masks_bf16", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0), None,
-                     Fi, self.dg.arg_kind, ptr(self.wmask[l]), ptr(self.ws), self.ws_bytes, st)
+                call("pg_spmm_max_fwd_bf16", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
+                     ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
             Fo = pd[l + 1]
             out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
             self._gemm(HM, W[p + "Wcat"], out, transb=True, bias=P[p + "b"], act=LEAKY,
@@ -175,8 +175,9 @@ class TrainEngineBF16(TrainEngine):
             # dM = dY Wneigh   (Wneigh = the right half of Wcat, read as a [Fo][Fi] k image)
             self._gemm(dY, W[p + "Wcat"][:, Fi:], self.dM[l], tag=f"gemm.dgrad.neigh.l{l + 1}")
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                call("pg_spmm_max_bwd_masks_bf16", g, gt, ptr(self.wmask[l]), Fi, ptr(self.dM[l]), Fi, None, 0,
-                     ptr(dP), DYP.stride(0), ptr(self.ws), self.ws_bytes, st)
+                call("pg_spmm_max_bwd_bf16", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.dM[l]),
+                     Fi, Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(dP), DYP.stride(0),
+                     ptr(self.ws), self.ws_bytes, st)
             self._gemm(dP, HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
                        tag=f"gemm.wgrad.pool.l{l + 1}")
             if l > 0:

@@ -108,50 +108,6 @@ def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
     return dx
 
 
-def spmm_max_masks(dg: DeviceGraph, X: torch.Tensor, ew_slots: Optional[torch.Tensor] = None,
-                   out: Optional[torch.Tensor] = None, wmask: Optional[torch.Tensor] = None,
-                   argpos: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """spmm_max that records winner masks instead of (or besides, with `argpos`) argmax
-    positions: wmask [nnz, ceil(F / 32)] int32, bit f of slot s set when the edge at in-CSR
-    slot s wins feature f with a nonzero maximum (pg_spmm_max_fwd_masks). GPU only."""
-    if X.dtype not in (torch.float32, torch.bfloat16) or not dg.is_cuda:
-        raise TypeError("spmm_max_masks: float32 or bfloat16 features on the GPU expected")
-    _check_device(dg, X, ew_slots)
-    n, F = dg.num_nodes, X.shape[1]
-    if out is None:
-        out = torch.empty(n, F, dtype=X.dtype, device=X.device)
-    if wmask is None:
-        wmask = torch.empty(max(dg.num_edges, 1), int(_lib.lib().pg_spmm_winner_words(F)), dtype=torch.int32,
-                            device=X.device)
-    g = dg.fwd.struct(ew_slots)
-    ws_n = _lib.lib().pg_spmm_max_fwd_workspace(g, F, dg.arg_kind)
-    ws = _workspace(ws_n, X.device)
-    call("pg_spmm_max_fwd_masks_bf16" if X.dtype == torch.bfloat16 else "pg_spmm_max_fwd_masks", g, ptr(X), _ld(X),
-         F, ptr(out), _ld(out), ptr(argpos), _ld(argpos) if argpos is not None else F, dg.arg_kind, ptr(wmask),
-         ptr(ws), ws_n, _stream(X))
-    return out, wmask
-
-
-def spmm_max_backward_masks(dg: DeviceGraph, wmask: torch.Tensor, dout: torch.Tensor,
-                            ew_slots: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
-                            dx: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dX from the winner masks of spmm_max_masks (pg_spmm_max_bwd_masks): ascending
-    destination order per feature; optional relu' mask (implied when the forward's input
-    is nonnegative)."""
-    _check_device(dg, dout, ew_slots, mask)
-    F = dout.shape[1]
-    if dx is None:
-        dx = torch.empty(dg.num_nodes, F, dtype=dout.dtype, device=dout.device)
-    g = dg.fwd.struct(ew_slots)
-    gt = dg.bwd.struct(None)
-    ws_n = _lib.lib().pg_spmm_max_bwd_masks_workspace(gt, F)
-    ws = _workspace(ws_n, dout.device)
-    call("pg_spmm_max_bwd_masks_bf16" if dout.dtype == torch.bfloat16 else "pg_spmm_max_bwd_masks", g, gt,
-         ptr(wmask), F, ptr(dout), _ld(dout), ptr(mask), _ld(mask) if mask is not None else 0, ptr(dx), _ld(dx),
-         ptr(ws), ws_n, _stream(dout))
-    return dx
-
-
 def spmm_max_backward_scatter(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
                               ew_slots: Optional[torch.Tensor] = None) -> torch.Tensor:
     """DGL-form backward with float atomics (non-deterministic summation order)."""

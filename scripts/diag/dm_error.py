@@ -83,10 +83,7 @@ for i in range(L):
 from plagnn import ops  # noqa: E402
 for l in range(L):
     F, Fi = eng.dims[l], eng.pd[l]
-    pe = eng.winner_positions(l).cpu().numpy()
-    fptr = eng.dg.fwd.ptr.cpu().numpy().astype(np.int64)
-    fcol = eng.dg.fwd.col.cpu().numpy()
-    ax_e = np.where(pe >= 0, fcol[np.minimum(fptr[:-1, None] + np.maximum(pe, 0), len(fcol) - 1)], ax_o)
+    ax_e = ops.argpos_to_src(eng.dg, eng.arg[l][:, :F].contiguous()).cpu().numpy()
     ax_o, ae_o, m_o = f32a[l]
     m_e = eng.HM[l][:, Fi:Fi + F].cpu().numpy()
     diff = ax_e != ax_o

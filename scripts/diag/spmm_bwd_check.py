@@ -33,9 +33,8 @@ outdeg = np.diff(g.bwd.ptr)
 for l in range(eng.L):
     F = eng.dims[l]
     Fi = eng.pd[l]
-    pos = eng.winner_positions(l).cpu().numpy()
-    argx = np.where(pos >= 0, g.fwd.col[np.minimum(ptr[:-1, None] + np.maximum(pos, 0), len(g.fwd.col) - 1)], 0)
-    pos = np.maximum(pos, 0)
+    pos = eng.arg[l][:, :F].to(torch.int32).cpu().numpy() & 0xFFFF
+    argx = ops.argpos_to_src(eng.dg, eng.arg[l][:, :F].contiguous()).cpu().numpy()
     slot = ptr[:-1, None] + pos
     arge = eid[np.minimum(slot, len(eid) - 1)]
     dM = eng.dHM[l][:, Fi:Fi + F].contiguous().cpu().numpy()

@@ -93,7 +93,11 @@ def _engine_signs(eng):
         s[f"conv{l + 1}.out"] = (out > 0).cpu()
     s["liner1"] = (eng.A4[:, :d[-2]] > 0).cpu()
     for l in range(L):
-        s[f"conv{l + 1}.argpos"] = eng.winner_positions(l).cpu().numpy()
+        pos = eng.arg[l][:, :d[l]].to(torch.int32)
+        if pos.dtype != eng.arg[l].dtype and eng.arg[l].dtype == torch.int16:
+            pos = pos & 0xFFFF
+            pos[pos == 0xFFFF] = -1
+        s[f"conv{l + 1}.argpos"] = pos.cpu().numpy()
     return s
 
 

@@ -408,52 +408,3 @@ def test_gemm_split_k_deferred_batch_reduce_is_bitwise():
     for (ref, rs_ref), (C, rs) in zip(refs, outs):
         assert torch.equal(C, ref)
         assert torch.equal(rs, rs_ref)
-
-
-@pytest.mark.parametrize("F,weighted,hub,chunk", [(64, False, 3000, 256), (256, True, 5000, 256),
-                                                  (300, False, 900, 64), (512, True, 2000, 256),
-                                                  (1000, False, 600, 128), (36, True, 400, 32)])
-def test_spmm_max_winner_masks(F, weighted, hub, chunk):
-    """The winner-mask pair (what TrainEngine runs) against the argmax-record path: the same
-    maxima bitwise; exactly one mask bit per nonzero maximum, at the recorded winner's slot,
-    none for zero maxima; dx bitwise equal to pg_spmm_max_bwd with fwd_out and the relu'
-    mask, with and without the (implied) mask. Hub rows split by the schedule (chunk
-    32 / 64 / 128 / 256), dead features, zero weights, F not a multiple of 32, bf16."""
-    from plagnn import ops
-
-    n = 700
-    src, dst = hub_graph(n, hub, seed=F)
-    g = _graph(src, dst, n, chunk=chunk)
-    dg = g.on(DEV)
-    gen = torch.Generator().manual_seed(F + 3)
-    P = torch.relu(torch.randn(n, F, generator=gen))
-    P[:, ::5] = 0.0  # dead features: every tie at position 0, all maxima 0
-    P = P.to(DEV)
-    ew = None
-    if weighted:
-        ew = dg.edge_weight_slots(torch.rand(g.num_edges, generator=gen))
-        ew[::7] = 0.0
-    out_r, arg = ops.spmm_max(dg, P, ew)
-    out_m, wm = ops.spmm_max_masks(dg, P, ew)
-    assert torch.equal(out_r, out_m)
-    # masks from the records: slot ptr[v] + argpos[v, f] holds bit f iff out[v, f] != 0
-    ptr = torch.from_numpy(g.fwd.ptr.astype(np.int64)).to(DEV)
-    pos = arg.to(torch.int64) & 0xFFFF if arg.dtype == torch.int16 else arg.to(torch.int64)
-    live = out_r != 0
-    v_idx, f_idx = live.nonzero(as_tuple=True)
-    slots = ptr[v_idx] + pos[v_idx, f_idx]
-    want = torch.zeros(g.num_edges, wm.shape[1] * 32, dtype=torch.bool, device=DEV)
-    want[slots, f_idx] = True
-    got = ((wm.unsqueeze(-1) >> torch.arange(32, device=DEV, dtype=torch.int32)) & 1).reshape(g.num_edges, -1) != 0
-    assert torch.equal(got, want)
-    dZ = torch.randn(n, F, generator=gen).to(DEV)
-    dx_r = ops.spmm_max_backward(dg, arg, dZ, ew, mask=P, fwd_out=out_r)
-    assert torch.equal(ops.spmm_max_backward_masks(dg, wm, dZ, ew, mask=P), dx_r)
-    assert torch.equal(ops.spmm_max_backward_masks(dg, wm, dZ, ew), dx_r)
-    # bf16 storage
-    Pb, dZb = P.to(torch.bfloat16), dZ.to(torch.bfloat16)
-    ob_r, argb = ops.spmm_max(dg, Pb, ew)
-    ob_m, wmb = ops.spmm_max_masks(dg, Pb, ew)
-    assert torch.equal(ob_r, ob_m)
-    assert torch.equal(ops.spmm_max_backward_masks(dg, wmb, dZb, ew),
-                       ops.spmm_max_backward(dg, argb, dZb, ew, mask=Pb, fwd_out=ob_r))
