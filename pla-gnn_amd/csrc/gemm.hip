@@ -55,6 +55,10 @@ constexpr int KPAD = BK + 4;  // [row][k] image row stride (floats)
 #ifndef PG_SPLIT_TARGET
 #define PG_SPLIT_TARGET 1024
 #endif
+#ifndef PG_SPLIT_TILE
+#define PG_SPLIT_TILE 64064  // BM * 1000 + BN of split-K products (weight gradients)
+#endif
+constexpr int kSplitBM = PG_SPLIT_TILE / 1000, kSplitBN = PG_SPLIT_TILE % 1000;
 #ifndef PG_GEMM_STAMP
 #define PG_GEMM_STAMP 0  // probe builds only: per-workgroup clock stamps (scripts/probes)
 #endif
@@ -688,7 +692,11 @@ inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& 
   }
   auto tiles = [&](int tm, int tn) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
   bm = bn = 64;
-  if (split > 1) return;
+  if (split > 1) {
+    bm = kSplitBM;
+    bn = kSplitBN;
+    return;
+  }
   if (N > 512) {
     bn = 128;
     bm = tiles(128, 128) >= 3 * 256 ? 128 : 64;
@@ -710,7 +718,7 @@ int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K) {
   // steps, at most 256 slices. Measured on the cfg2 step (whole step, batched combine):
   // 1024 workgroups 1.984 ms, 768 1.992, 1280 2.022, 640 / 896 2.06 / 2.03 (not a multiple
   // of the 256 CUs), 512 1.99, 384 2.15.
-  const int64_t tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  const int64_t tiles = ((M + kSplitBM - 1) / kSplitBM) * ((N + kSplitBN - 1) / kSplitBN);
   const int64_t target = (PG_SPLIT_TARGET + tiles - 1) / tiles;
   const int64_t by_k = K / (3 * BK);
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, by_k), 256));

@@ -41,11 +41,13 @@ RELU, LEAKY, NONE = _lib.PG_ACT_RELU, _lib.PG_ACT_LEAKY, _lib.PG_ACT_NONE
 
 
 class _Flat:
-    """Named views into one flat fp32 buffer (256-B aligned)."""
+    """Named views into one flat fp32 buffer (256-B aligned), plus named sub-views
+    (row ranges / column prefixes) of those blocks."""
 
     def __init__(self):
         self.layout: List = []  # (name, shape)
         self.offsets: Dict[str, int] = {}
+        self.subs: List = []  # (name, parent, row0, row1, ncols)
         self.size = 0
 
     def add(self, name, shape):
@@ -54,9 +56,16 @@ class _Flat:
         self.offsets[name] = self.size
         self.size += (n + 63) // 64 * 64
 
+    def sub(self, name, parent, row0, row1, ncols=None):
+        self.subs.append((name, parent, row0, row1, ncols))
+
     def views(self, buf: torch.Tensor) -> Dict[str, torch.Tensor]:
-        return {name: buf[self.offsets[name]:self.offsets[name] + int(np.prod(sh))].view(*sh)
-                for name, sh in self.layout}
+        v = {name: buf[self.offsets[name]:self.offsets[name] + int(np.prod(sh))].view(*sh)
+             for name, sh in self.layout}
+        for name, parent, r0, r1, nc in self.subs:
+            t = v[parent][r0:r1]
+            v[name] = t if nc is None else t[:, :nc]
+        return v
 
 
 class TrainEngine:
@@ -93,13 +102,20 @@ class TrainEngine:
         self.pd = pd
 
         # ---- parameters (flat, padded) ----
+        # per SAGE layer one block [Wcat ; Wpool | 0] of (Fo + Fi) x 2Fi: Wcat = [Wself | Wneigh]
+        # in rows [0, Fo), Wpool in rows [Fo, Fo + Fi) x columns [0, Fi) (the rest is a zero
+        # pad that stays zero), so that its left half [Wself ; Wpool] is the B operand of the
+        # stacked input gradient dH = ([dY | dP] [Wself ; Wpool]) * leaky'(H)
         fl = _Flat()
         for l in range(self.L):
             Fi, Fo = pd[l], pd[l + 1]
-            fl.add(f"conv{l + 1}.Wpool", (Fi, Fi))
-            fl.add(f"conv{l + 1}.bpool", (Fi,))
-            fl.add(f"conv{l + 1}.Wcat", (Fo, 2 * Fi))
-            fl.add(f"conv{l + 1}.b", (Fo,))
+            q = f"conv{l + 1}."
+            fl.add(q + "Wcp", (Fo + Fi, 2 * Fi))
+            fl.sub(q + "Wcat", q + "Wcp", 0, Fo)
+            fl.sub(q + "Wpool", q + "Wcp", Fo, Fo + Fi, Fi)
+            fl.sub(q + "Wstack", q + "Wcp", 0, Fo + Fi, Fi)
+            fl.add(q + "bpool", (Fi,))
+            fl.add(q + "b", (Fo,))
         fl.add("liner1.W", (pd[-2], pd[-3]))
         fl.add("liner1.b", (pd[-2],))
         fl.add("liner2.W", (pd[-1], pd[-2]))
@@ -168,12 +184,13 @@ class TrainEngine:
         self.A4 = torch.zeros(N, pd[-2], **f32)
         self.prob = torch.zeros(N, pd[-1], **f32)
         self.loss = torch.zeros(2, **f32)  # [train, val]
-        # backward buffers
+        # backward buffers: DYP_l = [dY_l | dP_l] (the gradients at layer l's pre-activation
+        # output and at P_l, side by side: the stacked input-gradient product's A operand),
+        # dM_l the gradient at the aggregated neighbourhood
         self.dZ = torch.zeros(N, pd[-1], **f32)
         self.dA4 = torch.zeros(N, pd[-2], **f32)
-        self.dA3 = torch.zeros(N, pd[-3], **f32)
-        self.dHM = [torch.zeros(N, 2 * pd[l], **f32) for l in range(self.L)]
-        self.dP = [torch.zeros(N, pd[l], **f32) for l in range(self.L)]
+        self.DYP = [torch.zeros(N, pd[l + 1] + pd[l], **f32) for l in range(self.L)]
+        self.dM = [torch.zeros(N, pd[l], **f32) for l in range(self.L)]
 
     def _alloc_workspace(self) -> None:
         # ---- workspace (one buffer, sized for the largest call) ----
@@ -378,33 +395,31 @@ class TrainEngine:
         self._gemm(self.dZ, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
         # liner1
         self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
-        self._gemm(self.dA4, P["liner1.W"], self.dA3, act=LEAKY, dact=self.A3, tag="gemm.dgrad.liner1")
-        dY = self.dA3
+        top = self.L - 1
+        self._gemm(self.dA4, P["liner1.W"], self.DYP[top][:, :pd[top + 1]], act=LEAKY, dact=self.A3,
+                   tag="gemm.dgrad.liner1")
         for l in reversed(range(self.L)):
             p = f"conv{l + 1}."
-            Fi = pd[l]
-            HM, dHM = self.HM[l], self.dHM[l]
+            Fi, Fo = pd[l], pd[l + 1]
+            HM, DYP = self.HM[l], self.DYP[l]
+            dY, dP = DYP[:, :Fo], DYP[:, Fo:]
             # d Wcat = dY^T [H | M], d b = sum_nodes dY
             self._gemm(dY, HM, G[p + "Wcat"], transa=True, rowsum=G[p + "b"], tag=f"gemm.wgrad.cat.l{l + 1}")
-            # d[H | M] = dY Wcat   (layer 1: only dM is needed)
-            if l > 0:
-                self._gemm(dY, P[p + "Wcat"], dHM, tag=f"gemm.dgrad.cat.l{l + 1}")
-            else:
-                self._gemm(dY, P[p + "Wcat"][:, Fi:], dHM[:, Fi:], tag=f"gemm.dgrad.cat.l{l + 1}")
+            # dM = dY Wneigh
+            self._gemm(dY, P[p + "Wcat"][:, Fi:], self.dM[l], tag=f"gemm.dgrad.neigh.l{l + 1}")
             # max backward with relu' of fc_pool fused; zero maxima (M = 0) are skipped
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(dHM[:, Fi:]),
-                     dHM.stride(0), Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(self.dP[l]),
-                     Fi, ptr(self.ws), self.ws_bytes, st)
+                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.dM[l]), Fi, Fi,
+                     ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(dP), DYP.stride(0), ptr(self.ws),
+                     self.ws_bytes, st)
             # d Wpool = dP^T H, d bpool = sum_nodes dP
-            self._gemm(self.dP[l], HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
-                        tag=f"gemm.wgrad.pool.l{l + 1}")
+            self._gemm(dP, HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
+                       tag=f"gemm.wgrad.pool.l{l + 1}")
             if l > 0:
-                # dH = (dH_self + dP Wpool) * leaky'(H): H is the previous layer's output
-                dH = dHM[:, :Fi]
-                self._gemm(self.dP[l], P[p + "Wpool"], dH, beta=1.0, act=LEAKY, dact=HM[:, :Fi],
-                           tag=f"gemm.dgrad.pool.l{l + 1}")
-                dY = dH
+                # dH = ([dY | dP] [Wself ; Wpool]) * leaky'(H), one K = Fo + Fi product: the
+                # lower layer's dY (H is the previous layer's output)
+                self._gemm(DYP, P[p + "Wstack"], self.DYP[l - 1][:, :Fi], act=LEAKY, dact=HM[:, :Fi],
+                           tag=f"gemm.dgrad.stack.l{l + 1}")
         self._reduce_deferred()
 
     def adam(self) -> None:

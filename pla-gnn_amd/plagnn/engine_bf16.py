@@ -67,14 +67,16 @@ class TrainEngineBF16(TrainEngine):
             wl.add(f"conv{l + 1}.Wstack", (Fo + Fi, Fi))  # [Wself ; Wpool]
         wl.add("liner1.W", (pd[-2], pd[-3]))
         idx = np.full(wl.size, -1, np.int64)
-        src = self.flat_layout.offsets
+        flat_ids = self.flat_layout.views(torch.arange(self.flat_layout.size))  # flat index of every entry
 
         def put(name, rows: np.ndarray):
             o = wl.offsets[name]
             idx[o:o + rows.size] = rows.ravel()
 
         def ids(name, shape):
-            return src[name] + np.arange(int(np.prod(shape))).reshape(shape)
+            t = flat_ids[name].numpy()
+            assert t.shape == tuple(shape), (name, t.shape, shape)
+            return t
 
         for l in range(L):
             Fi, Fo = pd[l], pd[l + 1]

@@ -81,6 +81,15 @@ class DeviceCsr:
         self.max_deg, self.chunk = h.max_deg, h.chunk
 
     def struct(self, ew: Optional[torch.Tensor] = None) -> PgCsr:
+        """The pg_csr_t view (cached per edge-weight pointer: it holds raw pointers only)."""
+        key = _lib.ptr(ew)
+        cache = self.__dict__.setdefault("_structs", {})
+        s = cache.get(key)
+        if s is None:
+            s = cache[key] = self._make_struct(ew)
+        return s
+
+    def _make_struct(self, ew: Optional[torch.Tensor]) -> PgCsr:
         s = PgCsr()
         s.n_rows, s.n_cols, s.nnz = self.n_rows, self.n_cols, self.nnz
         s.ptr = _lib.ptr(self.ptr)

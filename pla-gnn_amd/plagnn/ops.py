@@ -32,10 +32,22 @@ def _stream(t: torch.Tensor):
     return _lib.stream_handle(t.device)
 
 
+_scratch = {}
+
+
 def _workspace(nbytes: int, device) -> Optional[torch.Tensor]:
+    """Library scratch for one call: one buffer per (device, stream), grown on demand and
+    reused by every later call on that stream (stream order makes the reuse safe), so the
+    drop-in path's autograd functions allocate nothing per call."""
     if nbytes <= 0:
         return None
-    return torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+    device = torch.device(device)
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0)
+    buf = _scratch.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 1 << 20), dtype=torch.uint8, device=device)
+        _scratch[key] = buf
+    return buf
 
 
 def _check_device(dg: DeviceGraph, *ts):
