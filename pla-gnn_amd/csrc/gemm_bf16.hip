@@ -47,6 +47,14 @@ namespace {
 using namespace pg_gemm;
 
 constexpr int BK = 64;  // bf16 k-values per K step (two-stage kernels; deep ones use 32)
+#ifndef PG_BF16_WM  // wave grid of the 256 x 256 tile: 2 x 4 = eight waves, two per SIMD (measured
+                    // +9 ... +25 % over 2 x 2 on the cfg5 shapes: the second wave of a SIMD issues
+                    // its LDS reads and DMA while the first one runs MFMAs)
+#define PG_BF16_WM 2
+#endif
+#ifndef PG_BF16_WN
+#define PG_BF16_WN 4
+#endif
 #ifndef PG_BF16_DEEP
 #define PG_BF16_DEEP 0
 #endif
@@ -449,19 +457,13 @@ int launch_tile(bool ta, bool tb, bool obf, int epi, dim3 grid, hipStream_t st, 
 // 256 accumulators in AGPRs at one wave per SIMD; one 128-KiB workgroup per CU) wherever they still give >= 1 workgroup per CU, 128 x 128
 // (two per CU) next, 128 x 64 / 64 x 64 for narrow or small products. Split products
 // (weight gradients) use 256 x 256 when both sides allow it, else 64 x 64.
+#ifndef PG_BF16_TILE_FORCE
+#define PG_BF16_TILE_FORCE 0  // variant builds: BM * 1000 + BN forces one tile
+#endif
 inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& bn) {
-  static const int forced = [] {  // tuning knob PLAGNN_GEMM_BF16_TILE = "BMxBN"
-    const char* e = getenv("PLAGNN_GEMM_BF16_TILE");
-    if (!e) return 0;
-    int a = 0, b = 0;
-    if (sscanf(e, "%dx%d", &a, &b) != 2) return 0;
-    const int v = a * 1000 + b;
-    if (v != 64064 && v != 128064 && v != 64128 && v != 128128 && v != 256128 && v != 256256) return 0;
-    return v;
-  }();
-  if (forced) {
-    bm = forced / 1000;
-    bn = forced % 1000;
+  if constexpr (PG_BF16_TILE_FORCE != 0) {
+    bm = PG_BF16_TILE_FORCE / 1000;
+    bn = PG_BF16_TILE_FORCE % 1000;
     return;
   }
   auto tiles = [&](int tm, int tn) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
@@ -566,7 +568,7 @@ int pg_gemm_bf16(int transa, int transb, int64_t M, int64_t N, int64_t K, float 
                         : ep->dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
                                    : (act == PG_ACT_RELU ? EPI_RELU : act == PG_ACT_LEAKY ? EPI_LEAKY : EPI_NONE);
   int rc;
-  if (bm == 256 && bn == 256) rc = launch_tile<256, 256, 2, 2>(ta, tb, obf, epi, grid, st, a);
+  if (bm == 256 && bn == 256) rc = launch_tile<256, 256, PG_BF16_WM, PG_BF16_WN>(ta, tb, obf, epi, grid, st, a);
   else if (bm == 256) rc = launch_tile<256, 128, 2, 2>(ta, tb, obf, epi, grid, st, a);
   else if (bm == 128 && bn == 128) rc = launch_tile<128, 128, 2, 2>(ta, tb, obf, epi, grid, st, a);
   else if (bm == 128) rc = launch_tile<128, 64, 2, 2>(ta, tb, obf, epi, grid, st, a);

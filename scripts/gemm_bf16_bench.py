@@ -1,6 +1,6 @@
 """bf16 GEMM micro-benchmark (pg_gemm_bf16) on the cfg5 step shapes (N = 384,656 rows,
 hidden 512) and a square product, HIP-event timed, against torch.mm (hipBLASLt) on the
-same bf16 operands. Tile forced with PLAGNN_GEMM_BF16_TILE=BMxBN.
+same bf16 operands (A/B library variants with PLAGNN_LIB).
 Usage (GPU box): python scripts/gemm_bf16_bench.py [--rows 384656]"""
 import argparse
 import os
