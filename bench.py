@@ -44,7 +44,10 @@ PEAK_F32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
 # MI355X_MICROARCH.md: bf16 MFMA ~2.5 PF dense = 256 CUs x 4 SIMDs x (2*32*32*16 flops per
 # 32-cycle v_mfma_f32_32x32x16_bf16) x 2.4 GHz
 PEAK_BF16_TFLOPS = 2516.6
-ALPHA = 0.1               # main_normal.py -a default (code/main_normal.py:27)
+ALPHA = 0.1               # main_normal.py -a default (code/main_normal.py:29)
+# MI355X_MICROARCH.md "Indexed rows": rows gathered from an XCD's L2 16.8-18.8 TB/s chip-wide
+# (a uniformly random 38 MB table from the Infinity Cache: 8.6 TB/s)
+L2_GATHER_GBS = 17800.0
 
 
 def _group(name: str, gemm_group: str = "gemm_f32") -> str:
@@ -305,9 +308,15 @@ def main():
                     "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                     "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
         ach = g["work"] / sec / 1e9
-        return {"kernel": gname, "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
-                "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-                "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
+        r = {"kernel": gname, "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+             "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
+             "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
+        if gname == "spmm_max_fwd":
+            # the per-edge gathers of a feature matrix that fits the 256 MiB Infinity Cache are
+            # served by L2 / MALL, not HBM: also against the L2-served gather ceiling
+            r["ceiling_l2_gather_gbs"] = L2_GATHER_GBS
+            r["frac_vs_l2_gather"] = round(ach / L2_GATHER_GBS, 4)
+        return r
 
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")

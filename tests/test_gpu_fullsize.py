@@ -20,7 +20,7 @@ Bars (north_star "within 1e-4 fp32"):
   must then be within 1e-4 of the float64 result or no farther from it than 2x the float32
   oracle's own distance (a bias gradient summing cancelling terms can sit 2e-4 from exact
   in either float32 order);
-* post-Adam parameters (lr 5e-5, code/main_normal.py:22): Adam's first step moves every
+* post-Adam parameters (lr 5e-5, code/main_normal.py:26): Adam's first step moves every
   entry by about lr * sign(g), so an entry whose oracle gradient lies inside the gradient
   tolerance (|g| <= 1e-4 * max|g|) may legitimately move the other way. Those entries are
   checked against Adam applied to the engine's own gradient (the kernel's formula,
