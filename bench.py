@@ -170,7 +170,7 @@ def dropin_leg(wl, dims, dev, steps: int, warmup: int):
     ms = (time.perf_counter() - t0) / steps * 1e3
     L = len(dims) - 3
     return {"ms_per_step": round(ms, 4), "value": round(L * (len(wl.src)) / ms * 1e3, 1), "unit": "edges/s",
-            "loss": {"train": float(tl), "val": float(vl)},
+            "loss": {"train": float(tl.detach()), "val": float(vl.detach())},
             "what": "unmodified reference epoch body on the dgl shim: plagnn.model + multi_loss + autograd + "
                     "torch.optim.Adam (code/train.py:197-207)"}
 

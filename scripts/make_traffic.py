@@ -51,19 +51,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("config")
-    ap.add_argument("--launches", default="gemm_f32=22,spmm_max_fwd=3,spmm_max_bwd=3,head=1,adam=1")
+    ap.add_argument("--launches", default="", help="overrides of the per-step launch counts, e.g. gemm_f32=22")
     ap.add_argument("--gemm-group", default="gemm_f32", help="name of the GEMM group (gemm_bf16 for cfg5)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
-    launches = {k: float(v) for k, v in (kv.split("=") for kv in a.launches.split(","))}
+    launches = {"gemm_f32": 22.0, "spmm_max_fwd": 3.0, "spmm_max_bwd": 3.0, "head": 1.0, "adam": 1.0}
+    launches.update({k: float(v) for k, v in (kv.split("=") for kv in a.launches.split(",") if kv)})
     fetch, s1 = collect(a.root, "FETCH_SIZE")
     write, s2 = collect(a.root, "WRITE_SIZE")
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     cfg = {}
     for g in sorted(set(fetch) | set(write)):
         per_step = (2 * fetch.get(g, 0.0) / max(s1, 1) + write.get(g, 0.0) / max(s2, 1)) * 1024
-        cfg[g] = per_step / launches.get(g if g != "gemm_f32" else "gemm_f32", 1.0)
+        cfg[g] = per_step / launches.get(g, 1.0)
     if a.gemm_group != "gemm_f32" and "gemm_f32" in cfg:
         cfg[a.gemm_group] = cfg.pop("gemm_f32")
     out[a.config] = cfg

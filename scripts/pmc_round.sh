@@ -5,7 +5,7 @@ set -u
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-ARGS=${PMC_BENCH_ARGS:-"--steps 2 --warmup 2 --no-cpu-baseline --breakdown-reps 1"}
+ARGS=${PMC_BENCH_ARGS:-"--steps 2 --warmup 2 --no-cpu-baseline --no-legs --breakdown-reps 1"}
 run_pass() {
   name=$1; shift
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/pmc/$name -o run --pmc "$@" -- python3 $R/bench.py $ARGS > $R/gpurun_out/pmc/$name.out 2> $R/gpurun_out/pmc/$name.err
