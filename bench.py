@@ -44,6 +44,9 @@ PEAK_F32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA (= vector) dense peak
 # MI355X_MICROARCH.md: bf16 MFMA ~2.5 PF dense = 256 CUs x 4 SIMDs x (2*32*32*16 flops per
 # 32-cycle v_mfma_f32_32x32x16_bf16) x 2.4 GHz
 PEAK_BF16_TFLOPS = 2516.6
+# The aligned f32 GEMMs run as three-piece bf16 splits (gemm_x3.hip): 6 bf16 MFMA products per
+# f32 block, so their own ceiling is the bf16 peak / 6 in f32-equivalent flops
+X3_CEILING_TFLOPS = PEAK_BF16_TFLOPS / 6
 ALPHA = 0.1               # main_normal.py -a default (code/main_normal.py:29)
 # MI355X_MICROARCH.md "Indexed rows": rows gathered from an XCD's L2 16.8-18.8 TB/s chip-wide
 # (a uniformly random 38 MB table from the Infinity Cache: 8.6 TB/s)
@@ -304,9 +307,14 @@ def main():
             # algorithmic flops at the true (unpadded) dims, not the padded launch shapes
             ach = engine.flops_per_step() / sec / 1e12
             peak = PEAK_BF16_TFLOPS if bf16 else PEAK_F32_TFLOPS
-            return {"kernel": gname, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                    "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
+            r = {"kernel": gname, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                 "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                 "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
+            if not bf16:
+                r["algorithm"] = "f32 products as three-piece bf16 splits, 6 MFMA products, f32 accumulate"
+                r["ceiling_x3"] = round(X3_CEILING_TFLOPS, 1)
+                r["frac_vs_x3_ceiling"] = round(ach / X3_CEILING_TFLOPS, 4)
+            return r
         ach = g["work"] / sec / 1e9
         r = {"kernel": gname, "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
              "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),

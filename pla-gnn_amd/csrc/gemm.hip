@@ -59,6 +59,19 @@ constexpr int KPAD = BK + 4;  // [row][k] image row stride (floats)
 #define PG_SPLIT_TILE 64064  // BM * 1000 + BN of split-K products (weight gradients)
 #endif
 constexpr int kSplitBM = PG_SPLIT_TILE / 1000, kSplitBN = PG_SPLIT_TILE % 1000;
+//   PG_GEMM_ALGO       = 1: products whose operands allow 16-B loads run on the bf16 matrix
+//                        cores as three-piece splits (gemm_x3.hip), 0: f32 MFMA only;
+//   PG_X3_TILE_FORCE   = BM * 1000 + BN forces one tile of the three-piece kernel;
+//   PG_X3_SPLIT_TARGET = workgroups a split-K product of the three-piece kernel aims at.
+#ifndef PG_GEMM_ALGO
+#define PG_GEMM_ALGO 1
+#endif
+#ifndef PG_X3_TILE_FORCE
+#define PG_X3_TILE_FORCE 0
+#endif
+#ifndef PG_X3_SPLIT_TARGET
+#define PG_X3_SPLIT_TARGET 768
+#endif
 #ifndef PG_GEMM_STAMP
 #define PG_GEMM_STAMP 0  // probe builds only: per-workgroup clock stamps (scripts/probes)
 #endif
@@ -705,12 +718,54 @@ inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& 
   }
 }
 
+// Tile of the three-piece kernel: 128 x 128 (4 waves of 64 x 64: 0.5 fragment reads per
+// MFMA) wherever that still gives >= 2 workgroups per CU, else 128 x 64, else 64 x 64.
+inline void pick_tile_x3(int64_t M, int64_t N, int split, int& bm, int& bn) {
+  if constexpr (PG_X3_TILE_FORCE != 0) {  // variant builds only
+    bm = PG_X3_TILE_FORCE / 1000;
+    bn = PG_X3_TILE_FORCE % 1000;
+    return;
+  }
+  auto tiles = [&](int tm, int tn) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
+  if (split > 1) {
+    bm = M > 64 ? 128 : 64;
+    bn = N > 64 ? 128 : 64;
+    return;
+  }
+  bm = bn = 64;
+  if (tiles(128, 128) >= 512) bm = bn = 128;
+  else if (tiles(128, 64) >= 512) bm = 128;
+}
+
+// the three-piece kernel takes the product: 16-B loads along every contiguous extent, and
+// 16-B epilogue stores
+inline bool x3_ok(int transa, int transb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                  const float* B, int64_t ldb, const float* C, int64_t ldc, const pg_gemm_epilogue_t* ep,
+                  bool split, const void* ws) {
+  if constexpr (PG_GEMM_ALGO == 0) return false;
+  return al16(A) && lda % 4 == 0 && (transa ? M : K) % 4 == 0 && al16(B) && ldb % 4 == 0 &&
+         (transb ? K : N) % 4 == 0 && N % 4 == 0 &&
+         (split ? al16(ws) : (al16(C) && ldc % 4 == 0)) && (!ep->bias || al16(ep->bias)) &&
+         (!ep->dact || (al16(ep->dact) && ep->lddact % 4 == 0));
+}
+
 }  // namespace
 
 extern "C" {
 
 int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K < 1024) return 1;
+  if constexpr (PG_GEMM_ALGO != 0) {
+    // three-piece kernel (the engine's operands are aligned): ~3 128 x 128 workgroups per
+    // CU, each slice >= 8 K steps
+    int bm, bn;
+    pick_tile_x3(M, N, 1, bm, bn);
+    if (((M + bm - 1) / bm) * ((N + bn - 1) / bn) >= 512) return 1;
+    pick_tile_x3(M, N, 2, bm, bn);
+    const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+    const int64_t target = (PG_X3_SPLIT_TARGET + tiles - 1) / tiles;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, K / 128), 256));
+  }
   int bm, bn;
   pick_tile(M, N, K, 1, bm, bn);
   if (((M + bm - 1) / bm) * ((N + bn - 1) / bn) >= 768) return 1;
@@ -772,34 +827,43 @@ int gemm_f32_impl(int transa, int transb, int64_t M, int64_t N, int64_t K, float
   const bool split = split_k > 1;
   if (split_used) *split_used = split_k;
   if (defer && !split) return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32_partials: needs split_k > 1");
-  int bm, bn;
-  pick_tile(M, N, K, split_k, bm, bn);
-  const int tiles_n = (int)((N + bn - 1) / bn);
-  const int tiles = tiles_n * (int)((M + bm - 1) / bm);
-  dim3 grid((unsigned)tiles, 1, (unsigned)split_k);
   hipStream_t st = (hipStream_t)stream;
   float* wsf = split ? (float*)ws : nullptr;
-  // 16-B epilogue stores (finish_tile_lds) when every output-side operand allows them
-  const bool vec_out = (N % 4) == 0 &&
-                       (split ? al16(wsf) : (al16(C) && (ldc % 4) == 0)) &&
-                       (!ep->bias || al16(ep->bias)) &&
-                       (!ep->dact || (al16(ep->dact) && (ep->lddact % 4) == 0));
-  const Args a{(int)M, (int)N, (int)K, kps, tiles_n, tiles, alpha, A, lda, B, ldb, beta, C, ldc,
-               ep->bias, ep->slope, ep->dact, ep->lddact, ep->rowsum, wsf,
-               split ? wsf + (int64_t)split_k * M * N : nullptr, vec_out ? 1 : 0};
-  const bool ta = transa != 0, tb = transb != 0;
+  float* ws_rs = split ? wsf + (int64_t)split_k * M * N : nullptr;  // row-sum slices after the slabs
   const int epi = split ? EPI_SPLIT
                         : ep->dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
                                    : (act == PG_ACT_RELU ? EPI_RELU : act == PG_ACT_LEAKY ? EPI_LEAKY : EPI_NONE);
+  int bm, bn;
   int rc;
-  if (bm == 128 && bn == 128)
-    rc = launch_trans<128, 128>(ta, tb, va, vb, epi, grid, st, a);
-  else if (bm == 64 && bn == 128)
-    rc = launch_trans<64, 128>(ta, tb, va, vb, epi, grid, st, a);
-  else if (bm == 128)
-    rc = launch_trans<128, 64>(ta, tb, va, vb, epi, grid, st, a);
-  else
-    rc = launch_trans<64, 64>(ta, tb, va, vb, epi, grid, st, a);
+  if (x3_ok(transa, transb, M, N, K, A, lda, B, ldb, C, ldc, ep, split, ws)) {
+    pick_tile_x3(M, N, split_k, bm, bn);
+    const int tiles_n = (int)((N + bn - 1) / bn);
+    const int tiles = tiles_n * (int)((M + bm - 1) / bm);
+    const X3Args xa{transa != 0, transb != 0, bm, bn, epi, (int)M, (int)N, (int)K, kps, tiles_n, tiles,
+                    split_k, alpha, A, lda, B, ldb, beta, C, ldc, ep->bias, ep->slope, ep->dact,
+                    ep->lddact, ep->rowsum, wsf, ws_rs};
+    rc = gemm_x3_launch(xa, st);
+  } else {
+    pick_tile(M, N, K, split_k, bm, bn);
+    const int tiles_n = (int)((N + bn - 1) / bn);
+    const int tiles = tiles_n * (int)((M + bm - 1) / bm);
+    dim3 grid((unsigned)tiles, 1, (unsigned)split_k);
+    // 16-B epilogue stores (finish_tile_lds) when every output-side operand allows them
+    const bool vec_out = (N % 4) == 0 && (split ? al16(wsf) : (al16(C) && (ldc % 4) == 0)) &&
+                         (!ep->bias || al16(ep->bias)) &&
+                         (!ep->dact || (al16(ep->dact) && (ep->lddact % 4) == 0));
+    const Args a{(int)M, (int)N, (int)K, kps, tiles_n, tiles, alpha, A, lda, B, ldb, beta, C, ldc,
+                 ep->bias, ep->slope, ep->dact, ep->lddact, ep->rowsum, wsf, ws_rs, vec_out ? 1 : 0};
+    const bool ta = transa != 0, tb = transb != 0;
+    if (bm == 128 && bn == 128)
+      rc = launch_trans<128, 128>(ta, tb, va, vb, epi, grid, st, a);
+    else if (bm == 64 && bn == 128)
+      rc = launch_trans<64, 128>(ta, tb, va, vb, epi, grid, st, a);
+    else if (bm == 128)
+      rc = launch_trans<128, 64>(ta, tb, va, vb, epi, grid, st, a);
+    else
+      rc = launch_trans<64, 64>(ta, tb, va, vb, epi, grid, st, a);
+  }
   if (rc != PG_OK) return pg::set_error(rc, "pg_gemm_f32: dispatch failed");
   if (split && !defer) {
     const int64_t n = (N % 4 == 0 ? M * N / 4 : M * N) + (ep->rowsum ? M : 0);  // work units
@@ -809,7 +873,7 @@ int gemm_f32_impl(int transa, int transb, int64_t M, int64_t N, int64_t K, float
     const int blocks = (int)std::min<int64_t>(8192, (n + opb - 1) / opb);
 #define PG_R(G_)                                                                              \
   hipLaunchKernelGGL(splitk_reduce_kernel<G_>, dim3(blocks), dim3(256), 0, st, (const float*)wsf, \
-                     split_k, (int)M, (int)N, alpha, beta, C, ldc, (const float*)a.ws_rowsum,    \
+                     split_k, (int)M, (int)N, alpha, beta, C, ldc, (const float*)ws_rs,          \
                      ep->rowsum)
     if (G == 1) PG_R(1);
     else if (G == 4) PG_R(4);

@@ -125,6 +125,30 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   splitk_reduce_body<G>(ws, splits, M, N, alpha, beta, C, ldc, ws_rowsum, rowsum, blockIdx.x, gridDim.x);
 }
 
+// The three-piece bf16 GEMM (gemm_x3.hip): arguments and launcher (C = alpha op(A) op(B) +
+// beta C with the fused epilogue, or split-K partial slabs when epi == EPI_SPLIT).
+struct X3Args {
+  bool ta, tb;
+  int bm, bn, epi;
+  int M, N, K, kps, tiles_n, tiles, n_split;
+  float alpha;
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float beta;
+  float* C;
+  int64_t ldc;
+  const float* bias;
+  float slope;
+  const float* dact;
+  int64_t lddact;
+  float* rowsum;
+  float* ws;
+  float* ws_rowsum;
+};
+int gemm_x3_launch(const X3Args& a, hipStream_t st);
+
 // Threads per output of the split-K combine: enough slice groups that each thread sums
 // <= ~8 slices.
 inline int splitk_groups(int split_k) { return split_k <= 8 ? 1 : split_k <= 32 ? 4 : 16; }

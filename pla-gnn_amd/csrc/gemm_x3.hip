@@ -1,0 +1,449 @@
+// fp32 GEMM on the bf16 matrix cores: every f32 operand element is split into three bf16
+// pieces, a = a_h + a_m + a_l (each the round-to-nearest bf16 of what the previous pieces
+// leave), and C = sum over the six products A_h B_h + A_h B_m + A_m B_h + A_h B_l +
+// A_l B_h + A_m B_m of v_mfma_f32_32x32x16_bf16 (bf16 x bf16 products are exact in f32,
+// accumulation in f32). The three dropped products (A_m B_l, A_l B_m, A_l B_l) and the
+// split's remainder are below 2^-24 of |a b| each: per product the result is as accurate
+// as an f32 multiply; the sums run in f32 as in the exact kernel (gemm.hip), in another
+// order. Six bf16 MFMAs (6 x 32 cycles per 32x32x16 block) replace eight f32 MFMAs
+// (8 x 64 cycles): 2.67x the f32 MFMA peak is the ceiling (419 TF/s f32-equivalent).
+// Serves the same nn.Linear GEMMs as gemm.hip (code/model.py:13-17, forward and backward)
+// with the same epilogues and split-K partials; used where the operands allow 16-B loads.
+//
+// Tiling: BM x BN per 256-thread workgroup, 2 x 2 waves of (BM/2) x (BN/2) = TM x TN MFMA
+// tiles of 32 x 32, one MFMA k-step (16 k) per K step. K tiles go global -> registers
+// (float4 per thread and unit, issued one K step ahead), are split in registers and
+// stored as three bf16 images per operand (ds_write_b64 per piece) into the other half of
+// a double-buffered LDS array: one barrier per K step.
+// Images (u16 units), per piece:
+//   row image, operand stored k-contiguous (A[m][k], B stored [n][k]): [row][16 k], 32-B
+//     rows of two 8-k chunks; chunk c of row r at c ^ ((r >> 3) & 1), so the 16-lane groups
+//     of the ds_read_b128 fragment reads hit 16 distinct bank quads.
+//   k image, operand stored row-contiguous (A stored [k][m], B stored [k][n]): [16 k][ROWS],
+//     chunk c (8 rows) of k-row k at c ^ f(k) (gemm_bf16.hip's layout), read by
+//     ds_read_b64_tr_b16.
+// Requirements (the caller checks): 16-B aligned operands, leading dimensions and the
+// contiguous extents (K of a row image, M / N of a k image) multiples of 4.
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "gemm_common.hpp"
+
+namespace {
+
+using namespace pg_gemm;
+
+constexpr int KS = 16;  // k per K step
+constexpr int NT = 256;
+
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+using bf16x2 = __attribute__((ext_vector_type(2))) __bf16;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+using lds_bf16x4 = __attribute__((address_space(3))) bf16x4;
+
+template <int ROWS, bool KMAJ>
+__device__ __forceinline__ int img_off(int row, int k) {
+  if constexpr (!KMAJ) {
+    return row * KS + ((((k >> 3) ^ ((row >> 3) & 1))) << 3) + (k & 7);
+  } else {
+    const int f = ROWS == 64 ? ((k >> 1) & 1) * 4 : (k & 3) * 4;
+    return k * ROWS + ((((row >> 3) ^ f)) << 3) + (row & 7);
+  }
+}
+
+// the 8 k-values of MFMA row/col `rc` (tile-local) for lane half h = lane >> 5
+template <int ROWS, bool KMAJ>
+__device__ __forceinline__ bf16x8 frag(const uint16_t* __restrict__ S, int rc, int lane) {
+  if constexpr (!KMAJ) {
+    return *reinterpret_cast<const bf16x8*>(S + img_off<ROWS, false>(rc, 8 * (lane >> 5)));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int m = rc - (lane & 15) + 4 * p;
+    const int kb = 8 * (g >> 1);
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(S + img_off<ROWS, true>(m, kb + q)));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(S + img_off<ROWS, true>(m, kb + 4 + q)));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  const bf16x2 v = {static_cast<__bf16>(a), static_cast<__bf16>(b)};  // v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, v);
+}
+#ifndef PG_X3_PIPE
+#define PG_X3_PIPE 0  // 1: two register stages, the split interleaved with the MFMAs (measured slower on the step: 1.70 vs 1.65 ms)
+#endif
+#ifndef PG_X3_VALU_PER_MFMA
+#define PG_X3_VALU_PER_MFMA 4
+#endif
+#ifndef PG_X3_UNPACK
+#define PG_X3_UNPACK 1  // 1: low half widened by v_perm_b32 (the shift form gets rewritten into an extra cvt)
+#endif
+__device__ __forceinline__ float lo_f(uint32_t p) {
+  if constexpr (PG_X3_UNPACK) return __uint_as_float(__builtin_amdgcn_perm(0u, p, 0x01000c0cu));
+  else return __uint_as_float(p << 16);
+}
+__device__ __forceinline__ float hi_f(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
+
+// three-piece split of 4 floats: out[piece] = 4 bf16 (8 B)
+__device__ __forceinline__ void split4(const float4 v, uint2 (&out)[3]) {
+  float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int piece = 0; piece < 3; ++piece) {
+    const uint32_t p0 = pk_bf16(r[0], r[1]), p1 = pk_bf16(r[2], r[3]);
+    out[piece] = make_uint2(p0, p1);
+    if (piece < 2) {
+      r[0] = r[0] - lo_f(p0); r[1] = r[1] - hi_f(p0);
+      r[2] = r[2] - lo_f(p1); r[3] = r[3] - hi_f(p1);
+    }
+  }
+}
+
+// One operand's K tile: ROWS x KS, float4 units; row image unit = (row, 4 k), k image unit
+// = (k, 4 rows).
+template <int ROWS, bool KMAJ>
+struct Stage {
+  static constexpr int UNITS = ROWS * KS / 4;
+  static constexpr int PER = UNITS / NT;
+  static_assert(PER >= 1 && UNITS % NT == 0, "units per thread");
+  float4 v[PER];
+
+  __device__ __forceinline__ static void unit_pos(int q, int& row, int& k) {
+    if constexpr (!KMAJ) {
+      row = q >> 2;
+      k = (q & 3) << 2;
+    } else {
+      k = q / (ROWS / 4);
+      row = (q % (ROWS / 4)) << 2;
+    }
+  }
+  // rows past R read a clamped valid row (never stored); k past kz1 read as 0
+  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int r0, int R, int k0,
+                                       int kz1, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int row, k;
+      unit_pos(tid + i * NT, row, k);
+      const int gk = k0 + k;
+      if (gk < kz1) {
+        const float* p = !KMAJ ? P + (int64_t)min(r0 + row, R - 1) * ld + gk
+                               : P + (int64_t)gk * ld + min(r0 + row, R - 4);
+        v[i] = *reinterpret_cast<const float4*>(p);
+      } else {
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+  // a K tile wholly inside [k0, kz1): no per-unit guard (no branch)
+  __device__ __forceinline__ void load_full(const float* __restrict__ P, int64_t ld, int r0, int R, int k0,
+                                            int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int row, k;
+      unit_pos(tid + i * NT, row, k);
+      const float* p = !KMAJ ? P + (int64_t)min(r0 + row, R - 1) * ld + k0 + k
+                             : P + (int64_t)(k0 + k) * ld + min(r0 + row, R - 4);
+      v[i] = *reinterpret_cast<const float4*>(p);
+    }
+  }
+  __device__ __forceinline__ void load_any(const float* __restrict__ P, int64_t ld, int r0, int R, int k0,
+                                           int kz1, int tid) {
+    if (k0 + KS <= kz1) load_full(P, ld, r0, R, k0, tid);
+    else load(P, ld, r0, R, k0, kz1, tid);
+  }
+  // split and store the three pieces (images of IMG u16 each, consecutive)
+  template <int IMG>
+  __device__ __forceinline__ void store(uint16_t* __restrict__ S, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int row, k;
+      unit_pos(tid + i * NT, row, k);
+      uint2 pc[3];
+      split4(v[i], pc);
+      const int off = img_off<ROWS, KMAJ>(row, k);
+#pragma unroll
+      for (int piece = 0; piece < 3; ++piece) *reinterpret_cast<uint2*>(S + piece * IMG + off) = pc[piece];
+    }
+  }
+  // running row sums (float64) of an A tile: row image -> one row per unit, k image -> the
+  // same 4 rows for every unit of this thread
+  static constexpr int RSN = KMAJ ? 4 : PER;
+  __device__ __forceinline__ void rowsum(double (&rs)[RSN]) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if constexpr (!KMAJ) {
+        rs[i] += ((double)v[i].x + (double)v[i].y) + ((double)v[i].z + (double)v[i].w);
+      } else {
+        rs[0] += v[i].x; rs[1] += v[i].y; rs[2] += v[i].z; rs[3] += v[i].w;
+      }
+    }
+  }
+};
+
+template <int BM, int BN, bool TA, bool TB, int EPI>
+__global__ __launch_bounds__(NT) void gemm_x3_kernel(
+    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
+    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
+    const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
+    float* __restrict__ ws, float* __restrict__ ws_rowsum, int n_split) {
+  constexpr bool AK = TA, BKM = !TB;
+  constexpr bool SPLIT = EPI == EPI_SPLIT;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int IA = BM * KS, IB = BN * KS;  // one piece's image (u16)
+  constexpr int BUF = 3 * (IA + IB);         // one buffer: [A_h A_m A_l | B_h B_m B_l]
+  constexpr int STAGE_U16 = 2 * BUF;
+  constexpr int PASSES = 2 * BM * BN > STAGE_U16 ? 2 : 1;  // f32 epilogue image in row bands
+  constexpr int EPI_U16 = 2 * BM * BN / PASSES;
+  constexpr int LDS_U16 = STAGE_U16 > EPI_U16 ? STAGE_U16 : EPI_U16;
+  static_assert(LDS_U16 * 2 >= NT * 4 * 8, "row-sum scratch");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
+
+  // XCD-aware order over the (slice, tile) items (as gemm.hip's DMA kernel)
+  const int b = blockIdx.x;
+  const int items = tiles * n_split;
+  const int q8 = items / 8, r8 = items % 8, x8 = b % 8;
+  const int item = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int kz = item / tiles, tile = item % tiles;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kz0 = kz * k_per_split;
+  const int kz1 = min(K, kz0 + k_per_split);
+  const bool do_rs = rowsum != nullptr && tn == 0;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  Stage<BM, AK> sa;
+  Stage<BN, BKM> sb;
+  double rs[Stage<BM, AK>::RSN];
+#pragma unroll
+  for (int i = 0; i < Stage<BM, AK>::RSN; ++i) rs[i] = 0.0;
+
+  const int nk = kz1 > kz0 ? (kz1 - kz0 + KS - 1) / KS : 0;
+  const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
+  auto mfmas = [&](const uint16_t* As, const uint16_t* Bs) {
+    bf16x8 fa[3][TM], fb[3][TN];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[p][i] = frag<BM, AK>(As + p * IA, ra + i * 32, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[p][j] = frag<BN, BKM>(Bs + p * IB, rb + j * 32, lane);
+    }
+    // small terms first: (h,l) (l,h) (m,m) (h,m) (m,h) (h,h)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2][i], fb[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+      }
+  };
+  if constexpr (PG_X3_PIPE) {
+    // Registers double-buffered: in step t the tile t+1 (loaded during step t-1) is split
+    // and stored into the other LDS buffer between the MFMAs of tile t, and tile t+2 is
+    // loaded into the registers tile t occupied.
+    if (nk > 0) {
+      Stage<BM, AK> sa1;
+      Stage<BN, BKM> sb1;
+      sa.load_any(A, lda, m0, M, kz0, kz1, tid);
+      sb.load_any(B, ldb, n0, N, kz0, kz1, tid);
+      if (nk > 1) {
+        sa1.load_any(A, lda, m0, M, kz0 + KS, kz1, tid);
+        sb1.load_any(B, ldb, n0, N, kz0 + KS, kz1, tid);
+      }
+      if (do_rs) sa.rowsum(rs);
+      sa.template store<IA>(lds, tid);
+      sb.template store<IB>(lds + 3 * IA, tid);
+      __syncthreads();
+      auto step = [&](Stage<BM, AK>& san, Stage<BN, BKM>& sbn, Stage<BM, AK>& sac, Stage<BN, BKM>& sbc,
+                      int t) {
+        const int cur = t & 1;
+        if (t + 2 < nk) {
+          sac.load_any(A, lda, m0, M, kz0 + (t + 2) * KS, kz1, tid);
+          sbc.load_any(B, ldb, n0, N, kz0 + (t + 2) * KS, kz1, tid);
+        }
+        if (do_rs && t + 1 < nk) san.rowsum(rs);
+        const uint16_t* As = lds + cur * BUF;
+        mfmas(As, As + 3 * IA);
+        // (the last step's split writes stale registers into a buffer nobody reads again)
+        uint16_t* nx = lds + (cur ^ 1) * BUF;
+        san.template store<IA>(nx, tid);
+        sbn.template store<IB>(nx + 3 * IA, tid);
+        constexpr int NMF = PG_X3_VALU_PER_MFMA > 0 ? TM * TN * 6 : 0;
+#pragma unroll
+        for (int g = 0; g < NMF; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, PG_X3_VALU_PER_MFMA, 0);  // VALU
+          if (g % 2 == 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+        }
+        __syncthreads();
+      };
+      int t = 0;
+      for (; t + 1 < nk; t += 2) {
+        step(sa1, sb1, sa, sb, t);
+        step(sa, sb, sa1, sb1, t + 1);
+      }
+      if (t < nk) step(sa1, sb1, sa, sb, t);
+    }
+  } else if (nk > 0) {
+    sa.load(A, lda, m0, M, kz0, kz1, tid);
+    sb.load(B, ldb, n0, N, kz0, kz1, tid);
+    if (do_rs) sa.rowsum(rs);
+    sa.template store<IA>(lds, tid);
+    sb.template store<IB>(lds + 3 * IA, tid);
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const int cur = t & 1;
+      const bool more = t + 1 < nk;
+      if (more) {
+        sa.load(A, lda, m0, M, kz0 + (t + 1) * KS, kz1, tid);
+        sb.load(B, ldb, n0, N, kz0 + (t + 1) * KS, kz1, tid);
+      }
+      const uint16_t* As = lds + cur * BUF;
+      mfmas(As, As + 3 * IA);
+      if (more) {
+        if (do_rs) sa.rowsum(rs);
+        uint16_t* nx = lds + (cur ^ 1) * BUF;
+        sa.template store<IA>(nx, tid);
+        sb.template store<IB>(nx + 3 * IA, tid);
+      }
+      __syncthreads();  // the next buffer is complete; every wave is past its reads of this one
+    }
+  }
+
+  // row sums of op(A) (float64 partials per thread, combined in a fixed order)
+  if (do_rs) {
+    double* red = reinterpret_cast<double*>(lds);
+    if constexpr (!AK) {
+      // row image: unit i of thread tid is row (tid + i NT) / 4, k-quarter tid % 4
+#pragma unroll
+      for (int i = 0; i < Stage<BM, AK>::RSN; ++i) red[tid + i * NT] = rs[i];  // = 4 row + k-quarter
+      __syncthreads();
+      if (tid < BM && m0 + tid < M) {
+        const double t = (red[4 * tid] + red[4 * tid + 1]) + (red[4 * tid + 2] + red[4 * tid + 3]);
+        if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = (float)t;
+        else rowsum[m0 + tid] = (float)t;
+      }
+    } else {
+      // k image: thread tid holds rows 4 (tid % (BM / 4)) .. + 3 for the k-rows tid / (BM / 4)
+      constexpr int G = NT / (BM / 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[(tid / (BM / 4)) * BM + 4 * (tid % (BM / 4)) + e] = rs[e];
+      __syncthreads();
+      if (tid < BM && m0 + tid < M) {
+        double t = 0.0;
+        for (int g = 0; g < G; ++g) t += red[g * BM + tid];
+        if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = (float)t;
+        else rowsum[m0 + tid] = (float)t;
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue through LDS in PASSES row bands (16-B stores)
+  float* img = reinterpret_cast<float*>(lds);
+  constexpr int BAND = BM / PASSES;
+#pragma unroll
+  for (int pass = 0; pass < PASSES; ++pass) {
+    if (PASSES == 1 || wm == pass) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h - pass * BAND;
+            img[row * BN + wn * (BN / 2) + j * 32 + l32] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < BAND * BN / 4 / NT; ++it) {
+      const int u = it * NT + tid;
+      const int row = u / (BN / 4), c = (u % (BN / 4)) * 4;
+      const int gr = m0 + pass * BAND + row, gc = n0 + c;
+      if (gr >= M || gc >= N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(img + row * BN + c);
+      if constexpr (SPLIT) {
+        *reinterpret_cast<float4*>(ws + ((int64_t)kz * M + gr) * N + gc) = v;
+      } else {
+        float* cp = C + (int64_t)gr * ldc + gc;
+        float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
+        if (beta != 0.f) {
+          const float4 c4 = *reinterpret_cast<const float4*>(cp);
+          o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
+          o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
+        }
+        if (bias) {
+          const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
+          o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
+        }
+        float y[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
+          const float4 d4 = *reinterpret_cast<const float4*>(dact + (int64_t)gr * lddact + gc);
+          y[0] = d4.x; y[1] = d4.y; y[2] = d4.z; y[3] = d4.w;
+        }
+        *reinterpret_cast<float4*>(cp) =
+            make_float4(epi_apply<EPI>(o[0], y[0], slope), epi_apply<EPI>(o[1], y[1], slope),
+                        epi_apply<EPI>(o[2], y[2], slope), epi_apply<EPI>(o[3], y[3], slope));
+      }
+    }
+    if (PASSES > 1) __syncthreads();
+  }
+}
+
+template <int BM, int BN, bool TA, bool TB>
+int launch_epi(const X3Args& a, hipStream_t st) {
+  const dim3 grid((unsigned)(a.tiles * a.n_split)), block(NT);
+#define PG_L(EPI_)                                                                                   \
+  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, TA, TB, EPI_>), grid, block, 0, st, a.M, a.N, a.K, a.kps, \
+                     a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb, a.beta, a.C, a.ldc, a.bias,   \
+                     a.slope, a.dact, a.lddact, a.rowsum, a.ws, a.ws_rowsum, a.n_split)
+  switch (a.epi) {
+    case EPI_NONE: PG_L(EPI_NONE); break;
+    case EPI_RELU: PG_L(EPI_RELU); break;
+    case EPI_LEAKY: PG_L(EPI_LEAKY); break;
+    case EPI_DRELU: PG_L(EPI_DRELU); break;
+    case EPI_DLEAKY: PG_L(EPI_DLEAKY); break;
+    case EPI_SPLIT: PG_L(EPI_SPLIT); break;
+    default: return PG_ERR_INVALID;
+  }
+#undef PG_L
+  return PG_OK;
+}
+
+template <int BM, int BN>
+int launch_trans(const X3Args& a, hipStream_t st) {
+  if (!a.ta && !a.tb) return launch_epi<BM, BN, false, false>(a, st);
+  if (!a.ta && a.tb) return launch_epi<BM, BN, false, true>(a, st);
+  if (a.ta && !a.tb) return launch_epi<BM, BN, true, false>(a, st);
+  return launch_epi<BM, BN, true, true>(a, st);
+}
+
+}  // namespace
+
+namespace pg_gemm {
+
+int gemm_x3_launch(const X3Args& a, hipStream_t st) {
+  if (a.bm == 128 && a.bn == 128) return launch_trans<128, 128>(a, st);
+  if (a.bm == 128 && a.bn == 64) return launch_trans<128, 64>(a, st);
+  if (a.bm == 64 && a.bn == 128) return launch_trans<64, 128>(a, st);
+  if (a.bm == 64 && a.bn == 64) return launch_trans<64, 64>(a, st);
+  return PG_ERR_INVALID;
+}
+
+}  // namespace pg_gemm

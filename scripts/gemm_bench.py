@@ -45,11 +45,13 @@ def main():
     ap.add_argument("--dims", default="503,256,256,256,100,12")
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--square", type=int, default=4096, help="also time an NxNxN NN GEMM (0: skip)")
+    ap.add_argument("--err", action="store_true", help="also report the error against a float64 product")
     args = ap.parse_args()
     dims = [int(x) for x in args.dims.split(",")]
     extra = [("square", False, False, args.square, args.square, args.square)] if args.square else []
     tot_m = tot_t = 0.0
-    print(f"{'op':14} {'ta':>2} {'tb':>2} {'M':>6} {'N':>5} {'K':>6} {'mine_us':>8} {'TF':>6} {'torch_us':>8} {'TF':>6}")
+    print(f"{'op':14} {'ta':>2} {'tb':>2} {'M':>6} {'N':>5} {'K':>6} {'mine_us':>8} {'TF':>6} {'torch_us':>8} {'TF':>6}"
+          + ("  rel_fro   max/scale" if args.err else ""))
     seen = set()
     for name, ta, tb, M, N, K in shapes(dims) + extra:
         key = (ta, tb, M, N, K)
@@ -67,7 +69,14 @@ def main():
         if name != "square":
             tot_m += tm
             tot_t += tt
-        print(f"{name:14} {int(ta):>2} {int(tb):>2} {M:>6} {N:>5} {K:>6} {tm*1e3:8.1f} {fl/tm/1e9:6.1f} {tt*1e3:8.1f} {fl/tt/1e9:6.1f}")
+        err = ""
+        if args.err:
+            ops.gemm(A, B, transa=ta, transb=tb, out=C)
+            ref = torch.mm(a_.double(), b_.double())
+            scale = torch.mm(a_.double().abs(), b_.double().abs())  # sum |a b| per output
+            d = (C.double() - ref)
+            err = f"  {float(d.norm() / ref.norm()):.2e}  {float((d.abs() / scale).max()):.2e}"
+        print(f"{name:14} {int(ta):>2} {int(tb):>2} {M:>6} {N:>5} {K:>6} {tm*1e3:8.1f} {fl/tm/1e9:6.1f} {tt*1e3:8.1f} {fl/tt/1e9:6.1f}" + err)
     print(f"total (unique shapes): mine {tot_m*1e3:.1f} us, torch {tot_t*1e3:.1f} us")
 
 

@@ -191,6 +191,28 @@ def test_gemm_f32(ta, tb, shape):
     assert (C - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item()), (C - ref).abs().max()
 
 
+@pytest.mark.parametrize("ta,tb,M,N,K", [(False, True, 3000, 504, 504), (False, False, 3000, 512, 256),
+                                         (True, False, 256, 1008, 24041), (True, True, 136, 200, 1000)])
+def test_gemm_f32_is_f32_accurate(ta, tb, M, N, K):
+    """The f32 GEMM (three-piece bf16 products on the aligned path, gemm_x3.hip; the f32
+    MFMA chain elsewhere) has f32 accuracy: the error of every output, relative to the sum
+    of |a b| over its products, stays at the float32 level (measured 1.5e-8 .. 4.8e-7; a
+    two-piece split, 2^-17 per product, would be ~1e-6 .. 8e-6)."""
+    from plagnn import ops
+
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    a64 = A.double().t() if ta else A.double()
+    b64 = B.double().t() if tb else B.double()
+    ref = a64 @ b64
+    scale = a64.abs() @ b64.abs()
+    C = ops.gemm(A.to(DEV), B.to(DEV), transa=ta, transb=tb).cpu().double()
+    err = (C - ref).abs()
+    assert float((err / scale).max()) <= 1e-6
+    assert float(err.norm() / ref.norm()) <= 2e-6
+
+
 def test_gemm_epilogue_and_beta():
     from plagnn import _lib, ops
 
