@@ -70,7 +70,7 @@ constexpr int kSplitBM = PG_SPLIT_TILE / 1000, kSplitBN = PG_SPLIT_TILE % 1000;
 #define PG_X3_TILE_FORCE 0
 #endif
 #ifndef PG_X3_SPLIT_TARGET
-#define PG_X3_SPLIT_TARGET 768
+#define PG_X3_SPLIT_TARGET 512
 #endif
 #ifndef PG_GEMM_STAMP
 #define PG_GEMM_STAMP 0  // probe builds only: per-workgroup clock stamps (scripts/probes)
@@ -718,9 +718,12 @@ inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& 
   }
 }
 
-// Tile of the three-piece kernel: 128 x 128 (4 waves of 64 x 64: 0.5 fragment reads per
-// MFMA) wherever that still gives >= 2 workgroups per CU, else 128 x 64, else 64 x 64.
-inline void pick_tile_x3(int64_t M, int64_t N, int split, int& bm, int& bn) {
+// Tile of the three-piece kernel (measured per cfg2 shape with each tile forced, within 1-3 %
+// of the best everywhere): 128 x 128 (4 waves of 64 x 64: 0.5 fragment reads per MFMA)
+// wherever that gives >= 2 workgroups per CU, or >= 1 for K >= 1000; else 128 x 64, else
+// 64 x 64. Split products: 128 x 128, ~2 workgroups per CU (512: 1.636 ms/step, 768: 1.667,
+// 1024: 1.721).
+inline void pick_tile_x3(int64_t M, int64_t N, int64_t K, int split, int& bm, int& bn) {
   if constexpr (PG_X3_TILE_FORCE != 0) {  // variant builds only
     bm = PG_X3_TILE_FORCE / 1000;
     bn = PG_X3_TILE_FORCE % 1000;
@@ -733,7 +736,7 @@ inline void pick_tile_x3(int64_t M, int64_t N, int split, int& bm, int& bn) {
     return;
   }
   bm = bn = 64;
-  if (tiles(128, 128) >= 512) bm = bn = 128;
+  if (tiles(128, 128) >= 512 || (tiles(128, 128) >= 256 && K >= 1000)) bm = bn = 128;
   else if (tiles(128, 64) >= 512) bm = 128;
 }
 
@@ -756,12 +759,12 @@ extern "C" {
 int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K < 1024) return 1;
   if constexpr (PG_GEMM_ALGO != 0) {
-    // three-piece kernel (the engine's operands are aligned): ~3 128 x 128 workgroups per
+    // three-piece kernel (the engine's operands are aligned): ~2 128 x 128 workgroups per
     // CU, each slice >= 8 K steps
     int bm, bn;
-    pick_tile_x3(M, N, 1, bm, bn);
+    pick_tile_x3(M, N, K, 1, bm, bn);
     if (((M + bm - 1) / bm) * ((N + bn - 1) / bn) >= 512) return 1;
-    pick_tile_x3(M, N, 2, bm, bn);
+    pick_tile_x3(M, N, K, 2, bm, bn);
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
     const int64_t target = (PG_X3_SPLIT_TARGET + tiles - 1) / tiles;
     return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, K / 128), 256));
@@ -836,7 +839,7 @@ int gemm_f32_impl(int transa, int transb, int64_t M, int64_t N, int64_t K, float
   int bm, bn;
   int rc;
   if (x3_ok(transa, transb, M, N, K, A, lda, B, ldb, C, ldc, ep, split, ws)) {
-    pick_tile_x3(M, N, split_k, bm, bn);
+    pick_tile_x3(M, N, K, split_k, bm, bn);
     const int tiles_n = (int)((N + bn - 1) / bn);
     const int tiles = tiles_n * (int)((M + bm - 1) / bm);
     const X3Args xa{transa != 0, transb != 0, bm, bn, epi, (int)M, (int)N, (int)K, kps, tiles_n, tiles,

@@ -71,33 +71,13 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   const bf16x2 v = {static_cast<__bf16>(a), static_cast<__bf16>(b)};  // v_cvt_pk_bf16_f32 (RNE)
   return __builtin_bit_cast(uint32_t, v);
 }
-#ifndef PG_X3_PIPE
-#define PG_X3_PIPE 0  // 1: two register stages, the split interleaved with the MFMAs (measured slower on the step: 1.70 vs 1.65 ms)
-#endif
-#ifndef PG_X3_VALU_PER_MFMA
-#define PG_X3_VALU_PER_MFMA 4
-#endif
-#ifndef PG_X3_ABL
-#define PG_X3_ABL 0  // timing-only ablations (variant builds, wrong results): 1 no split, 2 no piece stores,
-                     // 3 one MFMA product per block, 4 no MFMA
-#endif
-#ifndef PG_X3_UNPACK
-#define PG_X3_UNPACK 1  // 1: low half widened by v_perm_b32 (the shift form gets rewritten into an extra cvt)
-#endif
-__device__ __forceinline__ float lo_f(uint32_t p) {
-  if constexpr (PG_X3_UNPACK) return __uint_as_float(__builtin_amdgcn_perm(0u, p, 0x01000c0cu));
-  else return __uint_as_float(p << 16);
-}
+// low bf16 of a packed pair widened to f32 by v_perm_b32 (the shift form gets rewritten into
+// an extra cvt)
+__device__ __forceinline__ float lo_f(uint32_t p) { return __uint_as_float(__builtin_amdgcn_perm(0u, p, 0x01000c0cu)); }
 __device__ __forceinline__ float hi_f(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
 
 // three-piece split of 4 floats: out[piece] = 4 bf16 (8 B)
 __device__ __forceinline__ void split4(const float4 v, uint2 (&out)[3]) {
-  if constexpr (PG_X3_ABL == 1) {
-    const uint2 u = make_uint2(__builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x07060302u),
-                               __builtin_amdgcn_perm(__float_as_uint(v.w), __float_as_uint(v.z), 0x07060302u));
-    out[0] = out[1] = out[2] = u;
-    return;
-  }
   float r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int piece = 0; piece < 3; ++piece) {
@@ -145,23 +125,6 @@ struct Stage {
       }
     }
   }
-  // a K tile wholly inside [k0, kz1): no per-unit guard (no branch)
-  __device__ __forceinline__ void load_full(const float* __restrict__ P, int64_t ld, int r0, int R, int k0,
-                                            int tid) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      int row, k;
-      unit_pos(tid + i * NT, row, k);
-      const float* p = !KMAJ ? P + (int64_t)min(r0 + row, R - 1) * ld + k0 + k
-                             : P + (int64_t)(k0 + k) * ld + min(r0 + row, R - 4);
-      v[i] = *reinterpret_cast<const float4*>(p);
-    }
-  }
-  __device__ __forceinline__ void load_any(const float* __restrict__ P, int64_t ld, int r0, int R, int k0,
-                                           int kz1, int tid) {
-    if (k0 + KS <= kz1) load_full(P, ld, r0, R, k0, tid);
-    else load(P, ld, r0, R, k0, kz1, tid);
-  }
   // split and store the three pieces (images of IMG u16 each, consecutive)
   template <int IMG>
   __device__ __forceinline__ void store(uint16_t* __restrict__ S, int tid) const {
@@ -172,12 +135,8 @@ struct Stage {
       uint2 pc[3];
       split4(v[i], pc);
       const int off = img_off<ROWS, KMAJ>(row, k);
-      if constexpr (PG_X3_ABL != 2) {
 #pragma unroll
-        for (int piece = 0; piece < 3; ++piece) *reinterpret_cast<uint2*>(S + piece * IMG + off) = pc[piece];
-      }
-      else if (pc[0].x == 0x12345678u && pc[1].y == 0x9abcdef0u && pc[2].x == 0x0fedcba9u)
-        *reinterpret_cast<uint2*>(S + off) = pc[0];  // keeps the split live
+      for (int piece = 0; piece < 3; ++piece) *reinterpret_cast<uint2*>(S + piece * IMG + off) = pc[piece];
     }
   }
   // running row sums (float64) of an A tile: row image -> one row per unit, k image -> the
@@ -273,17 +232,8 @@ __device__ unsigned long long pg_x3_stamp[64][66][4];
   } while (0)
 #endif
 
-#ifndef PG_X3_PHASED
-#define PG_X3_PHASED 0  // 1: fragments loaded in two phases (fewer live registers)
-#endif
-#ifndef PG_X3_WAVES
-#define PG_X3_WAVES 0  // > 0: amdgpu_waves_per_eu floor for the register-staged kernel
-#endif
 template <int BM, int BN, bool TA, bool TB, int EPI>
 __global__ __launch_bounds__(NT)
-#if PG_X3_WAVES > 0
-__attribute__((amdgpu_waves_per_eu(PG_X3_WAVES)))
-#endif
 void gemm_x3_kernel(
     int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
@@ -310,7 +260,7 @@ void gemm_x3_kernel(
   const int kz = item / tiles, tile = item % tiles;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1, l32 = lane & 31;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kz0 = kz * k_per_split;
   const int kz1 = min(K, kz0 + k_per_split);
@@ -333,40 +283,6 @@ void gemm_x3_kernel(
   const int nk = kz1 > kz0 ? (kz1 - kz0 + KS - 1) / KS : 0;
   const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
   auto mfmas = [&](const uint16_t* As, const uint16_t* Bs) {
-    if constexpr (PG_X3_PHASED) {
-      // h and m pieces first (hh, hm, mh, mm), then the l pieces into the m registers
-      // (hl, lh): 2 (TM + TN) fragments live instead of 3 (TM + TN)
-      bf16x8 ha[TM], hb[TN], xa[TM], xb[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) ha[i] = frag<BM, AK>(As, ra + i * 32, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) hb[j] = frag<BN, BKM>(Bs, rb + j * 32, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) xa[i] = frag<BM, AK>(As + IA, ra + i * 32, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) xb[j] = frag<BN, BKM>(Bs + IB, rb + j * 32, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[i], xb[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha[i], xb[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[i], hb[j], acc[i][j], 0, 0, 0);
-        }
-#pragma unroll
-      for (int i = 0; i < TM; ++i) xa[i] = frag<BM, AK>(As + 2 * IA, ra + i * 32, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) xb[j] = frag<BN, BKM>(Bs + 2 * IB, rb + j * 32, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha[i], xb[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[i], hb[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha[i], hb[j], acc[i][j], 0, 0, 0);
-        }
-      return;
-    }
     bf16x8 fa[3][TM], fb[3][TN];
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
@@ -380,12 +296,6 @@ void gemm_x3_kernel(
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        if constexpr (PG_X3_ABL == 4) continue;
-        if constexpr (PG_X3_ABL == 3) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i] + fa[2][i], fb[1][j] + fb[2][j], acc[i][j], 0, 0, 0);
-          continue;
-        }
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[2][j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2][i], fb[0][j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
@@ -394,54 +304,7 @@ void gemm_x3_kernel(
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
       }
   };
-  if constexpr (PG_X3_PIPE) {
-    // Registers double-buffered: in step t the tile t+1 (loaded during step t-1) is split
-    // and stored into the other LDS buffer between the MFMAs of tile t, and tile t+2 is
-    // loaded into the registers tile t occupied.
-    if (nk > 0) {
-      Stage<BM, AK> sa1;
-      Stage<BN, BKM> sb1;
-      sa.load_any(A, lda, m0, M, kz0, kz1, tid);
-      sb.load_any(B, ldb, n0, N, kz0, kz1, tid);
-      if (nk > 1) {
-        sa1.load_any(A, lda, m0, M, kz0 + KS, kz1, tid);
-        sb1.load_any(B, ldb, n0, N, kz0 + KS, kz1, tid);
-      }
-      if (do_rs) sa.rowsum(rs);
-      sa.template store<IA>(lds, tid);
-      sb.template store<IB>(lds + 3 * IA, tid);
-      __syncthreads();
-      auto step = [&](Stage<BM, AK>& san, Stage<BN, BKM>& sbn, Stage<BM, AK>& sac, Stage<BN, BKM>& sbc,
-                      int t) {
-        const int cur = t & 1;
-        if (t + 2 < nk) {
-          sac.load_any(A, lda, m0, M, kz0 + (t + 2) * KS, kz1, tid);
-          sbc.load_any(B, ldb, n0, N, kz0 + (t + 2) * KS, kz1, tid);
-        }
-        if (do_rs && t + 1 < nk) san.rowsum(rs);
-        const uint16_t* As = lds + cur * BUF;
-        mfmas(As, As + 3 * IA);
-        // (the last step's split writes stale registers into a buffer nobody reads again)
-        uint16_t* nx = lds + (cur ^ 1) * BUF;
-        san.template store<IA>(nx, tid);
-        sbn.template store<IB>(nx + 3 * IA, tid);
-        constexpr int NMF = PG_X3_VALU_PER_MFMA > 0 ? TM * TN * 6 : 0;
-#pragma unroll
-        for (int g = 0; g < NMF; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, PG_X3_VALU_PER_MFMA, 0);  // VALU
-          if (g % 2 == 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-        }
-        __syncthreads();
-      };
-      int t = 0;
-      for (; t + 1 < nk; t += 2) {
-        step(sa1, sb1, sa, sb, t);
-        step(sa, sb, sa1, sb1, t + 1);
-      }
-      if (t < nk) step(sa1, sb1, sa, sb, t);
-    }
-  } else if (nk > 0) {
+  if (nk > 0) {
     X3_STAMP(0, 0);
     sa.load(A, lda, m0, M, kz0, kz1, tid);
     sb.load(B, ldb, n0, N, kz0, kz1, tid);
@@ -508,230 +371,12 @@ void gemm_x3_kernel(
 }
 
 
-// ---------------------------------------------------------------------------------------
-// LDS-DMA form: the f32 K tiles go global -> LDS by global_load_lds_dwordx4 (no registers,
-// no VALU, NS stages in flight behind a counted s_waitcnt vmcnt and a raw s_barrier), and
-// every wave splits the f32 fragments it reads into the three bf16 pieces in registers.
-// f32 images (float units), XK k-values per K step:
-//   row image [row][XK]: 16-B chunk c of row r at c ^ s(r), s(r) = (r >> 2) & 3 (XK = 16,
-//     64-B rows) or (r >> 1) & 7 (XK = 32, 128-B rows): the 16-lane groups of the
-//     ds_read_b128 fragment reads (16 rows, one chunk) hit 16 distinct bank quads;
-//   k image [XK][ROWS]: chunk q (4 rows) of k-row k at q ^ (((k >> 3) & 1) * 8): the two
-//     lane halves (k and k + 8) of a ds_read_b32 fragment read land 32 banks apart.
-#ifndef PG_X3D_STAGES
-#define PG_X3D_STAGES 3
-#endif
-#ifndef PG_X3D_KS
-#define PG_X3D_KS 16
-#endif
-
-template <int ROWS, bool KMAJ, int XK>
-__device__ __forceinline__ int fimg_off(int row, int k) {
-  if constexpr (!KMAJ) {
-    constexpr int CPR = XK / 4;
-    const int sw = XK == 16 ? ((row >> 2) & 3) : ((row >> 1) & 7);
-    return row * XK + ((((k >> 2) & (CPR - 1)) ^ sw) << 2) + (k & 3);
-  } else {
-    return k * ROWS + ((((row >> 2) ^ (((k >> 3) & 1) * 8))) << 2) + (row & 3);
-  }
-}
-
-template <int ROWS, bool KMAJ, bool FULL, int XK>
-__device__ __forceinline__ void fdma_tile(const float* __restrict__ P, int64_t ld, int r0, int R, int k0,
-                                          int kvalid, float* S, int wave, int lane) {
-  constexpr int PIECES = ROWS * XK * 4 / 1024;
-  static_assert(PIECES % 4 == 0, "pieces per wave");
-#pragma unroll
-  for (int j = 0; j < PIECES / 4; ++j) {
-    const int piece = j * 4 + wave;
-    const int u = piece * 64 + lane;  // 16-B unit of the image
-    const float* src;
-    bool valid;
-    if constexpr (!KMAJ) {
-      constexpr int CPR = XK / 4;
-      const int row = u / CPR, cpos = u % CPR;
-      const int c = cpos ^ (XK == 16 ? ((row >> 2) & 3) : ((row >> 1) & 7));
-      valid = 4 * c < kvalid;
-      src = P + (int64_t)min(r0 + row, R - 1) * ld + k0 + 4 * c;
-    } else {
-      const int k = u / (ROWS / 4), qpos = u % (ROWS / 4);
-      const int q = qpos ^ (((k >> 3) & 1) * 8);
-      valid = k < kvalid;
-      src = P + (int64_t)(k0 + k) * ld + min(r0 + 4 * q, R - 4);
-    }
-    if (FULL || valid) __builtin_amdgcn_global_load_lds(src, S + piece * 256, 16, 0, 0);
-    else *reinterpret_cast<float4*>(S + u * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
-// the 8 f32 k-values (k = 16 s + 8 h + j) of MFMA row/col rc
-template <int ROWS, bool KMAJ, int XK>
-__device__ __forceinline__ void ffrag(const float* __restrict__ S, int rc, int s, int h, float (&f)[8]) {
-  const int kb = 16 * s + 8 * h;
-  if constexpr (!KMAJ) {
-    const float4 a = *reinterpret_cast<const float4*>(S + fimg_off<ROWS, false, XK>(rc, kb));
-    const float4 b = *reinterpret_cast<const float4*>(S + fimg_off<ROWS, false, XK>(rc, kb + 4));
-    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = S[fimg_off<ROWS, true, XK>(rc, kb + j)];
-  }
-}
-
-__device__ __forceinline__ void split8(const float (&f)[8], bf16x8 (&p)[3]) {
-  uint2 lo[3], hi[3];
-  split4(make_float4(f[0], f[1], f[2], f[3]), lo);
-  split4(make_float4(f[4], f[5], f[6], f[7]), hi);
-#pragma unroll
-  for (int q = 0; q < 3; ++q) p[q] = __builtin_bit_cast(bf16x8, make_uint4(lo[q].x, lo[q].y, hi[q].x, hi[q].y));
-}
-
-template <int N>
-__device__ __forceinline__ void x3_wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
-
-template <int BM, int BN, bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(NT) void gemm_x3d_kernel(
-    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
-    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
-    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
-    const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
-    float* __restrict__ ws, float* __restrict__ ws_rowsum, int n_split) {
-  constexpr bool AK = TA, BKM = !TB;
-  constexpr bool SPLIT = EPI == EPI_SPLIT;
-  constexpr int XK = PG_X3D_KS, NS = PG_X3D_STAGES, SS = XK / 16;
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int FA = BM * XK, FB = BN * XK;  // f32 images (floats)
-  constexpr int STAGEF = NS * (FA + FB);
-  constexpr int PASSES = BM * BN > STAGEF ? 2 : 1;
-  constexpr int EPIF = BM * BN / PASSES;
-  constexpr int LDSF = STAGEF > EPIF ? STAGEF : EPIF;
-  static_assert(LDSF >= 4 * BM, "row-sum scratch");
-  constexpr int D = (BM + BN) * XK * 4 / 1024 / 4;  // DMA instructions per tile and wave
-  __shared__ __attribute__((aligned(16))) float lds[LDSF];
-
-  const int b = blockIdx.x;
-  const int items = tiles * n_split;
-  const int q8 = items / 8, r8 = items % 8, x8 = b % 8;
-  const int item = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int kz = item / tiles, tile = item % tiles;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kz0 = kz * k_per_split;
-  const int kz1 = min(K, kz0 + k_per_split);
-  const bool do_rs = rowsum != nullptr && tn == 0;
-  const bool rs_wave = do_rs && wn == 0;  // the wn = 0 waves cover every row of the A tile once
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  double rs[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) rs[i] = 0.0;
-
-  const int nk = kz1 > kz0 ? (kz1 - kz0 + XK - 1) / XK : 0;
-  const bool tail = ((kz1 - kz0) % XK) != 0;
-  auto issue = [&](int t) {
-    const int k0 = kz0 + t * XK;
-    float* S = lds + (t % NS) * (FA + FB);
-    if (kz1 - k0 >= XK) {
-      fdma_tile<BM, AK, true, XK>(A, lda, m0, M, k0, XK, S, wave, lane);
-      fdma_tile<BN, BKM, true, XK>(B, ldb, n0, N, k0, XK, S + FA, wave, lane);
-    } else {
-      fdma_tile<BM, AK, false, XK>(A, lda, m0, M, k0, kz1 - k0, S, wave, lane);
-      fdma_tile<BN, BKM, false, XK>(B, ldb, n0, N, k0, kz1 - k0, S + FA, wave, lane);
-    }
-  };
-  const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
-  if (nk > 0) {
-    for (int p = 0; p < NS - 1 && p < nk; ++p) issue(p);
-    for (int t = 0; t < nk; ++t) {
-      // tile t landed (later tiles may stay in flight; the partial last tile issues fewer
-      // DMAs, so once it is in flight every wait is a full drain)
-      const int last = min(t + NS - 2, nk - 1);
-      const int after = last - t;
-      if (after <= 0 || (tail && last == nk - 1)) x3_wait_vmcnt<0>();
-      else if (after == 1) x3_wait_vmcnt<D>();
-      else x3_wait_vmcnt<2 * D>();
-      static_assert(NS <= 4, "vmcnt cases");
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's zero-fill stores
-      __builtin_amdgcn_s_barrier();
-      // every wave is past its reads of tile t - 1: its stage takes tile t + NS - 1
-      if (t + NS - 1 < nk) issue(t + NS - 1);
-      const float* As = lds + (t % NS) * (FA + FB);
-      const float* Bs = As + FA;
-#pragma unroll
-      for (int s = 0; s < SS; ++s) {
-        bf16x8 pa[TM][3], pb[TN][3];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          float f[8];
-          ffrag<BM, AK, XK>(As, ra + i * 32, s, h, f);
-          if (rs_wave) {
-            double t8 = 0.0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) t8 += (double)f[j];
-            rs[i] += t8;
-          }
-          split8(f, pa[i]);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float f[8];
-          ffrag<BN, BKM, XK>(Bs, rb + j * 32, s, h, f);
-          split8(f, pb[j]);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[i][0], pb[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[i][2], pb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[i][1], pb[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[i][0], pb[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[i][1], pb[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[i][0], pb[j][0], acc[i][j], 0, 0, 0);
-          }
-      }
-    }
-    x3_wait_vmcnt<0>();
-    __syncthreads();  // the epilogue reuses the staging array
-  }
-  if (do_rs) {
-    double* red = reinterpret_cast<double*>(lds);
-    if (wn == 0) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) red[(wm * (BM / 2) + i * 32 + l32) * 2 + h] = rs[i];
-    }
-    __syncthreads();
-    if (tid < BM && m0 + tid < M) {
-      const double t = red[2 * tid] + red[2 * tid + 1];
-      if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = (float)t;
-      else rowsum[m0 + tid] = (float)t;
-    }
-    __syncthreads();
-  }
-  x3_store<BM, BN, EPI, PASSES>(acc, lds, tid, m0, n0, M, N, kz, alpha, beta, C, ldc, bias, slope, dact, lddact, ws);
-}
-
-#ifndef PG_X3_DMA
-#define PG_X3_DMA 0  // 1: LDS-DMA staging with the split per wave after the fragment reads (measured slower: 916 vs 809 us on the cfg2 shapes)
-#endif
 
 template <int BM, int BN, bool TA, bool TB>
 int launch_epi(const X3Args& a, hipStream_t st) {
   const dim3 grid((unsigned)(a.tiles * a.n_split)), block(NT);
 #define PG_L(EPI_)                                                                                   \
-  hipLaunchKernelGGL((PG_X3_DMA ? gemm_x3d_kernel<BM, BN, TA, TB, EPI_> : gemm_x3_kernel<BM, BN, TA, TB, EPI_>), \
-                     grid, block, 0, st, a.M, a.N, a.K, a.kps, \
+  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, TA, TB, EPI_>), grid, block, 0, st, a.M, a.N, a.K, a.kps, \
                      a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb, a.beta, a.C, a.ldc, a.bias,   \
                      a.slope, a.dact, a.lddact, a.rowsum, a.ws, a.ws_rowsum, a.n_split)
   switch (a.epi) {
