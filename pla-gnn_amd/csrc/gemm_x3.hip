@@ -323,6 +323,10 @@ void gemm_x3_kernel(
       const uint16_t* As = lds + cur * BUF;
       mfmas(As, As + 3 * IA);
       X3_STAMP(t + 1, 1);
+#if PG_X3_STAMP
+      __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8));  // vmcnt(0): the next tile's loads
+      X3_STAMP(t + 1, 3);
+#endif
       if (more) {
         if (do_rs) sa.rowsum(rs);
         uint16_t* nx = lds + (cur ^ 1) * BUF;
@@ -331,7 +335,6 @@ void gemm_x3_kernel(
       }
       X3_STAMP(t + 1, 2);
       __syncthreads();  // the next buffer is complete; every wave is past its reads of this one
-      X3_STAMP(t + 1, 3);
     }
   }
 

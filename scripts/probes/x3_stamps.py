@@ -1,7 +1,7 @@
 """Per-step clock stamps of the register-staged three-piece GEMM (probe build:
 make variant V=stamp VSRC=gemm_x3 VFLAGS="-fno-slp-vectorize -DPG_X3_DMA=0 -DPG_X3_STAMP=1").
-Prints, for blocks 0..63 (wave 0), the median cycles of each step phase:
-load+frag+MFMA issue, split+store, barrier wait; and the prologue / epilogue.
+Prints, for blocks 0..63 (wave 0), the median cycles of each step phase: load+frag+MFMA
+issue, the wait for the next tile's global loads, split+store; and the prologue / epilogue.
 Usage: PLAGNN_LIB=.../libplagnn_stamp.so python scripts/probes/x3_stamps.py M N K ta tb"""
 import ctypes
 import os
@@ -30,15 +30,15 @@ nk = (K + 15) // 16
 st = buf.astype(np.int64)
 steps = st[:, 1:nk + 1, :]
 a = np.median(steps[:, :, 1] - steps[:, :, 0], axis=0)
-b = np.median(steps[:, :, 2] - steps[:, :, 1], axis=0)
-c = np.median(steps[:, :, 3] - steps[:, :, 2], axis=0)
-tot = np.median(steps[:, -1, 3] - st[:, 0, 0])
+c = np.median(steps[:, :, 3] - steps[:, :, 1], axis=0)  # wait for the loads
+b = np.median(steps[:, :, 2] - steps[:, :, 3], axis=0)  # split + store
+tot = np.median(steps[:, -1, 2] - st[:, 0, 0])
 print(f"shape {M}x{N}x{K} ta{ta} tb{tb}: steps {nk}, blocks 0..63 median total loop {tot} cycles")
 print(f"prologue (first tile) median {np.median(steps[:, 0, 0] - st[:, 0, 0]):.0f}")
-print("step: mfma-phase  split+store  barrier   (median over blocks; every 4th step)")
-for t in range(0, nk, 4):
+print("step: mfma-phase  split+store  load-wait   (median over blocks; every 4th step)")
+for t in range(0, min(nk, 64), 4):
     print(f"  {t:3d}: {a[t]:8.0f} {b[t]:8.0f} {c[t]:8.0f}")
-print(f"mean per step: mfma-phase {a.mean():.0f}, split+store {b.mean():.0f}, barrier {c.mean():.0f}")
+print(f"mean per step: mfma-phase {a.mean():.0f}, split+store {b.mean():.0f}, load-wait {c.mean():.0f}")
 print(f"epilogue median {np.median(st[:, 65, 1] - st[:, 65, 0]):.0f}")
 starts = st[:, 0, 0] - st[:, 0, 0].min()
 print(f"block start spread (cycles): {np.percentile(starts, [0, 50, 100])}")
