@@ -217,9 +217,6 @@ __device__ __forceinline__ void x3_store(const f32x16 (&acc)[BM / 64][BN / 64], 
 }
 
 
-#ifndef PG_X3_RING
-#define PG_X3_RING 0
-#endif
 #ifndef PG_X3_STAMP
 #define PG_X3_STAMP 0  // probe builds only: per-step shader-clock stamps of wave 0 of blocks 0..63
 #endif
@@ -248,7 +245,7 @@ void gemm_x3_kernel(
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int IA = BM * KS, IB = BN * KS;  // one piece's image (u16)
   constexpr int BUF = 3 * (IA + IB);         // one buffer: [A_h A_m A_l | B_h B_m B_l]
-  constexpr int STAGE_U16 = (PG_X3_RING ? 3 : 2) * BUF;
+  constexpr int STAGE_U16 = 2 * BUF;
   constexpr int PASSES = 2 * BM * BN > STAGE_U16 ? 2 : 1;  // f32 epilogue image in row bands
   constexpr int EPI_U16 = 2 * BM * BN / PASSES;
   constexpr int LDS_U16 = STAGE_U16 > EPI_U16 ? STAGE_U16 : EPI_U16;
@@ -307,76 +304,7 @@ void gemm_x3_kernel(
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
       }
   };
-  if (PG_X3_RING && nk > 0) {
-    // three piece buffers: in step t the fragments of tile t + 1 (stored in step t - 1) are
-    // read while the MFMAs of tile t run from registers, and tile t + 2 is split into the
-    // third buffer
-    using Frags = bf16x8[3][TM + TN];
-    auto read_frags = [&](int t, Frags& f) {
-      const uint16_t* As = lds + (t % 3) * BUF;
-      const uint16_t* Bs = As + 3 * IA;
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) f[p][i] = frag<BM, AK>(As + p * IA, ra + i * 32, lane);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) f[p][TM + j] = frag<BN, BKM>(Bs + p * IB, rb + j * 32, lane);
-      }
-    };
-    auto run = [&](const Frags& f) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0][i], f[2][TM + j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[2][i], f[0][TM + j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[1][i], f[1][TM + j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0][i], f[1][TM + j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[1][i], f[0][TM + j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0][i], f[0][TM + j], acc[i][j], 0, 0, 0);
-        }
-    };
-    auto stage = [&](int t) {  // load, split and store tile t into buffer t % 3
-      sa.load(A, lda, m0, M, kz0 + t * KS, kz1, tid);
-      sb.load(B, ldb, n0, N, kz0 + t * KS, kz1, tid);
-      if (do_rs) sa.rowsum(rs);
-      uint16_t* S = lds + (t % 3) * BUF;
-      sa.template store<IA>(S, tid);
-      sb.template store<IB>(S + 3 * IA, tid);
-    };
-    stage(0);
-    if (nk > 1) stage(1);
-    __syncthreads();
-    Frags f0, f1;
-    read_frags(0, f0);
-    if (nk > 2) {
-      sa.load(A, lda, m0, M, kz0 + 2 * KS, kz1, tid);
-      sb.load(B, ldb, n0, N, kz0 + 2 * KS, kz1, tid);
-    }
-    auto step = [&](int t, Frags& fc, Frags& fn) {
-      if (t + 1 < nk) read_frags(t + 1, fn);
-      run(fc);
-      if (t + 2 < nk) {
-        // tile t + 2 (loaded during the previous step) into buffer (t + 2) % 3, whose tile
-        // t - 1 every wave read before the last barrier; then the loads of tile t + 3
-        if (do_rs) sa.rowsum(rs);
-        uint16_t* S = lds + ((t + 2) % 3) * BUF;
-        sa.template store<IA>(S, tid);
-        sb.template store<IB>(S + 3 * IA, tid);
-        if (t + 3 < nk) {
-          sa.load(A, lda, m0, M, kz0 + (t + 3) * KS, kz1, tid);
-          sb.load(B, ldb, n0, N, kz0 + (t + 3) * KS, kz1, tid);
-        }
-      }
-      __syncthreads();
-    };
-    int t = 0;
-    for (; t + 1 < nk; t += 2) {
-      step(t, f0, f1);
-      step(t + 1, f1, f0);
-    }
-    if (t < nk) step(t, f0, f1);
-  } else if (nk > 0) {
+  if (nk > 0) {
     X3_STAMP(0, 0);
     sa.load(A, lda, m0, M, kz0, kz1, tid);
     sb.load(B, ldb, n0, N, kz0, kz1, tid);
