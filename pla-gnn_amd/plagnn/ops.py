@@ -180,7 +180,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
          bias: Optional[torch.Tensor] = None, act: int = _lib.PG_ACT_NONE,
          slope: float = LEAKY_SLOPE, split_k: Optional[int] = None,
          dact: Optional[torch.Tensor] = None, rowsum: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """C = alpha*op(A)@op(B) + beta*C (+bias, act) on the fp32 MFMA kernel (GPU) or
+    """C = alpha*op(A)@op(B) + beta*C (+bias, act): f32 GEMM on the GPU (three-piece bf16 MFMA
+    products where the operands are aligned, the f32 MFMA kernel otherwise; f32 accuracy) or
     torch-CPU (CPU device). With `dact` (an activation output) the result is instead
     multiplied by act'(dact): the fused activation backward. With `rowsum`, also
     rowsum[m] = sum_k op(A)[m][k] (bias gradients of a weight-gradient product)."""

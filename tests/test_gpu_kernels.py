@@ -430,3 +430,27 @@ def test_gemm_split_k_deferred_batch_reduce_is_bitwise():
     for (ref, rs_ref), (C, rs) in zip(refs, outs):
         assert torch.equal(C, ref)
         assert torch.equal(rs, rs_ref)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(1, 4, 4), (33, 12, 20), (129, 132, 100), (64, 4, 1000), (4, 260, 36)])
+def test_gemm_f32_edge_shapes_with_epilogue(ta, tb, M, N, K):
+    """Small and ragged shapes through pg_gemm_f32 (the three-piece path wherever the
+    operands are 16-B aligned with 4-multiple extents): partial K tiles, tiles past M / N,
+    beta = 1, bias and leaky_relu, against float64."""
+    from plagnn import _lib, ops
+
+    g = torch.Generator().manual_seed(M * 131 + N * 7 + K)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    bias = torch.randn(N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    Cd = C0.to(DEV)
+    ops.gemm(A.to(DEV), B.to(DEV), transa=ta, transb=tb, out=Cd, beta=1.0, bias=bias.to(DEV),
+             act=_lib.PG_ACT_LEAKY)
+    a64 = A.double().t() if ta else A.double()
+    b64 = B.double().t() if tb else B.double()
+    ref = torch.nn.functional.leaky_relu(a64 @ b64 + C0.double() + bias.double(), 0.01)
+    scale = (a64.abs() @ b64.abs()) + C0.double().abs() + bias.double().abs()
+    err = (Cd.cpu().double() - ref).abs()
+    assert float((err / scale).max()) <= 2e-6
