@@ -1,0 +1,13 @@
+#!/bin/bash
+# Rehearsal of bench.py's N-rank flow on a one-GPU box: torch.distributed.run with N ranks
+# sharing the GPU over gloo (the driver's 8-GPU runs use nccl = RCCL, one GPU per rank).
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+export PLAGNN_BENCH_BACKEND=gloo
+for cfg in ${CFGS:-cfg2}; do
+  n=${NR:-2}; [ "$cfg" = "cfg4" ] && n=4
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+    --master-port $((29500 + RANDOM % 500)) bench.py --gpus $n --steps 10 --warmup 3 --config $cfg \
+    > gpurun_out/rehearse_$cfg.json 2> gpurun_out/rehearse_$cfg.err
+  rc=$?; echo "$cfg n=$n rc=$rc"; cat gpurun_out/rehearse_$cfg.json; grep -v amdgpu.ids gpurun_out/rehearse_$cfg.err | tail -3
+  [ $rc -eq 0 ] || exit $rc
+done
