@@ -274,6 +274,20 @@ def main():
         dist.all_reduce(edges, op=dist.ReduceOp.SUM)
     t_max = t.item()
     value = edges.item() * args.steps / t_max
+    # per-step distribution (median of >= 50 steps), after the timed region:
+    # each step bracketed by HIP events on the stream the graphs replay on
+    n_med = max(50, args.steps)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_med)]
+    for ea, eb in evs:
+        ea.record()
+        engine.step()
+        eb.record()
+    torch.cuda.synchronize(dev)
+    per_step = np.array(sorted(ea.elapsed_time(eb) for ea, eb in evs))
+    step_dist = {"steps": n_med, "median_ms": round(float(np.median(per_step)), 4),
+                 "p10_ms": round(float(np.percentile(per_step, 10)), 4),
+                 "p90_ms": round(float(np.percentile(per_step, 90)), 4),
+                 "value_at_median": round(edges.item() / (float(np.median(per_step)) / 1e3), 1)}
     loss_tr, loss_va = engine.losses()
     if not (np.isfinite(loss_tr) and np.isfinite(loss_va)):
         raise SystemExit(f"non-finite loss after training: {loss_tr}, {loss_va}")
@@ -360,6 +374,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(t_max / args.steps * 1e3, 4),
+        "step_distribution": step_dist,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
