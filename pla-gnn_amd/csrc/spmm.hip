@@ -417,9 +417,6 @@ constexpr int kGroupMaxF = 1024;
 #ifndef PG_BWD_DIRECT
 #define PG_BWD_DIRECT 0
 #endif
-#ifndef PG_PULL_PIPE
-#define PG_PULL_PIPE 0
-#endif
 
 __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   const int per = (n + kBlock - 1) / kBlock;
@@ -844,47 +841,6 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     }
     const int excl = incl - nseg;
     const int nseg_all = bcast(incl, kWave - 1);
-#if PG_PULL_PIPE
-    // two batches in flight: batch k + 1's loads are issued before batch k's LDS adds, so
-    // the adds sit under the next loads' latency. A batch past the end loads a clamped valid
-    // segment with every lane off (no branch: the wait counts stay exact).
-    auto ld = [&](int s0, int (&fe)[U], float (&de)[U], int (&ie)[U], int (&ne)[U]) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int t = min(s0 + u, nseg_all - 1);
-        const int i = __popcll(__ballot(excl <= t)) - 1;
-        const int seg = t - bcast(excl, i);
-        const int base = bcast(gl.x, i) + seg * kWave;
-        const int n = s0 + u < nseg_all ? min(kWave, bcast(gl.y, i) - seg * kWave) : 0;
-        ie[u] = i;
-        ne[u] = n;
-        const bool on = lane < n;
-        fe[u] = on ? (int)gfeat[base + lane] : 0;
-        de[u] = on ? dpack[base + lane] : 0.f;
-      }
-    };
-    auto add = [&](const int (&fe)[U], const float (&de)[U], const int (&ie)[U], const int (&ne)[U]) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (lane < ne[u]) {
-          float w = 1.f;
-          if constexpr (HAS_W) w = bcastf(wv, ie[u]);
-          acc[fe[u]] += HAS_W ? w * de[u] : de[u];
-        }
-      }
-    };
-    if (nseg_all > 0) {
-      int fa[U], ia[U], na[U], fb[U], ib[U], nb[U];
-      float da[U], db[U];
-      ld(0, fa, da, ia, na);
-      for (int s0 = 0; s0 < nseg_all; s0 += 2 * U) {
-        ld(s0 + U, fb, db, ib, nb);
-        add(fa, da, ia, na);
-        ld(s0 + 2 * U, fa, da, ia, na);
-        add(fb, db, ib, nb);
-      }
-    }
-#else
     for (int s0 = 0; s0 < nseg_all; s0 += U) {
       const int nv = min(U, nseg_all - s0);
       int fe[U], ie[U], ne[U];
@@ -911,7 +867,6 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
         }
       }
     }
-#endif
   }
   wave_lds_sync();
   if (slot < 0) {
