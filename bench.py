@@ -9,11 +9,21 @@ synthetic PPI stand-in S0 (N = 24,041, power-law, mean degree 50, E' ~ 1.23 M), 
 layers of hidden 256 (503 -> 256 -> 256 -> 256, MLP 256 -> 100 -> 12), fp32. The other
 configs are plagnn.workload.CONFIGS (--config).
 
-Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): every rank holds a full-graph
-replica and starts from the same parameters; each step ends with ONE all-reduce (average)
-of the flat gradient bucket before Adam. Rank r trains the rows train_index[r::world] of
-the fold (cfg4: every rank its own perturbation graph, all train rows). Weak scaling:
-value = sum over ranks of edges / max-over-ranks time.
+Multi-GPU (torch.distributed.run, one rank per GPU), --mode:
+  replicas (default, Mode A): the reference's own parallelism — its 10 rounds x 10 folds
+    are independent trainings (code/train.py:162-178), so rank r trains job r (round
+    r // 10, fold r % 10) on its own full-graph replica with its own initial parameters,
+    with NO collective. Weak scaling: value = sum over ranks of edges / max-over-ranks time.
+  dp (Mode B; the default for cfg4, BASELINE configs[3]): one shared model; every rank
+    starts from rank 0's parameters and each step ends with ONE RCCL all-reduce (average)
+    of the flat gradient bucket before Adam. cfg4: rank r trains perturbation graph
+    r % 4 (different graphs: value = sum over ranks, weak scaling); other configs: rank r
+    trains the rows train_index[r::world] of the same graph, every rank repeating the same
+    full-graph forward/backward, so value = ONE model's edges / time (strong scaling).
+
+At N = 1 the line also carries `sub_configs`: ref (the reference dims), cfg3 (hidden
+512, edge-weighted) and cfg5 (RMAT x16, bf16), each timed the same way in a child process
+started before this process touches the GPU.
 
 Beside the engine's number (`value`), rank 0 at N = 1 also reports
   * `dropin`: the unmodified reference loop on the dgl shim (plagnn.model + torch Adam,
@@ -199,6 +209,224 @@ def epoch_with_eval_leg(engine, wl, dev, epochs: int = 20):
     return round((time.perf_counter() - t0) / epochs * 1e3, 4)
 
 
+def _roofline(engine, bd, gemm_group, bf16):
+    """Per-group time and the roofline of each group from a kernel breakdown (launches of
+    the replayed step graph, timed by event-record nodes: TrainEngine.kernel_breakdown)."""
+    groups = {}
+    for name, r in bd.items():
+        if name.startswith("_"):
+            continue
+        gname = _group(name, gemm_group)
+        g = groups.setdefault(gname, {"ms": 0.0, "work": 0.0, "launches": 0.0})
+        g["ms"] += r["ms"]
+        g["work"] += r["work"]
+        g["launches"] += r["calls"]
+
+    def roof(gname):
+        g = groups[gname]
+        sec = g["ms"] / 1e3
+        if gname == gemm_group:
+            # algorithmic flops at the true (unpadded) dims, not the padded launch shapes
+            ach = engine.flops_per_step() / sec / 1e12
+            r = {"kernel": gname, "bound": "mfma", "achieved": round(ach, 2), "unit": "TFLOP/s",
+                 "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4),
+                 "us_per_launch": round(g["ms"] * 1e3 / g["launches"], 2),
+                 "flops_per_step": engine.flops_per_step()}
+            if bf16:
+                r.update(peak=PEAK_BF16_TFLOPS, frac=round(ach / PEAK_BF16_TFLOPS, 4))
+            else:
+                # the pipe the kernel runs on: three-piece bf16 products (6 per f32 block)
+                r.update(peak=round(X3_CEILING_TFLOPS, 1), frac=round(ach / X3_CEILING_TFLOPS, 4),
+                         peak_is="bf16 MFMA peak / 6 (three-piece f32 split, gemm_x3.hip)",
+                         peak_f32_mfma=PEAK_F32_TFLOPS, frac_vs_f32_mfma=round(ach / PEAK_F32_TFLOPS, 4))
+            return r
+        ach = g["work"] / sec / 1e9
+        r = {"kernel": gname, "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+             "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
+             "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
+        if gname == "spmm_max_fwd":
+            # the per-edge gathers of a feature matrix that fits the 256 MiB Infinity Cache are
+            # served by L2 / MALL, not HBM: also against the L2-served gather ceiling
+            r["ceiling_l2_gather_gbs"] = L2_GATHER_GBS
+            r["frac_vs_l2_gather"] = round(ach / L2_GATHER_GBS, 4)
+        return r
+
+    return groups, roof
+
+
+def _traffic(config, group):
+    """HBM bytes per launch of `group` from the committed PMC pass (profiles/pmc_traffic.json,
+    scripts/pmc_round.sh), or None."""
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(tfile):
+        return None
+    with open(tfile) as f:
+        tj = json.load(f)
+    return tj.get(config, {}).get(group)
+
+
+def _job_of(rank, mode):
+    return rank if mode == "replicas" else 0
+
+
+def run(args, rank, world, dev, dist, mode):
+    """Build, capture and time one config; returns the result dict (rank 0) or None."""
+    import plagnn
+    from plagnn import workload as W
+
+    job = _job_of(rank, mode)
+    wl = W.build(args.config, rank=rank, device=dev, job=job)
+    if mode == "dp" and world > 1 and args.config != "cfg4":
+        wl.train_index = wl.train_index[rank::world]  # the fold's train rows sharded over ranks
+    graph = wl.graph()
+    dims, bf16 = wl.dims, wl.bf16
+    if wl.conv != "pool":
+        raise SystemExit(f"--config {args.config}: TrainEngine runs SAGEConv 'pool' layers; {wl.conv} runs on the "
+                         f"dgl shim (tests/test_gpu_graphconv.py)")
+    Engine = plagnn.TrainEngineBF16 if bf16 else plagnn.TrainEngine
+    gemm_group = "gemm_bf16" if bf16 else "gemm_f32"
+    engine = Engine(graph, torch.from_numpy(wl.ds.feat), torch.from_numpy(wl.ds.loc.astype(np.float32)),
+                    dims, wl.class_weight, wl.train_index, wl.val_index, lr=5e-5, device=dev,
+                    edge_weight=wl.edge_weight, seed=job)
+    allreduce = None
+    if dist is not None and mode == "dp":
+        from plagnn import dist as pdist
+
+        engine.broadcast_params()  # identical starting replicas
+        allreduce = pdist.allreduce_mean
+
+    if args.eager:  # PMC passes: every launch a plain dispatch (counters see graph replays poorly)
+        for _ in range(args.warmup):
+            engine.step_eager(allreduce)
+    else:
+        n_cap_warm = min(2, args.warmup)
+        engine.capture(warmup=n_cap_warm, allreduce=allreduce)
+        for _ in range(args.warmup - n_cap_warm):
+            engine.step()
+    step = (lambda: engine.step_eager(allreduce)) if args.eager else engine.step
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    edges = torch.tensor([float(engine.edges_per_step)], dtype=torch.float64, device=dev)
+    summed = world > 1 and (mode == "replicas" or args.config == "cfg4")
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if summed:
+            dist.all_reduce(edges, op=dist.ReduceOp.SUM)
+    t_max = t.item()
+    value = edges.item() * args.steps / t_max
+    # per-step distribution (SURVEY.md §8d: median of >= 50 steps), after the timed region:
+    # each step bracketed by HIP events on the stream the graphs replay on
+    n_med = max(50, args.steps)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_med)]
+    for ea, eb in evs:
+        ea.record()
+        step()
+        eb.record()
+    torch.cuda.synchronize(dev)
+    per_step = np.array(sorted(ea.elapsed_time(eb) for ea, eb in evs))
+    med = float(np.median(per_step))
+    step_dist = {"steps": n_med, "median_ms": round(med, 4),
+                 "p10_ms": round(float(np.percentile(per_step, 10)), 4),
+                 "p90_ms": round(float(np.percentile(per_step, 90)), 4),
+                 "value_at_median": round(edges.item() / (med / 1e3), 1)}
+    loss_tr, loss_va = engine.losses()
+    if not (np.isfinite(loss_tr) and np.isfinite(loss_va)):
+        raise SystemExit(f"non-finite loss after training: {loss_tr}, {loss_va}")
+    if dist is not None and mode == "dp":
+        # every rank must hold bitwise the same parameters after the timed steps: the
+        # element-wise MIN and MAX over ranks of the whole flat buffer (as int32 bits) agree
+        bits = engine.flat.view(torch.int32)
+        lo, hi = bits.clone(), bits.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        if not torch.equal(lo, hi):
+            raise SystemExit(f"replicas diverged at {int((lo != hi).sum())} of {bits.numel()} parameters")
+    if dist is not None:
+        dist.barrier()
+    if rank != 0:
+        return None
+
+    # per-kernel breakdown after the timed region, on rank 0 only (without the collective):
+    # the step captured with an event-record node around every launch, replayed
+    bd = engine.kernel_breakdown(args.breakdown_reps, graph=not args.eager)
+    method = bd.pop("_method")
+    if args.dump_breakdown:
+        with open(args.dump_breakdown, "w") as f:
+            json.dump(bd, f, indent=1)
+    groups, roof = _roofline(engine, bd, gemm_group, bf16)
+    dom = max(groups, key=lambda k: groups[k]["ms"])
+    rf = roof(dom)
+    rf["timing"] = {"graph": "launches of the replayed step graph, timed by event-record nodes around each launch",
+                    "eager+spin": "eager steps queued behind a GPU spin, events around each launch"}[method]
+    rf["traffic"] = _traffic(args.config, dom)
+    if world > 1:
+        par = (f"replicas{world}: independent (round, fold) trainings, no collective" if mode == "replicas" else
+               f"dp{world}: shared model, one gradient all-reduce per step, "
+               + ("a different perturbation graph per rank" if args.config == "cfg4" else "train rows sharded"))
+    else:
+        par = "single"
+    return {
+        "metric": "edges aggregated/sec per training epoch, full PPI graph",
+        "value": round(value, 1),
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t_max / args.steps * 1e3, 4),
+        "step_distribution": step_dist,
+        "higher_is_better": True,
+        "scaling": "strong" if (world > 1 and not summed) else "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if bf16 else "f32",
+        "data": "synthetic (seeded power-law PPI stand-in; real PPI/GEO/UniProt inputs are not shipped)",
+        "config": {"workload": f"{args.config}: {wl.desc}", "nodes": wl.n, "edges_with_self_loops": graph.num_edges,
+                   "graph_variant_rank0": wl.variant, "sage_layers": len(dims) - 3, "dims": dims,
+                   "edges_per_step": engine.edges_per_step, "mode": mode if world > 1 else "single",
+                   "parallelism": par},
+        "roofline": rf,
+        "spmm_roofline": {k: roof(k) for k in ("spmm_max_fwd", "spmm_max_bwd") if k in groups},
+        "kernels_ms_per_step": {k: round(v["ms"], 4) for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])},
+        "loss": {"train": loss_tr, "val": loss_va},
+        "_engine": engine,
+        "_wl": wl,
+    }
+
+
+def sub_configs(args):
+    """The other single-GPU configs, each in a child process of its own (started before this
+    process initialises the GPU), timed with the same steps / warm-up."""
+    import subprocess
+
+    out = {}
+    for name in [c for c in args.sub_configs.split(",") if c]:
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", name, "--steps", str(args.steps), "--warmup",
+               str(args.warmup), "--no-cpu-baseline", "--no-legs", "--sub-configs", "",
+               "--breakdown-reps", str(args.breakdown_reps)]
+        t0 = time.perf_counter()
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        if r.returncode != 0:
+            raise SystemExit(f"sub-config {name} failed (rc {r.returncode}):\n{r.stderr[-3000:]}")
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        res = json.loads(line)
+        keep = ("value", "unit", "ms_per_step", "step_distribution", "dtype", "config", "roofline", "spmm_roofline",
+                "kernels_ms_per_step", "loss")
+        out[name] = {k: res[k] for k in keep}
+        out[name]["child_wall_s"] = round(time.perf_counter() - t0, 1)
+        print(f"sub-config {name}: {res['ms_per_step']} ms/step", file=sys.stderr, flush=True)
+    return out
+
+
 def main():
     from plagnn import workload as W
 
@@ -207,6 +435,12 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2", choices=sorted(W.CONFIGS))
+    ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "dp"],
+                    help="N > 1: replicas = independent (round, fold) trainings, dp = shared model + all-reduce "
+                         "(auto: dp for cfg4, replicas otherwise)")
+    ap.add_argument("--sub-configs", default="ref,cfg3,cfg5",
+                    help="N = 1: other configs timed in child processes (comma list, '' for none)")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph (PMC counter passes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the drop-in and epoch-with-eval legs")
     ap.add_argument("--breakdown-reps", type=int, default=5)
@@ -218,6 +452,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    mode = args.mode if args.mode != "auto" else ("dp" if args.config == "cfg4" else "replicas")
+    subs = sub_configs(args) if (world == 1 and args.sub_configs) else None
     # one rank per GPU; more ranks than GPUs (a rehearsal of the N-rank flow on a smaller
     # box, with PLAGNN_BENCH_BACKEND=gloo) share them round-robin
     local_dev = local_rank % max(1, torch.cuda.device_count())
@@ -233,164 +469,25 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    import plagnn
-    from plagnn import dist as pdist
-
-    wl = W.build(args.config, rank=rank, device=dev)
-    if world > 1 and args.config != "cfg4":
-        wl.train_index = wl.train_index[rank::world]  # the fold's train rows sharded over ranks
-    graph = wl.graph()
-    dims, bf16 = wl.dims, wl.bf16
-    Engine = plagnn.TrainEngineBF16 if bf16 else plagnn.TrainEngine
-    gemm_group = "gemm_bf16" if bf16 else "gemm_f32"
-    engine = Engine(graph, torch.from_numpy(wl.ds.feat), torch.from_numpy(wl.ds.loc.astype(np.float32)),
-                    dims, wl.class_weight, wl.train_index, wl.val_index, lr=5e-5, device=dev,
-                    edge_weight=wl.edge_weight, seed=0)
-    allreduce = None
-    if dist is not None:
-        pdist.broadcast_([engine.flat])  # identical starting replicas (same seed as well)
-        allreduce = pdist.allreduce_mean
-
-    n_cap_warm = min(2, args.warmup)
-    engine.capture(warmup=n_cap_warm, allreduce=allreduce)
-    for _ in range(args.warmup - n_cap_warm):
-        engine.step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        engine.step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    edges = torch.tensor([float(engine.edges_per_step)], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(edges, op=dist.ReduceOp.SUM)
-    t_max = t.item()
-    value = edges.item() * args.steps / t_max
-    # per-step distribution (median of >= 50 steps), after the timed region:
-    # each step bracketed by HIP events on the stream the graphs replay on
-    n_med = max(50, args.steps)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_med)]
-    for ea, eb in evs:
-        ea.record()
-        engine.step()
-        eb.record()
-    torch.cuda.synchronize(dev)
-    per_step = np.array(sorted(ea.elapsed_time(eb) for ea, eb in evs))
-    step_dist = {"steps": n_med, "median_ms": round(float(np.median(per_step)), 4),
-                 "p10_ms": round(float(np.percentile(per_step, 10)), 4),
-                 "p90_ms": round(float(np.percentile(per_step, 90)), 4),
-                 "value_at_median": round(edges.item() / (float(np.median(per_step)) / 1e3), 1)}
-    loss_tr, loss_va = engine.losses()
-    if not (np.isfinite(loss_tr) and np.isfinite(loss_va)):
-        raise SystemExit(f"non-finite loss after training: {loss_tr}, {loss_va}")
-    if dist is not None:
-        # every rank must hold the same parameters after the timed steps
-        probe = engine.flat[:4096].double().sum().reshape(1)
-        lo, hi = probe.clone(), probe.clone()
-        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-        if lo.item() != hi.item():
-            raise SystemExit("replicas diverged")
-        dist.barrier()
-
-    if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+    out = run(args, rank, world, dev, dist, mode)
+    if out is None:
+        dist.destroy_process_group()
         return
-
-    # per-kernel HIP-event breakdown: eager diagnostic steps after the timed region, on rank 0
-    # only, so without the collective
-    bd = engine.kernel_breakdown(args.breakdown_reps)
-    if args.dump_breakdown:
-        with open(args.dump_breakdown, "w") as f:
-            json.dump(bd, f, indent=1)
-    groups = {}
-    for name, r in bd.items():
-        gname = _group(name, gemm_group)
-        g = groups.setdefault(gname, {"ms": 0.0, "work": 0.0, "launches": 0.0})
-        g["ms"] += r["ms"]
-        g["work"] += r["work"]
-        g["launches"] += r["calls"]
-    dom = max(groups, key=lambda k: groups[k]["ms"])
-
-    def roof(gname):
-        g = groups[gname]
-        sec = g["ms"] / 1e3
-        if gname == gemm_group:
-            # algorithmic flops at the true (unpadded) dims, not the padded launch shapes
-            ach = engine.flops_per_step() / sec / 1e12
-            peak = PEAK_BF16_TFLOPS if bf16 else PEAK_F32_TFLOPS
-            r = {"kernel": gname, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-                 "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                 "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
-            if not bf16:
-                r["algorithm"] = "f32 products as three-piece bf16 splits, 6 MFMA products, f32 accumulate"
-                r["ceiling_x3"] = round(X3_CEILING_TFLOPS, 1)
-                r["frac_vs_x3_ceiling"] = round(ach / X3_CEILING_TFLOPS, 4)
-            return r
-        ach = g["work"] / sec / 1e9
-        r = {"kernel": gname, "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
-             "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-             "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
-        if gname == "spmm_max_fwd":
-            # the per-edge gathers of a feature matrix that fits the 256 MiB Infinity Cache are
-            # served by L2 / MALL, not HBM: also against the L2-served gather ceiling
-            r["ceiling_l2_gather_gbs"] = L2_GATHER_GBS
-            r["frac_vs_l2_gather"] = round(ach / L2_GATHER_GBS, 4)
-        return r
-
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    rf = roof(dom)
-    if os.path.exists(tfile):
-        with open(tfile) as f:
-            tj = json.load(f)
-        traffic = tj.get(args.config, {}).get(dom)
-    rf["traffic"] = traffic
-
+    engine, wl = out.pop("_engine"), out.pop("_wl")
     legs = {}
     if world == 1 and not args.no_legs:
         legs["epoch_with_eval_ms"] = epoch_with_eval_leg(engine, wl, dev)
-        if not bf16:
-            legs["dropin"] = dropin_leg(wl, dims, dev, steps=min(args.steps, 20), warmup=3)
-
+        if not wl.bf16:
+            legs["dropin"] = dropin_leg(wl, wl.dims, dev, steps=min(args.steps, 20), warmup=3)
+    out.update(legs)
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not args.config.startswith("cfg5"):
-        cpu = cpu_baseline(wl, dims)
-
-    out = {
-        "metric": "edges aggregated/sec per training epoch, full PPI graph",
-        "value": round(value, 1),
-        "unit": "edges/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(t_max / args.steps * 1e3, 4),
-        "step_distribution": step_dist,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16" if bf16 else "f32",
-        "data": "synthetic (seeded power-law PPI stand-in; real PPI/GEO/UniProt inputs are not shipped)",
-        "config": {"workload": f"{args.config}: {wl.desc}", "nodes": wl.n, "edges_with_self_loops": graph.num_edges,
-                   "graph_variant_rank0": wl.variant, "sage_layers": len(dims) - 3, "dims": dims,
-                   "edges_per_step": engine.edges_per_step,
-                   "parallelism": f"replicas{world}+grad-allreduce" if world > 1 else "single"},
-        "roofline": rf,
-        "spmm_roofline": {k: roof(k) for k in ("spmm_max_fwd", "spmm_max_bwd") if k in groups},
-        "kernels_ms_per_step": {k: round(v["ms"], 4) for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])},
-        **legs,
-        "cpu_baseline": cpu,
-        "loss": {"train": loss_tr, "val": loss_va},
-    }
+        cpu = cpu_baseline(wl, wl.dims)
+    out["cpu_baseline"] = cpu
+    if subs is not None:
+        out["sub_configs"] = subs
+    loss = out.pop("loss")
+    out["loss"] = loss
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

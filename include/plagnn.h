@@ -33,7 +33,9 @@
  *                           (code/model.py:21-27), fused
  *   pg_col_sum           <- bias gradients (sum of dY over nodes)
  *   pg_gemm_f32          <- nn.Linear GEMMs (fc_pool / fc_self / fc_neigh / liner1-2),
- *                           fp32 MFMA (v_mfma_f32_32x32x2_f32), exact f32
+ *                           f32 in / f32 out with f32 accuracy: aligned operands run as
+ *                           three-piece bf16 splits on v_mfma_f32_32x32x16_bf16
+ *                           (gemm_x3.hip), the rest on v_mfma_f32_32x32x2_f32 (gemm.hip)
  *   pg_gemm_bf16,        <- the same layers and aggregation in the bf16-storage mode
  *   pg_spmm_max_*_bf16      (BASELINE configs[4]: bf16 storage, f32 accumulate); not run
  *   pg_cast_*               by the reference (fp32 only): reference-unpinned
@@ -258,7 +260,14 @@ typedef struct pg_gemm_epilogue {
 
 /* C[M,N] = alpha * op(A) * op(B) + beta * C, then the epilogue.
  * op(A) = A (M x K, lda) or A^T when transa (A stored K x M); op(B) = B (K x N) or B^T when
- * transb (B stored N x K). fp32 in, fp32 accumulate on MFMA (v_mfma_f32_32x32x2_f32).
+ * transb (B stored N x K). fp32 in, fp32 out, f32 accumulate on the matrix cores:
+ *   - 16-B aligned operands whose contiguous extents and leading dimensions are multiples
+ *     of 4: every element split into three bf16 pieces a = a_h + a_m + a_l, six piece
+ *     products (h.h, h.m, m.h, h.l, l.h, m.m) on v_mfma_f32_32x32x16_bf16. Error per
+ *     output <= ~1e-6 of sum_k |a b| (f32 level). Finite operands with |x| < 3.39e38
+ *     only: an Inf or NaN operand gives NaN in its outputs (where f32 arithmetic could
+ *     give +-Inf), and finite values that round to Inf in bf16 also give NaN.
+ *   - otherwise: v_mfma_f32_32x32x2_f32 (f32 products, IEEE non-finite behaviour).
  * When split_k > 1, beta must be 0 or 1 and the epilogue may only carry rowsum (partials
  * are combined in the workspace, in slice order: deterministic). */
 /* Recommended split_k for pg_gemm_f32 (long-K products such as weight gradients):

@@ -73,10 +73,10 @@ def lib():
         L.oracle_spmm_max_f64.restype = None
         _i32p = ctypes.POINTER(ctypes.c_int32)
         L.oracle_spmm_max_align.argtypes = [_i64p, _i64p, _i64p, _f32p, _f32p, ctypes.c_int64, ctypes.c_int64,
-                                            _i32p, ctypes.c_double, _f32p, _i64p, _i64p]
+                                            _i32p, _d, ctypes.c_double, _f32p, _i64p, _i64p, _i64p, _d]
         L.oracle_spmm_max_align.restype = ctypes.c_int64
         L.oracle_spmm_max_align_f64.argtypes = [_i64p, _i64p, _i64p, _d, _d, ctypes.c_int64, ctypes.c_int64, _i32p,
-                                                ctypes.c_double, _d, _i64p, _i64p]
+                                                _d, ctypes.c_double, _d, _i64p, _i64p, _i64p, _d]
         L.oracle_spmm_max_align_f64.restype = ctypes.c_int64
         L.oracle_spmm_max_bwd.argtypes = [_i64p, _i64p, _f32p, _f32p, _u8p, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.c_int64, _f32p]
@@ -187,36 +187,53 @@ def spmm_sum(g: OracleGraph, X: np.ndarray, mean: bool = False, use_weight: bool
     return out
 
 
-def spmm_max_align(g: OracleGraph, X: np.ndarray, use_weight: bool, hint: np.ndarray, tol: float,
-                   out, argx, arge) -> int:
+def spmm_max_align(g: OracleGraph, X: np.ndarray, use_weight: bool, hint: np.ndarray, scale: np.ndarray,
+                   band: float, out, argx, arge) -> Tuple[int, int]:
     """In place: entries where `hint` (another computation's winning in-row positions,
-    -1 = none) names a candidate within tol * max|out| of the maximum take it (see
-    oracle_spmm_max_align). Returns the number of changed entries."""
+    -1 = none) names a different candidate within `band` x the candidates' rounding scale
+    (`scale`: n x F float64 running-error magnitudes of X, times |w| for weighted edges)
+    of the maximum take it (oracle_spmm_max_align). Returns (changed, hard, max_gap): hard =
+    the entries whose hint lies outside the band (real disagreements), max_gap = the largest
+    gap / scale among the changed entries."""
     hint = np.ascontiguousarray(hint, np.int32)
+    S = np.ascontiguousarray(scale, np.float64)
     F = X.shape[1]
-    tol = float(tol) * float(np.abs(out).max(initial=0.0))
+    hard = ctypes.c_int64(0)
+    gap = ctypes.c_double(0.0)
+    d = ctypes.POINTER(ctypes.c_double)
+    i32 = ctypes.POINTER(ctypes.c_int32)
     if X.dtype == np.float64:
-        d = ctypes.POINTER(ctypes.c_double)
         w = g.ew.astype(np.float64) if use_weight else None
-        return int(lib().oracle_spmm_max_align_f64(
+        n = lib().oracle_spmm_max_align_f64(
             _p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p), _p(w, d), _p(X, d), g.n, F,
-            _p(hint, ctypes.POINTER(ctypes.c_int32)), tol, _p(out, d), _p(argx, _i64p), _p(arge, _i64p)))
-    w = g.ew if use_weight else None
-    return int(lib().oracle_spmm_max_align(
-        _p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p), _p(w, _f32p), _p(X, _f32p), g.n, F,
-        _p(hint, ctypes.POINTER(ctypes.c_int32)), tol, _p(out, _f32p), _p(argx, _i64p), _p(arge, _i64p)))
+            _p(hint, i32), _p(S, d), float(band), _p(out, d), _p(argx, _i64p), _p(arge, _i64p), ctypes.byref(hard),
+            ctypes.byref(gap))
+    else:
+        w = g.ew if use_weight else None
+        n = lib().oracle_spmm_max_align(
+            _p(g.indptr, _i64p), _p(g.indices, _i64p), _p(g.eids, _i64p), _p(w, _f32p), _p(X, _f32p), g.n, F,
+            _p(hint, i32), _p(S, d), float(band), _p(out, _f32p), _p(argx, _i64p), _p(arge, _i64p), ctypes.byref(hard),
+            ctypes.byref(gap))
+    return int(n), int(hard.value), float(gap.value)
 
 
 class _MaxAggregate(torch.autograd.Function):
-    """update_all(copy_u|u_mul_e, max) with DGL's GSpMM backward (scatter_add_ on argX)."""
+    """update_all(copy_u|u_mul_e, max) with DGL's GSpMM backward (scatter_add_ on argX).
+    `align` (optional dict: hint, scale, band, counts) aligns near-tie winners with another
+    computation (spmm_max_align) and receives the final argx / arge."""
 
     @staticmethod
     def forward(ctx, P, g, use_weight, parallel=False, align=None):
         Xn = np.ascontiguousarray(P.detach().numpy())
         out, argx, arge = spmm_max(g, Xn, use_weight, parallel)
-        if align is not None:  # (hint positions, tol, signs dict for the count)
-            hint, tol, counts = align
-            counts["_ties"] = counts.get("_ties", 0) + spmm_max_align(g, Xn, use_weight, hint, tol, out, argx, arge)
+        if align is not None:
+            n, hard, gap = spmm_max_align(g, Xn, use_weight, align["hint"], align["scale"], align["band"], out,
+                                          argx, arge)
+            c = align["counts"]
+            c["_ties"] = c.get("_ties", 0) + n
+            c["_hard_ties"] = c.get("_hard_ties", 0) + hard
+            c["_max_tie_ulps"] = max(c.get("_max_tie_ulps", 0.0), gap / U32)
+            align["argx"], align["arge"] = argx, arge
         ctx.g, ctx.argx, ctx.arge, ctx.use_weight, ctx.parallel = g, argx, arge, use_weight, parallel
         return torch.from_numpy(out)
 
@@ -238,70 +255,240 @@ def leaky_relu(x):
     return torch.nn.functional.leaky_relu(x)  # negative_slope 0.01 (model.py:21,23,25,27)
 
 
-# Winner alignment band (spmm_max_align): a fraction of the aggregation's largest |value|.
-# Float32 GEMM rounding moves P by ~1e-7 of that scale; near-ties seen differing between the
-# engine and this oracle sat within 4e-8 of it.
-WINNER_TOL = 1e-6
+# Decision alignment (parity tests at full size). Two float32 computations of the same
+# algorithm round differently, so a relu / leaky_relu decision at a pre-activation near 0,
+# or the winner among two nearly equal maximum candidates, can differ between them. Such a
+# decision is taken from the other computation (`signs`) when it lies within BAND_ULPS
+# units of 2^-24 x its running-error scale: the float64 sum of |terms| the value was
+# formed from, propagated through the layers (|x| -> |h| |W|^T + |b| -> the winner's scale
+# -> ...), i.e. a few ulp of the magnitudes that formed THAT value, not of the layer's
+# largest value. Entries outside the band where the decisions differ count as "hard".
+BAND_ULPS = 16.0
+U32 = 2.0 ** -24
 
 
-def _act(pre, slope, site, signs, sign_tol):
+def _act(pre, slope, site, signs, scale=None, band_ulps: float = BAND_ULPS):
     """relu (slope 0) / leaky_relu of `pre`. With `signs` (site -> the other computation's
-    "output > 0" mask), entries whose pre-activation lies within sign_tol * max|pre| of zero
-    take that decision instead of their own: there the derivative (1 or slope) is decided by
-    float32 rounding, not by the algorithm. signs["_flips"] counts the entries whose decision
-    changed."""
+    "output > 0" mask) and `scale` (running-error scale of pre, float64), entries with
+    |pre| <= band_ulps * 2^-24 * scale take that decision instead of their own.
+    signs["_flips"] counts the changed decisions, signs["_hard_flips"] the differing ones
+    outside the band, signs["_max_flip_ulps"] the largest |pre| / (2^-24 scale) among the
+    changed ones."""
     if signs is None or site not in signs:
         return torch.relu(pre) if slope == 0.0 else torch.nn.functional.leaky_relu(pre, slope)
     with torch.no_grad():
         own = pre > 0
-        tiny = pre.abs() <= sign_tol * pre.abs().max()
-        pos = torch.where(tiny, signs[site].to(own.device), own)
-        signs["_flips"] = signs.get("_flips", 0) + int((pos != own).sum())
+        eng = signs[site].to(own.device)
+        ulps = pre.detach().abs().double() / (U32 * scale.clamp(min=1e-300))
+        tiny = ulps <= band_ulps
+        pos = torch.where(tiny, eng, own)
+        changed = pos != own
+        signs["_flips"] = signs.get("_flips", 0) + int(changed.sum())
+        signs["_hard_flips"] = signs.get("_hard_flips", 0) + int(((eng != own) & ~tiny).sum())
+        if bool(changed.any()):
+            signs["_max_flip_ulps"] = max(signs.get("_max_flip_ulps", 0.0), float(ulps[changed].max()))
     return torch.where(pos, pre, pre * slope)
 
 
+def _absmm(s: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """Running-error scale of s-scaled inputs times w^T: s |w|^T (float64)."""
+    return s @ w.detach().abs().double().t()
+
+
 def sage_pool(g: OracleGraph, h: torch.Tensor, p: Dict[str, torch.Tensor], prefix: str,
-              use_weight: bool = False, parallel: bool = False, signs=None, sign_tol: float = 0.0
-              ) -> torch.Tensor:
+              use_weight: bool = False, parallel: bool = False, signs=None, sh: Optional[torch.Tensor] = None
+              ):
     """DGL 0.8.2 SAGEConv(aggregator_type='pool', feat_drop=0, bias=True, norm=None,
-    activation=None).forward(graph, feat[, edge_weight])."""
-    P = _act(h @ p[prefix + "fc_pool.weight"].t() + p[prefix + "fc_pool.bias"], 0.0, prefix + "pool", signs,
-             sign_tol)
+    activation=None).forward(graph, feat[, edge_weight]). With `signs` and `sh` (the
+    running-error scale of h) the decisions are aligned and (rst, scale of rst) returned."""
+    pre = h @ p[prefix + "fc_pool.weight"].t() + p[prefix + "fc_pool.bias"]
+    if signs is None:
+        P = torch.relu(pre)
+        neigh = _MaxAggregate.apply(P, g, use_weight, parallel, None)
+        return neigh @ p[prefix + "fc_neigh.weight"].t() + h @ p[prefix + "fc_self.weight"].t() + p[prefix + "bias"]
+    s_pool = _absmm(sh, p[prefix + "fc_pool.weight"]) + p[prefix + "fc_pool.bias"].detach().abs().double()
+    P = _act(pre, 0.0, prefix + "pool", signs, s_pool)
     align = None
-    if signs is not None and prefix + "argpos" in signs:
-        align = (signs[prefix + "argpos"], WINNER_TOL, signs)
+    if prefix + "argpos" in signs:
+        align = {"hint": signs[prefix + "argpos"], "scale": s_pool.numpy(), "band": BAND_ULPS * U32, "counts": signs}
     neigh = _MaxAggregate.apply(P, g, use_weight, parallel, align)
-    h_neigh = neigh @ p[prefix + "fc_neigh.weight"].t()
-    rst = h @ p[prefix + "fc_self.weight"].t() + h_neigh
+    if align is not None:
+        s_m = torch.gather(s_pool, 0, torch.from_numpy(align["argx"]))
+        if use_weight:
+            s_m = s_m * torch.from_numpy(np.abs(g.ew)).double()[torch.from_numpy(align["arge"])]
+    else:
+        s_m = torch.zeros_like(s_pool)
+    rst = neigh @ p[prefix + "fc_neigh.weight"].t() + h @ p[prefix + "fc_self.weight"].t() + p[prefix + "bias"]
+    s_rst = (_absmm(s_m, p[prefix + "fc_neigh.weight"]) + _absmm(sh, p[prefix + "fc_self.weight"])
+             + p[prefix + "bias"].detach().abs().double())
+    return rst, s_rst
+
+
+class _SumAggregate(torch.autograd.Function):
+    """update_all(copy_u|u_mul_e, sum|mean) (C: oracle_spmm_sum) with DGL's GSpMM backward:
+    the same aggregation over the reversed graph, dX[u] = sum_{e = (u -> v)} w_e dZ[v]
+    (mean: dZ[v] / max(in_deg(v), 1)), summed in edge-id order. Float64 inputs run the
+    whole aggregation in torch float64 (the yardstick)."""
+
+    @staticmethod
+    def forward(ctx, X, g, use_weight, mean):
+        ctx.g, ctx.use_weight, ctx.mean = g, use_weight, mean
+        if X.dtype == torch.float64:
+            return _sum_t(g, X, use_weight, mean)
+        return torch.from_numpy(spmm_sum(g, X.detach().numpy(), mean=mean, use_weight=use_weight))
+
+    @staticmethod
+    def backward(ctx, dZ):
+        g = ctx.g
+        src, dst = torch.from_numpy(g.src), torch.from_numpy(g.dst)
+        d = dZ
+        if ctx.mean:
+            deg = torch.from_numpy(np.maximum(g.in_degrees(), 1)).to(dZ.dtype)
+            d = dZ / deg[:, None]
+        m = d[dst]
+        if ctx.use_weight:
+            m = m * torch.from_numpy(g.ew).to(dZ.dtype)[:, None]
+        return torch.zeros_like(dZ).index_add_(0, src, m), None, None, None
+
+
+def _sum_t(g: OracleGraph, X: torch.Tensor, use_weight: bool, mean: bool) -> torch.Tensor:
+    src, dst = torch.from_numpy(g.src), torch.from_numpy(g.dst)
+    m = X[src]
+    if use_weight:
+        m = m * torch.from_numpy(g.ew).to(X.dtype)[:, None]
+    out = torch.zeros_like(X).index_add_(0, dst, m)
+    if mean:
+        out = out / torch.from_numpy(np.maximum(g.in_degrees(), 1)).to(X.dtype)[:, None]
+    return out
+
+
+def out_degrees(g: OracleGraph) -> np.ndarray:
+    return np.bincount(g.src, minlength=g.n)
+
+
+def graph_conv(g: OracleGraph, feat: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+               norm: str = "both", use_weight: bool = False) -> torch.Tensor:
+    """DGL 0.8.2 GraphConv.forward(graph, feat[, edge_weight]) (dgl/nn/pytorch/conv/
+    graphconv.py; BASELINE configs[0], not run by the reference: reference-unpinned):
+    norm 'left'/'both' scales the source features by out_degree.clamp(min=1)^-1/2 (or ^-1),
+    the product with weight [in, out] runs BEFORE the sum aggregation when in_feats >
+    out_feats and after it otherwise, norm 'right'/'both' scales by
+    in_degree.clamp(min=1)^-1/2 (or ^-1), then + bias."""
+    if norm in ("left", "both"):
+        degs = torch.from_numpy(out_degrees(g)).to(feat.dtype).clamp(min=1)
+        nrm = torch.pow(degs, -0.5) if norm == "both" else 1.0 / degs
+        feat = feat * nrm.reshape(-1, 1)
+    if weight.shape[0] > weight.shape[1]:
+        rst = _SumAggregate.apply(feat @ weight, g, use_weight, False)
+    else:
+        rst = _SumAggregate.apply(feat, g, use_weight, False) @ weight
+    if norm in ("right", "both"):
+        degs = torch.from_numpy(g.in_degrees()).to(feat.dtype).clamp(min=1)
+        nrm = torch.pow(degs, -0.5) if norm == "both" else 1.0 / degs
+        rst = rst * nrm.reshape(-1, 1)
+    if bias is not None:
+        rst = rst + bias
+    return rst
+
+
+def sage_mean(g: OracleGraph, h: torch.Tensor, p: Dict[str, torch.Tensor], prefix: str, aggr: str = "mean",
+              use_weight: bool = False) -> torch.Tensor:
+    """DGL 0.8.2 SAGEConv(aggregator_type='mean' | 'gcn').forward (reference-unpinned; the
+    reference runs 'pool' only): fc_neigh before the aggregation when in_feats > out_feats
+    (lin_before_mp), after it otherwise; 'mean' = fc_self(h) + fc_neigh(mean over in-edges)
+    + bias; 'gcn' = fc_neigh((sum over in-edges + h) / (in_degree + 1)) + bias."""
+    wn = p[prefix + "fc_neigh.weight"]
+    lin_before = wn.shape[1] > wn.shape[0]
+    src = h @ wn.t() if lin_before else h
+    if aggr == "mean":
+        neigh = _SumAggregate.apply(src, g, use_weight, True)
+    else:
+        s = _SumAggregate.apply(src, g, use_weight, False)
+        neigh = (s + src) / (torch.from_numpy(g.in_degrees()).to(h.dtype)[:, None] + 1)
+    if not lin_before:
+        neigh = neigh @ wn.t()
+    rst = neigh if aggr == "gcn" else h @ p[prefix + "fc_self.weight"].t() + neigh
     return rst + p[prefix + "bias"]
 
 
+def _graph_conv_scale(g: OracleGraph, sh: torch.Tensor, weight: torch.Tensor, bias, norm: str = "both",
+                      use_weight: bool = False) -> torch.Tensor:
+    """Running-error scale of graph_conv's output (the same operations on |values|)."""
+    if norm in ("left", "both"):
+        degs = torch.from_numpy(out_degrees(g)).double().clamp(min=1)
+        sh = sh * (torch.pow(degs, -0.5) if norm == "both" else 1.0 / degs).reshape(-1, 1)
+    wa = weight.detach().abs().double()
+    r = _sum_t(g, sh @ wa, use_weight, False) if weight.shape[0] > weight.shape[1] else _sum_t(g, sh, use_weight,
+                                                                                                False) @ wa
+    if norm in ("right", "both"):
+        degs = torch.from_numpy(g.in_degrees()).double().clamp(min=1)
+        r = r * (torch.pow(degs, -0.5) if norm == "both" else 1.0 / degs).reshape(-1, 1)
+    return r + (0.0 if bias is None else bias.detach().abs().double())
+
+
+def _sage_mean_scale(g: OracleGraph, sh: torch.Tensor, p, prefix: str, aggr: str, use_weight: bool) -> torch.Tensor:
+    wn = p[prefix + "fc_neigh.weight"]
+    lin_before = wn.shape[1] > wn.shape[0]
+    src = _absmm(sh, wn) if lin_before else sh
+    if aggr == "mean":
+        neigh = _sum_t(g, src, use_weight, True)
+    else:
+        neigh = (_sum_t(g, src, use_weight, False) + src) / (torch.from_numpy(g.in_degrees()).double()[:, None] + 1)
+    if not lin_before:
+        neigh = _absmm(neigh, wn)
+    r = neigh if aggr == "gcn" else _absmm(sh, p[prefix + "fc_self.weight"]) + neigh
+    return r + p[prefix + "bias"].detach().abs().double()
+
+
 def gnn32_forward(g: OracleGraph, x: torch.Tensor, p: Dict[str, torch.Tensor],
-                  use_weight: bool = False, parallel: bool = False, signs=None,
-                  sign_tol: float = 0.0) -> torch.Tensor:
-    """GNN32.forward (code/model.py:19-31), generalised to any number of conv layers.
-    Activation sites for `signs`: conv<i>.pool (relu of fc_pool), conv<i>.out (the layer's
-    leaky_relu), liner1."""
+                  use_weight: bool = False, parallel: bool = False, signs=None) -> torch.Tensor:
+    """GNN32.forward (code/model.py:19-31), generalised to any number of conv layers and,
+    for BASELINE configs[0] (reference-unpinned), to GraphConv / SAGEConv('mean'|'gcn')
+    layers (told apart by their parameter names: conv<i>.weight = GraphConv, no
+    fc_pool = SAGE mean, no fc_self = SAGE gcn).
+    Activation sites for `signs` (decision alignment, see _act): conv<i>.pool (relu of
+    fc_pool), conv<i>.out (the layer's leaky_relu), liner1; conv<i>.argpos the max
+    aggregation's winners. The running-error scale of every value is carried beside it."""
     h = x
+    sh = x.detach().abs().double() if signs is not None else None
     i = 1
-    while f"conv{i}.fc_pool.weight" in p:
-        h = _act(sage_pool(g, h, p, f"conv{i}.", use_weight, parallel, signs, sign_tol), 0.01, f"conv{i}.out",
-                 signs, sign_tol)
+    while f"conv{i}.bias" in p:
+        q = f"conv{i}."
+        s_y = None
+        if q + "weight" in p:
+            y = graph_conv(g, h, p[q + "weight"], p[q + "bias"], use_weight=use_weight)
+            if signs is not None:
+                s_y = _graph_conv_scale(g, sh, p[q + "weight"], p[q + "bias"], use_weight=use_weight)
+        elif q + "fc_pool.weight" in p:
+            r = sage_pool(g, h, p, q, use_weight, parallel, signs, sh)
+            y, s_y = r if signs is not None else (r, None)
+        else:
+            aggr = "mean" if q + "fc_self.weight" in p else "gcn"
+            y = sage_mean(g, h, p, q, aggr, use_weight)
+            if signs is not None:
+                s_y = _sage_mean_scale(g, sh, p, q, aggr, use_weight)
+        h = _act(y, 0.01, q + "out", signs, s_y)
+        sh = s_y
         i += 1
-    h = _act(h @ p["liner1.weight"].t() + p["liner1.bias"], 0.01, "liner1", signs, sign_tol)
+    pre = h @ p["liner1.weight"].t() + p["liner1.bias"]
+    s1 = None if signs is None else _absmm(sh, p["liner1.weight"]) + p["liner1.bias"].detach().abs().double()
+    h = _act(pre, 0.01, "liner1", signs, s1)
     h = h @ p["liner2.weight"].t() + p["liner2.bias"]
     return torch.sigmoid(h)
 
 
-def init_params(dims, seed: int = 0) -> Dict[str, torch.Tensor]:
+def init_params(dims, seed: int = 0, conv: str = "pool") -> Dict[str, torch.Tensor]:
     """Fresh parameters shaped like GNN32(dims[0], ..., num_classes); DGL 0.8 init
-    (xavier_uniform gain sqrt(2) on fc_pool/fc_self/fc_neigh, zero SAGE bias)."""
+    (xavier_uniform gain sqrt(2) on fc_pool/fc_self/fc_neigh, zero SAGE bias). conv:
+    'pool' (the reference), 'mean' / 'gcn' (SAGEConv variants) or 'graphconv' (GraphConv:
+    weight [in, out] xavier_uniform gain 1; the biases drawn small and non-zero here so
+    that their gradients are exercised)."""
     gen = torch.Generator().manual_seed(seed)
     n_conv = len(dims) - 3
     p: Dict[str, torch.Tensor] = {}
 
-    def xavier(o, i):
-        a = (2.0 ** 0.5) * (6.0 / (i + o)) ** 0.5
+    def xavier(o, i, gain=2.0 ** 0.5):
+        a = gain * (6.0 / (i + o)) ** 0.5
         return (torch.rand(o, i, generator=gen) * 2 - 1) * a
 
     def lin(o, i):
@@ -311,11 +498,17 @@ def init_params(dims, seed: int = 0) -> Dict[str, torch.Tensor]:
     for li in range(n_conv):
         fi, fo = dims[li], dims[li + 1]
         pre = f"conv{li + 1}."
-        p[pre + "fc_pool.weight"] = xavier(fi, fi)
-        p[pre + "fc_pool.bias"] = lin(fi, fi)[1]
+        if conv == "graphconv":
+            p[pre + "weight"] = xavier(fi, fo, 1.0)
+            p[pre + "bias"] = lin(fo, fo)[1] * 0.1
+            continue
+        if conv == "pool":
+            p[pre + "fc_pool.weight"] = xavier(fi, fi)
+            p[pre + "fc_pool.bias"] = lin(fi, fi)[1]
         p[pre + "fc_neigh.weight"] = xavier(fo, fi)
-        p[pre + "fc_self.weight"] = xavier(fo, fi)
-        p[pre + "bias"] = torch.zeros(fo)
+        if conv != "gcn":
+            p[pre + "fc_self.weight"] = xavier(fo, fi)
+        p[pre + "bias"] = torch.zeros(fo) if conv == "pool" else lin(fo, fo)[1] * 0.1
     w1, b1 = lin(dims[-2], dims[-3])
     w2, b2 = lin(dims[-1], dims[-2])
     p["liner1.weight"], p["liner1.bias"] = w1, b1
@@ -362,22 +555,22 @@ def adam_step_torch110(params, grads, exp_avg, exp_avg_sq, step: int, lr: float,
 # ---------------------------------------------------------------- one training step
 def train_step(g: OracleGraph, x: torch.Tensor, labels: torch.Tensor, train_index,
                i_weight, p: Dict[str, torch.Tensor], use_weight: bool = False,
-               parallel: bool = False, dtype=torch.float32, signs=None, sign_tol: float = 1e-5
+               parallel: bool = False, dtype=torch.float32, signs=None
                ) -> Tuple[torch.Tensor, torch.Tensor, Dict[str, torch.Tensor]]:
     """zero_grad -> forward -> multi_loss(train rows) -> backward (code/train.py:197-204).
     Returns (logits, loss, grads). parallel=True runs the message passing as DGL's CPU
     backend does (OpenMP rows forward, torch scatter_add_ backward): the CPU baseline.
     dtype=torch.float64 computes the same step in double precision (the yardstick the
     full-size tests use to judge two float32 results that differ by more than 1e-4).
-    signs: see _act — the activation decisions of another computation at pre-activations
-    within sign_tol * max|pre| of zero; "conv<i>.argpos" entries (N x F int32 in-row
-    positions) do the same for the max aggregation's winners (spmm_max_align)."""
+    signs: another computation's decisions, taken where they lie within the rounding band
+    (see _act / BAND_ULPS): "<site>" masks ("output > 0") and "conv<i>.argpos" (N x F int32
+    in-row winner positions, spmm_max_align); the counts come back in its "_" keys."""
     if dtype != torch.float32:  # the float64 yardstick: every tensor and product in double
         x = x.to(dtype)
         p = {k: v.to(dtype) for k, v in p.items()}
         labels = labels.to(dtype)
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
-    logits = gnn32_forward(g, x, leaves, use_weight, parallel, signs, sign_tol)
+    logits = gnn32_forward(g, x, leaves, use_weight, parallel, signs)
     loss = multi_loss(logits[train_index], labels[train_index], i_weight)
     loss.backward()
     return logits.detach(), loss.detach(), {k: v.grad.detach() for k, v in leaves.items()}

@@ -208,16 +208,24 @@ void oracle_spmm_max_f64(const int64_t* indptr, const int64_t* indices, const in
 
 /* Decision alignment for parity tests: after oracle_spmm_max[_f64] has run, entries where
  * another computation picked a different winning edge (`hint`: in-row positions of the
- * in-CSR, n_dst x F, -1 = none) whose value is within `tol` of the maximum (an absolute
- * band: the caller passes a fraction of the layer's largest |value|, the scale of the
- * float32 rounding of the values compared) take that winner instead. Which of two
- * candidates this close wins is decided by that rounding, not by the algorithm. Returns
- * the number of changed entries. */
+ * in-CSR, n_dst x F, -1 = none) take that winner when the two candidates lie within the
+ * rounding band of each other: m - val <= band * max(S[u_own, f] w_own, S[u_hint, f] w_hint),
+ * S (n_src x F) being the float64 running-error scale of X (the sum of |terms| X was formed
+ * from, propagated through the layers: oracle.py) — a few ulp of the magnitudes that
+ * formed THESE candidates. Which of two candidates this close wins is decided by float32
+ * rounding, not by the algorithm. Returns the number of changed entries; *hard counts the
+ * entries where the hint names a different winner OUTSIDE the band (a real disagreement),
+ * *max_gap the largest (m - val) / max(scale) among the changed entries. */
+static inline double cand_scale(const double* S, const float* w, int64_t u, int64_t e, int64_t F, int64_t f) {
+  return S[u * F + f] * (w ? fabs((double)w[e]) : 1.0);
+}
+
 int64_t oracle_spmm_max_align(const int64_t* indptr, const int64_t* indices, const int64_t* eids,
                               const float* w, const float* X, int64_t n_dst, int64_t F,
-                              const int32_t* hint, double tol, float* out, int64_t* argx,
-                              int64_t* arge) {
-  int64_t changed = 0;
+                              const int32_t* hint, const double* S, double band, float* out,
+                              int64_t* argx, int64_t* arge, int64_t* hard, double* max_gap) {
+  int64_t changed = 0, nhard = 0;
+  double gap_max = 0.0;
   for (int64_t v = 0; v < n_dst; ++v) {
     for (int64_t f = 0; f < F; ++f) {
       const int32_t p = hint[v * F + f];
@@ -227,22 +235,31 @@ int64_t oracle_spmm_max_align(const int64_t* indptr, const int64_t* indices, con
       if (u == argx[v * F + f] && e == arge[v * F + f]) continue;
       const float val = w ? X[u * F + f] * w[e] : X[u * F + f];
       const float m = out[v * F + f];
-      if ((double)m - (double)val <= tol) {
+      const double s0 = cand_scale(S, w, argx[v * F + f], arge[v * F + f], F, f);
+      const double s1 = cand_scale(S, w, u, e, F, f);
+      const double smax = s0 > s1 ? s0 : s1;
+      if ((double)m - (double)val <= band * smax) {
+        if (smax > 0.0 && ((double)m - (double)val) / smax > gap_max) gap_max = ((double)m - (double)val) / smax;
         out[v * F + f] = val;
         argx[v * F + f] = u;
         arge[v * F + f] = e;
         ++changed;
+      } else {
+        ++nhard;
       }
     }
   }
+  if (hard) *hard = nhard;
+  if (max_gap) *max_gap = gap_max;
   return changed;
 }
 
 int64_t oracle_spmm_max_align_f64(const int64_t* indptr, const int64_t* indices, const int64_t* eids,
                                   const double* w, const double* X, int64_t n_dst, int64_t F,
-                                  const int32_t* hint, double tol, double* out, int64_t* argx,
-                                  int64_t* arge) {
-  int64_t changed = 0;
+                                  const int32_t* hint, const double* S, double band, double* out,
+                                  int64_t* argx, int64_t* arge, int64_t* hard, double* max_gap) {
+  int64_t changed = 0, nhard = 0;
+  double gap_max = 0.0;
   for (int64_t v = 0; v < n_dst; ++v) {
     for (int64_t f = 0; f < F; ++f) {
       const int32_t p = hint[v * F + f];
@@ -252,13 +269,22 @@ int64_t oracle_spmm_max_align_f64(const int64_t* indptr, const int64_t* indices,
       if (u == argx[v * F + f] && e == arge[v * F + f]) continue;
       const double val = w ? X[u * F + f] * w[e] : X[u * F + f];
       const double m = out[v * F + f];
-      if (m - val <= tol) {
+      const int64_t uo = argx[v * F + f], eo = arge[v * F + f];
+      const double s0 = S[uo * F + f] * (w ? fabs(w[eo]) : 1.0);
+      const double s1 = S[u * F + f] * (w ? fabs(w[e]) : 1.0);
+      const double smax = s0 > s1 ? s0 : s1;
+      if (m - val <= band * smax) {
+        if (smax > 0.0 && (m - val) / smax > gap_max) gap_max = (m - val) / smax;
         out[v * F + f] = val;
         argx[v * F + f] = u;
         arge[v * F + f] = e;
         ++changed;
+      } else {
+        ++nhard;
       }
     }
   }
+  if (hard) *hard = nhard;
+  if (max_gap) *max_gap = gap_max;
   return changed;
 }

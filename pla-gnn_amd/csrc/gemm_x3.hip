@@ -422,130 +422,3 @@ extern "C" int pg_x3_stamps(void* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pg_x3_stamp), sizeof(pg_x3_stamp), 0, hipMemcpyDeviceToHost);
 }
 #endif
-
-#if PG_X3_PLANES_PROBE
-// Probe builds only: the three-piece GEMM with both operands given as pre-split bf16 pieces,
-// staged by LDS-DMA (no register staging, no split, no LDS stores by the waves): how fast is
-// the kernel when the split happens in the producers? A [M][K] pieces, B [N][K] (transb) or
-// [K][N] pieces, plane p at base + p * stride; C = A B (f32), no epilogue.
-namespace {
-template <int ROWS, bool KMAJ, bool FULL>
-__device__ __forceinline__ void probe_pdma(const uint16_t* __restrict__ P, int64_t ld, int r0, int R, int k0,
-                                           int kvalid, uint16_t* S, int wave, int lane) {
-  constexpr int PIECES = ROWS * KS * 2 / 1024;
-  for (int piece = wave; piece < PIECES; piece += 4) {
-    const int u = piece * 64 + lane;
-    const uint16_t* src;
-    bool valid;
-    if constexpr (!KMAJ) {
-      const int row = u >> 1, c = (u & 1) ^ ((row >> 3) & 1);
-      valid = 8 * c < kvalid;
-      src = P + (int64_t)min(r0 + row, R - 1) * ld + k0 + 8 * c;
-    } else {
-      const int k = u / (ROWS / 8), pos = u % (ROWS / 8);
-      const int c = pos ^ (ROWS == 64 ? ((k >> 1) & 1) * 4 : (k & 3) * 4);
-      valid = k < kvalid;
-      src = P + (int64_t)(k0 + k) * ld + min(r0 + 8 * c, R - 8);
-    }
-    if (FULL || valid) __builtin_amdgcn_global_load_lds(src, S + piece * 512, 16, 0, 0);
-    else *reinterpret_cast<uint4*>(S + u * 8) = make_uint4(0u, 0u, 0u, 0u);
-  }
-}
-
-template <int BM, int BN, bool TB>
-__global__ __launch_bounds__(NT) void gemm_x3pl_kernel(int M, int N, int K, int tiles_n, int tiles,
-                                                       const uint16_t* __restrict__ Ap, int64_t aps, int64_t lda,
-                                                       const uint16_t* __restrict__ Bp, int64_t bps, int64_t ldb,
-                                                       float* __restrict__ C, int64_t ldc) {
-  constexpr bool BKM = !TB;
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int IA = BM * KS, IB = BN * KS;
-  constexpr int BUF = 3 * (IA + IB);
-  constexpr int STAGE_U16 = 2 * BUF;
-  constexpr int PASSES = 2 * BM * BN > STAGE_U16 ? 2 : 1;
-  constexpr int EPI_U16 = 2 * BM * BN / PASSES;
-  constexpr int LDS_U16 = STAGE_U16 > EPI_U16 ? STAGE_U16 : EPI_U16;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
-  const int b = blockIdx.x;
-  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
-  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, l32 = lane & 31;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const int nk = (K + KS - 1) / KS;
-  auto issue = [&](int t, int buf) {
-    const int k0 = t * KS;
-    uint16_t* S = lds + buf * BUF;
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      if (K - k0 >= KS) {
-        probe_pdma<BM, false, true>(Ap + p * aps, lda, m0, M, k0, KS, S + p * IA, wave, lane);
-        probe_pdma<BN, BKM, true>(Bp + p * bps, ldb, n0, N, k0, KS, S + 3 * IA + p * IB, wave, lane);
-      } else {
-        probe_pdma<BM, false, false>(Ap + p * aps, lda, m0, M, k0, K - k0, S + p * IA, wave, lane);
-        probe_pdma<BN, BKM, false>(Bp + p * bps, ldb, n0, N, k0, K - k0, S + 3 * IA + p * IB, wave, lane);
-      }
-    }
-  };
-  issue(0, 0);
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nk) issue(t + 1, cur ^ 1);
-    const uint16_t* As = lds + cur * BUF;
-    const uint16_t* Bs = As + 3 * IA;
-    bf16x8 fa[3][TM], fb[3][TN];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) fa[p][i] = frag<BM, false>(As + p * IA, ra + i * 32, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) fb[p][j] = frag<BN, BKM>(Bs + p * IB, rb + j * 32, lane);
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[2][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2][i], fb[0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[1][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fb[0][j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
-      }
-    __syncthreads();
-  }
-  x3_store<BM, BN, EPI_NONE, PASSES>(acc, reinterpret_cast<float*>(lds), tid, m0, n0, M, N, 0, 1.f, 0.f, C, ldc,
-                                     nullptr, 0.f, nullptr, 0, nullptr);
-}
-}  // namespace
-
-extern "C" int pg_x3_planes_probe(int transb, int M, int N, int K, const uint16_t* Ap, int64_t aps, int64_t lda,
-                                  const uint16_t* Bp, int64_t bps, int64_t ldb, float* C, int64_t ldc, int bm,
-                                  int bn, void* stream) {
-  const int tiles_n = (N + bn - 1) / bn, tiles = tiles_n * ((M + bm - 1) / bm);
-  hipStream_t st = (hipStream_t)stream;
-#define PL(BM_, BN_)                                                                                            \
-  {                                                                                                             \
-    if (transb) hipLaunchKernelGGL((gemm_x3pl_kernel<BM_, BN_, true>), dim3(tiles), dim3(NT), 0, st, M, N, K, \
-                                   tiles_n, tiles, Ap, aps, lda, Bp, bps, ldb, C, ldc);                          \
-    else hipLaunchKernelGGL((gemm_x3pl_kernel<BM_, BN_, false>), dim3(tiles), dim3(NT), 0, st, M, N, K,        \
-                            tiles_n, tiles, Ap, aps, lda, Bp, bps, ldb, C, ldc);                                 \
-    return (int)hipGetLastError();                                                                              \
-  }
-  if (bm == 128 && bn == 128) PL(128, 128)
-  if (bm == 128 && bn == 64) PL(128, 64)
-  if (bm == 64 && bn == 64) PL(64, 64)
-#undef PL
-  return -1;
-}
-#endif

@@ -262,6 +262,17 @@ class TrainEngine:
     def state_dict(self) -> Dict[str, torch.Tensor]:
         return self._unpad(self.P)
 
+    def params_updated(self) -> None:
+        """Call after writing `flat` from outside the engine (e.g. a broadcast from rank 0):
+        refreshes whatever the engine derives from the parameters (nothing in fp32)."""
+
+    def broadcast_params(self, src: int = 0) -> None:
+        """Every rank takes rank `src`'s parameters (multi-GPU replicas start identical)."""
+        from . import dist as pdist
+
+        pdist.broadcast_([self.flat], src)
+        self.params_updated()
+
     def grads(self) -> Dict[str, torch.Tensor]:
         return self._unpad(self.G)
 
@@ -274,35 +285,75 @@ class TrainEngine:
     # ------------------------------------------------------------------ timing
     @contextlib.contextmanager
     def _t(self, name: str, work: float = 0.0):
-        """HIP events around one launch on the engine's stream (diagnostic passes only)."""
+        """HIP events around one launch on the engine's stream (diagnostic passes only).
+        While a step is being captured the events are external: they become event-record
+        nodes of the graph, so the timed launches are the graph's own."""
         if self._timing is None:
             yield
             return
         st = torch.cuda.current_stream(self.device)
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
+        ext = torch.cuda.is_current_stream_capturing()
+        a = torch.cuda.Event(enable_timing=True, external=ext)
+        b = torch.cuda.Event(enable_timing=True, external=ext)
         a.record(st)
         yield
         b.record(st)
         self._timing.append((name, work, a, b))
 
-    def kernel_breakdown(self, reps: int = 5) -> Dict[str, Dict[str, float]]:
-        """Per-launch-site mean duration (ms) and work over `reps` eager steps, timed with
-        HIP events on the launch stream. Returns {name: {ms, work, calls}} per step. A
-        diagnostic of this process alone: the steps run without the gradient all-reduce
-        (the other ranks take no part in them)."""
+    def kernel_breakdown(self, reps: int = 5, graph: bool = True) -> Dict[str, Dict[str, float]]:
+        """Per-launch-site mean duration (ms) and work over `reps` steps, timed with HIP
+        events on the launch stream. Returns {name: {ms, work, calls}} per step, and the
+        method used under the key "_method". graph=True captures one step (forward,
+        backward, Adam) with an event-record node around every launch and replays it: the
+        launches are timed as the benchmark's replayed graph runs them. If the runtime
+        refuses timing events in a graph, eager steps are timed instead, each issued behind
+        a GPU spin (torch.cuda._sleep) so that the host has queued the whole step before
+        the GPU starts it (no host gaps inside the measured launches). A diagnostic of this
+        process alone: the steps run without the gradient all-reduce. Each timed step is a
+        real training step."""
         acc: Dict[str, List[float]] = defaultdict(lambda: [0.0, 0.0, 0])
-        for _ in range(reps):
-            self._timing = []
-            self.step_eager(None)
-            torch.cuda.synchronize(self.device)
-            for name, work, a, b in self._timing:
+
+        def collect(timing):
+            for name, work, a, b in timing:
                 r = acc[name]
                 r[0] += a.elapsed_time(b)
                 r[1] += work
                 r[2] += 1
-            self._timing = None
-        return {k: {"ms": v[0] / reps, "work": v[1] / reps, "calls": v[2] / reps} for k, v in acc.items()}
+
+        method = "eager+spin"
+        if graph:
+            try:
+                self._timing = []
+                g = torch.cuda.CUDAGraph()
+                s = torch.cuda.Stream(self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.graph(g, stream=s):
+                    self.forward()
+                    self.backward()
+                    self.adam()
+                timing, self._timing = self._timing, None
+                for _ in range(reps):
+                    g.replay()
+                    torch.cuda.synchronize(self.device)
+                    collect(timing)
+                    self.steps_done += 1
+                method = "graph"
+                del g
+            except Exception:  # noqa: BLE001 - timing nodes unsupported: time eager steps
+                self._timing = None
+                acc.clear()
+                torch.cuda.synchronize(self.device)
+        if method != "graph":
+            for _ in range(reps):
+                self._timing = []
+                torch.cuda._sleep(20_000_000)
+                self.step_eager(None)
+                torch.cuda.synchronize(self.device)
+                collect(self._timing)
+                self._timing = None
+        out = {k: {"ms": v[0] / reps, "work": v[1] / reps, "calls": v[2] / reps} for k, v in acc.items()}
+        out["_method"] = method
+        return out
 
     # ------------------------------------------------------------------ kernels
     def _s(self):

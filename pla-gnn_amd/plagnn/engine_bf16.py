@@ -101,6 +101,10 @@ class TrainEngineBF16(TrainEngine):
         if hasattr(self, "wb"):
             self._cast_weights()
 
+    def params_updated(self) -> None:
+        """The bf16 weight copies follow the f32 master parameters."""
+        self._cast_weights()
+
     def _alloc_workspace(self) -> None:
         N, pd, C, dev = self.N, self.pd, self.C, self.device
         L = _lib.lib()

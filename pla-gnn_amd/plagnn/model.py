@@ -13,7 +13,7 @@ import torch as th
 import torch.nn as nn
 import torch.nn.functional as F
 
-from dgl.nn.pytorch import SAGEConv
+from dgl.nn.pytorch import GraphConv, SAGEConv
 
 
 class GNN32(nn.Module):
@@ -42,17 +42,28 @@ class GNN32(nn.Module):
 
 
 class GNN(nn.Module):
-    """GNN32 with any number of SAGE-pool layers: dims = [in, h_1, ..., h_L, h_mlp, classes]."""
+    """GNN32 with any number of graph layers: dims = [in, h_1, ..., h_L, h_mlp, classes].
+    conv = 'pool' (the reference's SAGEConv aggregator), or for BASELINE configs[0]
+    ("2-layer GraphConv hidden=64"; not a configuration of the reference, reference-
+    unpinned) 'graphconv' (dgl.nn.pytorch.GraphConv, norm 'both') and the SAGEConv
+    variants 'mean' / 'gcn'."""
 
-    def __init__(self, dims: Sequence[int]):
+    def __init__(self, dims: Sequence[int], conv: str = "pool"):
         super().__init__()
         dims = list(dims)
         if len(dims) < 4:
             raise ValueError("dims = [in, h_1, ..., h_L, h_mlp, classes] with L >= 1")
         self.dims = dims
+        self.conv = conv
         self.n_conv = len(dims) - 3
         for i in range(self.n_conv):
-            setattr(self, f"conv{i + 1}", SAGEConv(dims[i], dims[i + 1], "pool"))
+            if conv == "graphconv":
+                layer = GraphConv(dims[i], dims[i + 1])
+            elif conv in ("pool", "mean", "gcn"):
+                layer = SAGEConv(dims[i], dims[i + 1], conv)
+            else:
+                raise ValueError(f"unknown conv {conv!r}")
+            setattr(self, f"conv{i + 1}", layer)
         self.liner1 = nn.Linear(dims[-3], dims[-2])
         self.liner2 = nn.Linear(dims[-2], dims[-1])
 

@@ -38,10 +38,14 @@ _scratch = {}
 def _workspace(nbytes: int, device) -> Optional[torch.Tensor]:
     """Library scratch for one call: one buffer per (device, stream), grown on demand and
     reused by every later call on that stream (stream order makes the reuse safe), so the
-    drop-in path's autograd functions allocate nothing per call."""
+    drop-in path's autograd functions allocate nothing per call. During HIP-graph capture a
+    call gets a fresh buffer from the graph's private pool instead: a cached buffer would
+    be shared between the graph's replays and eager calls that can run beside them."""
     if nbytes <= 0:
         return None
     device = torch.device(device)
+    if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        return torch.empty(int(nbytes), dtype=torch.uint8, device=device)
     key = (str(device), torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0)
     buf = _scratch.get(key)
     if buf is None or buf.numel() < nbytes:

@@ -1,9 +1,13 @@
 """The benchmark workloads of BASELINE.json `configs`, built the same way
 for bench.py and the full-size parity tests.
 
+  cfg1   S0, 2 GraphConv layers of hidden 64 (BASELINE configs[0]; dgl GraphConv, norm
+         'both'), then the reference's MLP head: not a configuration of the reference
+         (its layers are SAGEConv 'pool'), reference-unpinned
   cfg2   S0 PPI stand-in (N = 24 041, mean degree 50), SAGE-pool 503 -> 256 x 3, fp32
   ref    S0, the reference's own dims GNN32(503, 400, 300, 200, 100, 12) (code/train.py:179)
-  cfg3   S0 with about ±3 % of its edges changed, ECC of that graph (pg_ecc,
+  cfg3   GSE30931's PPI_inter of S0 (pg_perturb with the dataset's threshold,
+         code/data_preprocess.py:217-257, 498), ECC of that graph (pg_ecc,
          code/data_preprocess.py:175-214) as u_mul_e edge weights, hidden 512, fp32
   cfg4   the perturbation replicas of main_inter.py: rank r trains variant r % 4 —
          0 the normal graph, 1-3 <GSE>/PPI_inter for GSE30931 / GSE27182 / GSE74572, each
@@ -25,16 +29,19 @@ import torch
 
 from . import data
 from .graph import CSRGraph
-from .train import fold_splits, weight_cal
+from .train import FOLD_SEEDS, fold_splits, weight_cal
 
 CONFIGS = {
     # name: (graph kind, dims, bf16, description)
+    "cfg1": ("s0", [503, 64, 64, 100, 12], False,
+             "S0 PPI stand-in, 2x GraphConv (norm both) hidden 64 + MLP 64 -> 100 -> 12, fp32"),
     "cfg2": ("s0", [503, 256, 256, 256, 100, 12], False,
              "S0 PPI stand-in (N=24041, mean deg 50), 3x SAGE-pool hidden 256, fp32"),
     "ref": ("s0", [503, 400, 300, 200, 100, 12], False,
             "S0 PPI stand-in, reference dims GNN32(503,400,300,200,100,12), fp32"),
     "cfg3": ("s0", [503, 512, 512, 512, 100, 12], False,
-             "S0 perturbed (+-3% edges), ECC edge weights (pg_ecc, u_mul_e max), hidden 512, fp32"),
+             "GSE30931 PPI_inter of S0 (pg_perturb, thr 2.75), ECC_inter edge weights (pg_ecc, u_mul_e max), "
+             "hidden 512, fp32"),
     "cfg4": ("s0", [503, 400, 300, 200, 100, 12], False,
              "normal S0 + PPI_inter replicas of GSE30931/GSE27182/GSE74572 (pg_perturb, the reference "
              "thresholds), one graph per rank (rank % 4), reference dims, grad all-reduce"),
@@ -45,6 +52,7 @@ CONFIGS = {
                  "RMAT x16 PPI (N=384656, a,b,c,d=.57,.19,.19,.05, mean deg 50), hidden 512, fp32"),
 }
 CFG4_VARIANTS = ["normal"] + list(data.GSE_THRESHOLDS)
+CONV = {"cfg1": "graphconv"}  # the graph layer of each config (default: SAGEConv 'pool')
 
 
 @dataclass
@@ -61,6 +69,7 @@ class Workload:
     train_index: List[int]
     val_index: List[int]
     class_weight: np.ndarray
+    conv: str = "pool"
 
     def graph(self) -> CSRGraph:
         return CSRGraph(self.src, self.dst, self.ds.n)
@@ -110,20 +119,31 @@ def perturbed_graph(ds: data.Dataset, gse: str, device="cuda"):
     return res.row.astype(np.int64), res.col.astype(np.int64)
 
 
-def build(name: str, rank: int = 0, device="cuda", n: Optional[int] = None) -> Workload:
+def fold_job(label, job: int):
+    """The reference's training job `job` of its rounds x folds loop (code/train.py:162-178,
+    10 folds): round job // 10 (KFold seed FOLD_SEEDS[round]), fold job % 10."""
+    rnd, fold = divmod(int(job), 10)
+    splits = fold_splits(label, 10, FOLD_SEEDS[rnd % len(FOLD_SEEDS)])
+    for _ in range(fold):
+        next(splits)
+    return next(splits)
+
+
+def build(name: str, rank: int = 0, device="cuda", n: Optional[int] = None, job: int = 0) -> Workload:
     """The workload of BASELINE config `name` for `rank` (n overrides the node count, for
-    reduced-size parity cases of the same construction)."""
+    reduced-size parity cases of the same construction; job selects the (round, fold) of
+    the train / val rows, fold_job; 0 = round 1, fold 1)."""
     kind, dims, bf16, desc = CONFIGS[name]
     ds = data.make_dataset(kind, n=n, seed=70)
     label = [int(i) for i in ds.labelled]
-    train_idx, val_idx = next(fold_splits(label, 10, 12))  # round 1, fold 1
+    train_idx, val_idx = fold_job(label, job)
     w = weight_cal(ds.loc)
     variant = "normal"
     ew = None
     if name == "cfg3":
-        row, col = data.random_perturbation(ds, seed=70)
+        row, col = perturbed_graph(ds, "GSE30931", device)
         src, dst, ew = _with_loops(row, col, ds.n, ecc_weights(row, col, ds.n, device))
-        variant = "perturbed+-3%+ecc"
+        variant = "GSE30931+ecc"
     elif name == "cfg4":
         variant = CFG4_VARIANTS[rank % len(CFG4_VARIANTS)]
         if variant == "normal":
@@ -133,4 +153,5 @@ def build(name: str, rank: int = 0, device="cuda", n: Optional[int] = None) -> W
             src, dst, _ = _with_loops(row, col, ds.n)
     else:
         src, dst = ds.edges_with_self_loops()
-    return Workload(name, list(dims), bf16, desc, ds, src, dst, ew, variant, train_idx, val_idx, w)
+    return Workload(name, list(dims), bf16, desc, ds, src, dst, ew, variant, train_idx, val_idx, w,
+                    CONV.get(name, "pool"))

@@ -29,8 +29,9 @@ void oracle_spmm_max_bwd(const int64_t* argx, const int64_t* arge, const float* 
 void oracle_spmm_sum(const int64_t* indptr, const int64_t* indices, const int64_t* eids, const float* w,
                      const float* X, int64_t n_dst, int64_t F, int mean, float* out);
 int64_t oracle_spmm_max_align(const int64_t* indptr, const int64_t* indices, const int64_t* eids, const float* w,
-                              const float* X, int64_t n_dst, int64_t F, const int32_t* hint, double tol, float* out,
-                              int64_t* argx, int64_t* arge);
+                              const float* X, int64_t n_dst, int64_t F, const int32_t* hint, const double* S,
+                              double band, float* out, int64_t* argx, int64_t* arge, int64_t* hard,
+                              double* max_gap);
 int64_t oracle_ecc(const int64_t* indptr, const int64_t* indices, const double* data, int64_t n, double epsilon,
                    int64_t* rows, int64_t* cols, double* vals);
 void oracle_perturb_sd(const double* xc, int64_t n, int S, double inv_fact, double* sd);
@@ -135,8 +136,18 @@ static void run_case(int64_t n, int64_t e, int64_t hub, int64_t F, int chunk, bo
   oracle_spmm_max_bwd(argx_o.data(), arge_o.data(), w, dZ.data(), has_in.data(), n, n, F, odx.data());
   oracle_spmm_sum(optr.data(), oind.data(), oeid.data(), w, X.data(), n, F, 1, osum.data());
   std::vector<int32_t> hint(n * F, -1);
-  oracle_spmm_max_align(optr.data(), oind.data(), oeid.data(), w, X.data(), n, F, hint.data(), 0.0, oout2.data(),
-                        ax2.data(), ae2.data());
+  for (int64_t v = 0; v < n; ++v)  // every row's hint: its first in-edge (real mismatches mostly)
+    for (int64_t f = 0; f < F; ++f) hint[v * F + f] = optr[v + 1] > optr[v] ? 0 : -1;
+  std::vector<double> S(n * F);
+  for (int64_t i = 0; i < n * F; ++i) S[i] = std::fabs((double)X[i]);
+  std::vector<float> oout3(oout2);
+  std::vector<int64_t> ax3(ax2), ae3(ae2);
+  int64_t hard = -1;
+  double gap = -1.0;
+  const int64_t changed = oracle_spmm_max_align(optr.data(), oind.data(), oeid.data(), w, X.data(), n, F, hint.data(),
+                                                S.data(), 0.0, oout3.data(), ax3.data(), ae3.data(), &hard, &gap);
+  CHECK(changed >= 0 && hard >= 0 && gap == 0.0, "align counts");
+  for (int64_t i = 0; i < n * F; ++i) CHECK(oout3[i] <= oout2[i], "align never raises a maximum (%ld)", (long)i);
   for (int64_t i = 0; i < n * F; ++i) {
     const int64_t v = i / F;
     CHECK(out[i] == oout[i] && out[i] == oout2[i], "max value (%ld)", (long)i);

@@ -17,6 +17,7 @@ from conftest import PKG, ROOT, random_graph
 pytestmark = pytest.mark.gpu
 DIMS = (31, 24, 20, 16, 10, 12)
 LR = 1e-3
+DEV = "cuda"
 
 
 def _problem(rank):
@@ -102,3 +103,97 @@ def test_engine_two_rank_allreduce_matches_serial_adam(tmp_path, oracle_mod):
         settled = g.abs() > 1e-4 * max(g.abs().max().item(), 1e-30)
         err = ((got[0][k].double() - p[k].double()).abs() * settled).max().item()
         assert err <= 1e-4 * scale, f"{k}: {err:.3e} vs scale {scale:.3e}"
+
+
+def _worker_cfg4(rank, world, port, outdir):
+    """Rank r trains cfg4 replica r + 1 (GSE30931 / GSE27182 PPI_inter, reference dims)."""
+    import sys
+
+    sys.path[:0] = [PKG, ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import plagnn
+    from plagnn import dist as pdist
+    from plagnn import workload
+    from test_gpu_fullsize import _engine_signs
+
+    torch.cuda.set_device(0)
+    assert pdist.init("gloo")
+    wl = workload.build("cfg4", rank=rank + 1, device="cuda:0")
+    sd = torch.load(os.path.join(outdir, "sd.pt"), weights_only=True)
+    if rank == 1:  # a different start everywhere but rank 0: the broadcast must fix it
+        sd = {k: v + 0.01 for k, v in sd.items()}
+    eng = plagnn.TrainEngine(wl.graph(), torch.from_numpy(wl.ds.feat), torch.from_numpy(wl.ds.loc.astype(np.float32)),
+                             wl.dims, wl.class_weight, wl.train_index, wl.val_index, lr=5e-5, device="cuda:0",
+                             params=sd)
+    eng.broadcast_params()
+    eng.forward()
+    eng.backward()
+    torch.cuda.synchronize()
+    signs = {k: torch.from_numpy(v) if isinstance(v, np.ndarray) else v for k, v in _engine_signs(eng).items()}
+    local = {k: v.cpu() for k, v in eng.grads().items()}
+    pdist.allreduce_mean(eng.gflat)
+    eng.adam()
+    torch.cuda.synchronize()
+    step1 = {k: v.cpu() for k, v in eng.state_dict().items()}
+    eng.capture(warmup=0, allreduce=pdist.allreduce_mean)
+    eng.step()
+    torch.cuda.synchronize()
+    step2 = {k: v.cpu() for k, v in eng.state_dict().items()}
+    torch.save({"signs": signs, "local": local, "step1": step1, "step2": step2},
+               os.path.join(outdir, f"cfg4_rank{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_cfg4_two_replicas_allreduce_matches_serial_adam(tmp_path, oracle_mod):
+    """BASELINE configs[3] on two ranks: each holds a DIFFERENT cfg4 perturbation graph
+    (GSE30931 and GSE27182 PPI_inter, N = 24,041, reference dims). Checked: each rank's
+    local gradient against the oracle's on its own graph (the bars of
+    test_gpu_fullsize._check_step), the step-1 parameters against serial Adam on the
+    oracle's averaged gradients, and bitwise agreement of the ranks after a second,
+    graph-captured step."""
+    from plagnn import workload
+    from test_gpu_fullsize import LR, _check_signs, _close_judged, _oracle_graph, _Yardstick
+
+    world = 2
+    dims = workload.CONFIGS["cfg4"][1]
+    sd = oracle_mod.init_params(dims, seed=20)
+    torch.save(sd, tmp_path / "sd.pt")
+    mp.start_processes(_worker_cfg4, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    got = [torch.load(tmp_path / f"cfg4_rank{r}.pt", weights_only=True) for r in range(world)]
+    for k in got[0]["step2"]:
+        assert torch.equal(got[0]["step2"][k], got[1]["step2"][k]), f"ranks diverged on {k}"
+    ref = []
+    for r in range(world):
+        wl = workload.build("cfg4", rank=r + 1, device=DEV)
+        og = _oracle_graph(oracle_mod, wl)
+        x = torch.from_numpy(wl.ds.feat)
+        labels = torch.from_numpy(wl.ds.loc.astype(np.float32))
+        signs = {k: v.numpy() if k.endswith("argpos") else v for k, v in got[r]["signs"].items()}
+        _, _, g = oracle_mod.train_step(og, x, labels, wl.train_index, wl.class_weight, sd, signs=signs)
+        _check_signs(signs)
+        s64 = {k: v for k, v in signs.items() if not k.startswith("_")}
+        exact = _Yardstick(lambda og=og, x=x, labels=labels, wl=wl, s64=s64: oracle_mod.train_step(
+            og, x, labels, wl.train_index, wl.class_weight, sd, dtype=torch.float64, signs=s64))
+        for k, v in g.items():
+            _close_judged(got[r]["local"][k], v, lambda k=k, exact=exact: exact.get()[2][k], name=f"rank{r} grad {k}")
+        ref.append(g)
+    keys = list(sd)
+    zeros = lambda: [torch.zeros_like(sd[k]) for k in keys]  # noqa: E731
+    avg = {k: (ref[0][k] + ref[1][k]) / 2 for k in keys}
+    p_ref = [sd[k].clone() for k in keys]
+    oracle_mod.adam_step_torch110(p_ref, [avg[k] for k in keys], zeros(), zeros(), 1, LR)
+    own = {k: (got[0]["local"][k] + got[1]["local"][k]) / 2 for k in keys}
+    p_own = [sd[k].clone() for k in keys]
+    oracle_mod.adam_step_torch110(p_own, [own[k] for k in keys], zeros(), zeros(), 1, LR)
+    for k, pr, po in zip(keys, p_ref, p_own):
+        for r in range(world):
+            p1 = got[r]["step1"][k].double()
+            scale = max(pr.abs().max().item(), 1e-12)
+            g = avg[k].double()
+            settled = g.abs() > 1e-4 * max(g.abs().max().item(), 1e-30)
+            err = ((p1 - pr.double()).abs() * settled).max().item()
+            assert err <= 1e-4 * scale, f"rank{r} adam {k}: {err:.3e} vs scale {scale:.3e}"
+            assert (p1 - po.double()).abs().max().item() <= 1e-6 * scale, f"rank{r} adam(own grads) {k}"

@@ -6,20 +6,20 @@ deferred batched combine at K = 24,041, the chunked hub rows of the max forward 
 backward, the zero-maximum skip of the backward.
 
 Bars (north_star "within 1e-4 fp32"):
-* decision-aligned: the oracle takes the engine's relu / leaky_relu decision at the
-  pre-activations that lie within 1e-5 of zero (relative to the layer's largest), and the
-  engine's winning edge where it is within 1e-6 of the maximum (relative to the layer's
-  largest value, oracle.WINNER_TOL). There the derivative
-  (1 or 0.01) or the winner (whose edge weight scales the gradient) is decided by float32
-  rounding, and one flipped entry moves a 24,041-term weight gradient by ~1e-4 of its
-  scale. The numbers of changed decisions are asserted small;
+* decision-aligned: a relu / leaky_relu decision at a pre-activation within
+  oracle.BAND_ULPS (16) x 2^-24 of its running-error scale (the float64 sum of |terms|
+  the value was formed from, propagated through the layers), and the winner of a maximum
+  whose two candidates lie that close, are taken from the engine: there float32 rounding
+  decides them, not the algorithm, and one flipped entry moves a 24,041-term weight
+  gradient by ~1e-4 of its scale. Differing decisions OUTSIDE the band ("hard") must be
+  zero, and the counts of aligned ones are capped near twice the observed counts;
 * logits, train/val loss, every parameter gradient: max |err| <= 1e-4 * max |oracle|.
   Where the two float32 computations (engine, oracle) differ by more than that — a weight
   gradient is a 24,041-term sum whose float32 rounding depends on the summation order —
   the same step in float64 (oracle, dtype=float64, same decisions) decides: the engine
   must then be within 1e-4 of the float64 result or no farther from it than 2x the float32
   oracle's own distance (a bias gradient summing cancelling terms can sit 2e-4 from exact
-  in either float32 order);
+  in either float32 order). The number of tensors judged that way is printed and capped;
 * post-Adam parameters (lr 5e-5, code/main_normal.py:26): Adam's first step moves every
   entry by about lr * sign(g), so an entry whose oracle gradient lies inside the gradient
   tolerance (|g| <= 1e-4 * max|g|) may legitimately move the other way. Those entries are
@@ -68,19 +68,23 @@ class _Yardstick:
         return self.val
 
 
-def _close_judged(a, b, exact, name=""):
-    """_close at 1e-4; past it, judged against the float64 result `exact()`."""
+def _close_judged(a, b, exact, name="") -> bool:
+    """_close at 1e-4; past it, judged against the float64 result `exact()`. Returns True
+    when the float64 judgement was needed."""
     a = a.detach().cpu().double()
     b = b.detach().cpu().double()
     scale = max(b.abs().max().item(), 1e-12)
     err = (a - b).abs().max().item()
     if err <= 1e-4 * scale:
-        return
+        return False
     t = exact().detach().cpu().double()
     e_got = (a - t).abs().max().item()
     e_ref = (b - t).abs().max().item()
+    print(f"  {name}: engine-oracle {err / scale:.2e} of scale; vs float64 engine {e_got / scale:.2e}, "
+          f"oracle {e_ref / scale:.2e}")
     assert e_got <= max(1e-4 * scale, 2.0 * e_ref), (
         f"{name}: engine-oracle {err:.3e} (scale {scale:.3e}); vs float64: engine {e_got:.3e}, oracle {e_ref:.3e}")
+    return True
 
 
 def _engine_signs(eng):
@@ -106,6 +110,25 @@ def _oracle_graph(oracle_mod, wl):
     return oracle_mod.OracleGraph(src, dst, wl.n, edge_weight=w)
 
 
+# caps: about twice the largest counts observed on the BASELINE workloads (printed by each
+# test)
+CAP_FLIPS, CAP_TIES, CAP_FALLBACK = 40, 200, 1
+
+
+def _decision_stats(signs) -> dict:
+    return {k: signs.get(k, 0) for k in ("_flips", "_ties", "_hard_flips", "_hard_ties", "_max_flip_ulps",
+                                         "_max_tie_ulps")}
+
+
+def _check_signs(signs):
+    st = _decision_stats(signs)
+    print(f"decisions taken from the engine: activations {st['_flips']} (largest {st['_max_flip_ulps']:.2f} ulp of "
+          f"scale), winners {st['_ties']} (largest {st['_max_tie_ulps']:.2f} ulp); outside the band: "
+          f"{st['_hard_flips']} / {st['_hard_ties']}")
+    assert st["_hard_flips"] == 0 and st["_hard_ties"] == 0, st
+    assert st["_flips"] <= CAP_FLIPS and st["_ties"] <= CAP_TIES, st
+
+
 def _check_step(oracle_mod, wl, dims, sd):
     import plagnn
 
@@ -116,25 +139,25 @@ def _check_step(oracle_mod, wl, dims, sd):
     eng.forward()
     eng.backward()
     torch.cuda.synchronize()
+    grads = {k: v.cpu() for k, v in eng.grads().items()}
     og = _oracle_graph(oracle_mod, wl)
     use_w = wl.edge_weight is not None
     signs = _engine_signs(eng)
     ref_logits, ref_loss, ref_grads = oracle_mod.train_step(og, x, labels, wl.train_index, wl.class_weight, sd,
                                                             use_weight=use_w, signs=signs)
-    print(f"decisions taken from the engine: activations {signs.get('_flips', 0)}, "
-          f"winners {signs.get('_ties', 0)}")
-    assert signs.get("_flips", 0) <= 64 and signs.get("_ties", 0) <= 1024, signs
+    _check_signs(signs)
     signs64 = {k: v for k, v in signs.items() if not k.startswith("_")}
     exact = _Yardstick(lambda: oracle_mod.train_step(og, x, labels, wl.train_index, wl.class_weight, sd,
                                                      use_weight=use_w, dtype=torch.float64, signs=signs64))
-    _close_judged(eng.logits(), ref_logits, lambda: exact.get()[0], name="logits")
+    fallback = int(_close_judged(eng.logits(), ref_logits, lambda: exact.get()[0], name="logits"))
     tl, vl = eng.losses()
     assert abs(tl - ref_loss.item()) <= 1e-4 * abs(ref_loss.item()), (tl, ref_loss.item())
     ref_val = oracle_mod.multi_loss(ref_logits[wl.val_index], labels[wl.val_index], wl.class_weight)
     assert abs(vl - ref_val.item()) <= 1e-4 * abs(ref_val.item()), (vl, ref_val.item())
-    grads = {k: v.cpu() for k, v in eng.grads().items()}
     for k, v in ref_grads.items():
-        _close_judged(grads[k], v, lambda k=k: exact.get()[2][k], name="grad " + k)
+        fallback += int(_close_judged(grads[k], v, lambda k=k: exact.get()[2][k], name="grad " + k))
+    print(f"tensors judged against float64: {fallback} of {len(ref_grads) + 1}")
+    assert fallback <= CAP_FALLBACK, fallback
     eng.adam()
     after = eng.state_dict()
     keys = list(sd)
@@ -162,7 +185,8 @@ def test_full_size_step_matches_oracle(oracle_mod, s0_cfg2, dims):
 
 
 def test_cfg3_edge_weighted_step_matches_oracle(oracle_mod):
-    """cfg3: S0 with ±3 % of its edges changed, ECC edge weights (u_mul_e max), hidden 512."""
+    """cfg3: GSE30931's PPI_inter of S0 (pg_perturb), ECC_inter edge weights (u_mul_e max),
+    hidden 512."""
     from plagnn import workload
 
     wl = workload.build("cfg3", device=DEV)
@@ -185,6 +209,19 @@ def test_cfg4_replica_graphs():
         key = np.sort(src * wl.n + dst)
         assert np.array_equal(key, np.sort(dst * wl.n + src)), "asymmetric"
         assert 0.005 < abs(len(src) - e0) / e0 < 0.2, (wl.variant, len(src), e0)
+
+
+@pytest.mark.parametrize("rank", [1, 2, 3], ids=["GSE30931", "GSE27182", "GSE74572"])
+def test_cfg4_replica_step_matches_oracle(oracle_mod, rank):
+    """cfg4 (BASELINE configs[3]; code/main_inter.py:57-61 loads <GSE>/PPI_inter.npz): one
+    TrainEngine step at the reference dims on each perturbation replica's own graph
+    against the oracle, with the same bars as the normal graph."""
+    from plagnn import workload
+
+    wl = workload.build("cfg4", rank=rank, device=DEV)
+    assert wl.variant == workload.CFG4_VARIANTS[rank]
+    sd = oracle_mod.init_params(wl.dims, seed=10 + rank)
+    _check_step(oracle_mod, wl, wl.dims, sd)
 
 
 class _RoundFwd(torch.autograd.Function):

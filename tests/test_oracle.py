@@ -242,23 +242,37 @@ def test_rowwise_loc_correction_equals_vectorised(oracle_mod):
 
 
 def test_decision_alignment(oracle_mod):
-    """spmm_max_align takes another computation's winner only when it is within tol of the
-    maximum; _act takes another computation's sign only at near-zero pre-activations."""
+    """spmm_max_align takes another computation's winner only when the two candidates lie
+    within BAND_ULPS x 2^-24 of their running-error scale; _act takes another
+    computation's sign only at pre-activations that small against their own scale. Both
+    count the differing decisions outside the band as hard."""
     src = np.array([1, 2, 3], np.int64)
     dst = np.array([0, 0, 0], np.int64)
     og = oracle_mod.OracleGraph(src, dst, 4, self_loop=False)
     X = np.array([[0.0, 0.0], [1.0, 5.0], [1.0 - 1e-7, 4.0], [0.5, 5.0]], np.float32)
+    S = np.abs(X).astype(np.float64)
+    band = 64 * oracle_mod.U32  # 3.8e-6 of the candidates' scale
     out, ax, ae = oracle_mod.spmm_max(og, X)
     assert ax[0].tolist() == [1, 1]
     hint = np.full((4, 2), -1, np.int32)
     hint[0] = [1, 1]  # positions: edge 1->0 is 0, 2->0 is 1, 3->0 is 2
-    n = oracle_mod.spmm_max_align(og, X, False, hint, 1e-7, out, ax, ae)  # band 1e-7 * max|out| = 5e-7
-    assert n == 1 and ax[0].tolist() == [2, 1] and out[0, 0] == np.float32(1.0 - 1e-7)
+    n, hard, _ = oracle_mod.spmm_max_align(og, X, False, hint, S, band, out, ax, ae)
+    assert (n, hard) == (1, 1) and ax[0].tolist() == [2, 1] and out[0, 0] == np.float32(1.0 - 1e-7)
     hint[0] = [2, 2]
-    n = oracle_mod.spmm_max_align(og, X, False, hint, 1e-7, out, ax, ae)
-    assert n == 1 and ax[0].tolist() == [2, 3]  # 0.5 is far from the max; the tie at 5.0 is taken
+    n, hard, _ = oracle_mod.spmm_max_align(og, X, False, hint, S, band, out, ax, ae)
+    assert (n, hard) == (1, 1) and ax[0].tolist() == [2, 3]  # 0.5 is far from the max; the tie at 5.0 is taken
+    # a candidate 1e-7 below a maximum of scale 1e-3 is NOT a rounding tie
+    X2 = X.copy()
+    X2[1, 0], X2[2, 0], X2[3, 0] = 1e-3, 1e-3 - 1e-7, 0.0
+    out, ax, ae = oracle_mod.spmm_max(og, X2)
+    hint[0] = [1, -1]
+    n, hard, _ = oracle_mod.spmm_max_align(og, X2, False, hint, np.abs(X2).astype(np.float64), band, out, ax, ae)
+    assert (n, hard) == (0, 1) and ax[0, 0] == 1
     pre = torch.tensor([1e-9, -1e-9, 1.0, -1.0])
     signs = {"s": torch.tensor([False, True, False, True])}
-    y = oracle_mod._act(pre, 0.01, "s", signs, 1e-5)
-    assert signs["_flips"] == 2
+    y = oracle_mod._act(pre, 0.01, "s", signs, torch.ones(4, dtype=torch.float64))
+    assert signs["_flips"] == 2 and signs["_hard_flips"] == 2
     torch.testing.assert_close(y, torch.tensor([1e-11, -1e-9, 1.0, -0.01]), rtol=1e-6, atol=0)
+    signs = {"s": torch.tensor([False, True, True, False])}
+    oracle_mod._act(pre, 0.01, "s", signs, torch.full((4,), 1e-6, dtype=torch.float64))  # 1e-9 is 0.017 ulp of 1e0,
+    assert signs["_flips"] == 0 and signs["_hard_flips"] == 2                          # 16.7 k ulp of 1e-6
