@@ -23,7 +23,8 @@ Multi-GPU (torch.distributed.run, one rank per GPU), --mode:
 
 At N = 1 the line also carries `sub_configs`: ref (the reference dims), cfg3 (hidden
 512, edge-weighted) and cfg5 (RMAT x16, bf16), each timed the same way in a child process
-started before this process touches the GPU.
+started before this process touches the GPU (as is the drop-in leg), so that every GEMM
+dispatch of this process belongs to the headline engine's steps.
 
 Beside the engine's number (`value`), rank 0 at N = 1 also reports
   * `dropin`: the unmodified reference loop on the dgl shim (plagnn.model + torch Adam,
@@ -61,12 +62,6 @@ ALPHA = 0.1               # main_normal.py -a default (code/main_normal.py:29)
 # MI355X_MICROARCH.md "Indexed rows": rows gathered from an XCD's L2 16.8-18.8 TB/s chip-wide
 # (a uniformly random 38 MB table from the Infinity Cache: 8.6 TB/s)
 L2_GATHER_GBS = 17800.0
-
-
-def _group(name: str, gemm_group: str = "gemm_f32") -> str:
-    if name.startswith("gemm"):
-        return gemm_group
-    return name.split(".")[0]
 
 
 def _cpu_model() -> str:
@@ -209,29 +204,32 @@ def epoch_with_eval_leg(engine, wl, dev, epochs: int = 20):
     return round((time.perf_counter() - t0) / epochs * 1e3, 4)
 
 
-def _roofline(engine, bd, gemm_group, bf16):
-    """Per-group time and the roofline of each group from a kernel breakdown (launches of
-    the replayed step graph, timed by event-record nodes: TrainEngine.kernel_breakdown)."""
+def _roofline(engine, gt, bf16):
+    """Roofline of each launch group from TrainEngine.group_times (the group's launches of
+    one step, replayed as a graph: the benchmark's own execution), with the algorithmic
+    work of SURVEY.md §8(d) at the true dims."""
+    L = engine.L
+    work = {"gemm": float(engine.flops_per_step()),
+            "spmm_max_fwd": float(sum(engine.spmm_bytes(l) for l in range(L))),
+            "spmm_max_bwd": float(sum(engine.spmm_bwd_bytes(l) for l in range(L))),
+            "adam": 16.0 * engine.flat.numel()}
+    gemm_group = "gemm_bf16" if bf16 else "gemm_f32"
     groups = {}
-    for name, r in bd.items():
-        if name.startswith("_"):
-            continue
-        gname = _group(name, gemm_group)
-        g = groups.setdefault(gname, {"ms": 0.0, "work": 0.0, "launches": 0.0})
-        g["ms"] += r["ms"]
-        g["work"] += r["work"]
-        g["launches"] += r["calls"]
+    for gname, r in gt.items():
+        name = gemm_group if gname == "gemm" else gname
+        groups[name] = {"ms": r["ms"], "launches": r["launches"], "work": work.get(gname, 0.0)}
 
     def roof(gname):
         g = groups[gname]
         sec = g["ms"] / 1e3
+        base = {"kernel": gname, "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4),
+                "us_per_launch": round(g["ms"] * 1e3 / g["launches"], 2)}
         if gname == gemm_group:
             # algorithmic flops at the true (unpadded) dims, not the padded launch shapes
-            ach = engine.flops_per_step() / sec / 1e12
-            r = {"kernel": gname, "bound": "mfma", "achieved": round(ach, 2), "unit": "TFLOP/s",
-                 "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4),
-                 "us_per_launch": round(g["ms"] * 1e3 / g["launches"], 2),
-                 "flops_per_step": engine.flops_per_step()}
+            ach = g["work"] / sec / 1e12
+            r = {"bound": "mfma", "achieved": round(ach, 2), "unit": "TFLOP/s", **base,
+                 "flops_per_step": int(g["work"]),
+                 "compulsory_bytes_per_launch": round(engine.gemm_bytes_per_step() / g["launches"])}
             if bf16:
                 r.update(peak=PEAK_BF16_TFLOPS, frac=round(ach / PEAK_BF16_TFLOPS, 4))
             else:
@@ -241,9 +239,8 @@ def _roofline(engine, bd, gemm_group, bf16):
                          peak_f32_mfma=PEAK_F32_TFLOPS, frac_vs_f32_mfma=round(ach / PEAK_F32_TFLOPS, 4))
             return r
         ach = g["work"] / sec / 1e9
-        r = {"kernel": gname, "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
-             "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-             "launches_per_step": g["launches"], "ms_per_step": round(g["ms"], 4)}
+        r = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+             "frac": round(ach / PEAK_HBM_GBS, 4), **base, "bytes_per_step": int(g["work"])}
         if gname == "spmm_max_fwd":
             # the per-edge gathers of a feature matrix that fits the 256 MiB Infinity Cache are
             # served by L2 / MALL, not HBM: also against the L2-served gather ceiling
@@ -254,15 +251,21 @@ def _roofline(engine, bd, gemm_group, bf16):
     return groups, roof
 
 
-def _traffic(config, group):
-    """HBM bytes per launch of `group` from the committed PMC pass (profiles/pmc_traffic.json,
-    scripts/pmc_round.sh), or None."""
+def _traffic(config, group, engine):
+    """HBM bytes per launch (per library call, as `achieved`) of `group` from the committed
+    PMC passes (profiles/pmc_traffic.json, scripts/pmc_traffic.sh: 2 FETCH_SIZE + WRITE_SIZE
+    per KERNEL dispatch), or None. A GEMM call is one kernel; a max-aggregation call is the
+    max kernel (+ the merge kernel when the graph has split rows), a max-backward call the
+    pack and pull kernels (+ the merge)."""
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(tfile):
         return None
     with open(tfile) as f:
-        tj = json.load(f)
-    return tj.get(config, {}).get(group)
+        b = json.load(f).get(config, {}).get(group)
+    if b is None:
+        return None
+    per_call = {"spmm_max_fwd": 1 + (engine.dg.fwd.n_merges > 0), "spmm_max_bwd": 2 + (engine.dg.bwd.n_merges > 0)}
+    return round(b * per_call.get(group, 1))
 
 
 def _job_of(rank, mode):
@@ -284,7 +287,6 @@ def run(args, rank, world, dev, dist, mode):
         raise SystemExit(f"--config {args.config}: TrainEngine runs SAGEConv 'pool' layers; {wl.conv} runs on the "
                          f"dgl shim (tests/test_gpu_graphconv.py)")
     Engine = plagnn.TrainEngineBF16 if bf16 else plagnn.TrainEngine
-    gemm_group = "gemm_bf16" if bf16 else "gemm_f32"
     engine = Engine(graph, torch.from_numpy(wl.ds.feat), torch.from_numpy(wl.ds.loc.astype(np.float32)),
                     dims, wl.class_weight, wl.train_index, wl.val_index, lr=5e-5, device=dev,
                     edge_weight=wl.edge_weight, seed=job)
@@ -357,19 +359,18 @@ def run(args, rank, world, dev, dist, mode):
     if rank != 0:
         return None
 
-    # per-kernel breakdown after the timed region, on rank 0 only (without the collective):
-    # the step captured with an event-record node around every launch, replayed
-    bd = engine.kernel_breakdown(args.breakdown_reps, graph=not args.eager)
-    method = bd.pop("_method")
-    if args.dump_breakdown:
+    # per-group times after the timed region, on rank 0 only (without the collective): each
+    # group's launches of one step captured as a graph and replayed back to back
+    gt = engine.group_times(reps=args.breakdown_reps)
+    if args.dump_breakdown:  # per launch site, eager steps (diagnostic)
         with open(args.dump_breakdown, "w") as f:
-            json.dump(bd, f, indent=1)
-    groups, roof = _roofline(engine, bd, gemm_group, bf16)
+            json.dump(engine.kernel_breakdown(5), f, indent=1)
+    groups, roof = _roofline(engine, gt, bf16)
     dom = max(groups, key=lambda k: groups[k]["ms"])
     rf = roof(dom)
-    rf["timing"] = {"graph": "launches of the replayed step graph, timed by event-record nodes around each launch",
-                    "eager+spin": "eager steps queued behind a GPU spin, events around each launch"}[method]
-    rf["traffic"] = _traffic(args.config, dom)
+    rf["timing"] = ("HIP events around back-to-back replays of a graph holding this group's launches of one step "
+                    "(the step's own buffers), per step")
+    rf["traffic"] = _traffic(args.config, dom, engine)
     if world > 1:
         par = (f"replicas{world}: independent (round, fold) trainings, no collective" if mode == "replicas" else
                f"dp{world}: shared model, one gradient all-reduce per step, "
@@ -379,6 +380,7 @@ def run(args, rank, world, dev, dist, mode):
     return {
         "metric": "edges aggregated/sec per training epoch, full PPI graph",
         "value": round(value, 1),
+        "pid": os.getpid(),
         "unit": "edges/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -403,22 +405,26 @@ def run(args, rank, world, dev, dist, mode):
     }
 
 
-def sub_configs(args):
-    """The other single-GPU configs, each in a child process of its own (started before this
-    process initialises the GPU), timed with the same steps / warm-up."""
+def _child(args, extra):
+    """Run this script in a child process (started before this process initialises the GPU,
+    so the GEMM dispatches of this process are the headline engine's alone); its JSON line."""
     import subprocess
 
+    cmd = [sys.executable, os.path.abspath(__file__), "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--no-cpu-baseline", "--no-legs", "--sub-configs", "", "--breakdown-reps", str(args.breakdown_reps)] + extra
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise SystemExit(f"child {extra} failed (rc {r.returncode}):\n{r.stderr[-3000:]}")
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def sub_configs(args):
+    """The other single-GPU configs, each in a child process of its own, timed with the same
+    steps / warm-up."""
     out = {}
     for name in [c for c in args.sub_configs.split(",") if c]:
-        cmd = [sys.executable, os.path.abspath(__file__), "--config", name, "--steps", str(args.steps), "--warmup",
-               str(args.warmup), "--no-cpu-baseline", "--no-legs", "--sub-configs", "",
-               "--breakdown-reps", str(args.breakdown_reps)]
         t0 = time.perf_counter()
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
-        if r.returncode != 0:
-            raise SystemExit(f"sub-config {name} failed (rc {r.returncode}):\n{r.stderr[-3000:]}")
-        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
-        res = json.loads(line)
+        res = _child(args, ["--config", name])
         keep = ("value", "unit", "ms_per_step", "step_distribution", "dtype", "config", "roofline", "spmm_roofline",
                 "kernels_ms_per_step", "loss")
         out[name] = {k: res[k] for k in keep}
@@ -443,8 +449,9 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no HIP graph (PMC counter passes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the drop-in and epoch-with-eval legs")
-    ap.add_argument("--breakdown-reps", type=int, default=5)
+    ap.add_argument("--breakdown-reps", type=int, default=5, help="replays of each launch-group timing graph")
     ap.add_argument("--dump-breakdown", default="", help="write the per-launch-site breakdown (JSON)")
+    ap.add_argument("--dropin-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -453,7 +460,14 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     mode = args.mode if args.mode != "auto" else ("dp" if args.config == "cfg4" else "replicas")
+    if args.dropin_only:
+        wl = W.build(args.config, device="cuda")
+        print(json.dumps(dropin_leg(wl, wl.dims, torch.device("cuda"), steps=min(args.steps, 20), warmup=3)))
+        return
     subs = sub_configs(args) if (world == 1 and args.sub_configs) else None
+    dropin = None
+    if world == 1 and not args.no_legs and not W.CONFIGS[args.config][2]:
+        dropin = _child(args, ["--config", args.config, "--dropin-only"])
     # one rank per GPU; more ranks than GPUs (a rehearsal of the N-rank flow on a smaller
     # box, with PLAGNN_BENCH_BACKEND=gloo) share them round-robin
     local_dev = local_rank % max(1, torch.cuda.device_count())
@@ -477,8 +491,8 @@ def main():
     legs = {}
     if world == 1 and not args.no_legs:
         legs["epoch_with_eval_ms"] = epoch_with_eval_leg(engine, wl, dev)
-        if not wl.bf16:
-            legs["dropin"] = dropin_leg(wl, wl.dims, dev, steps=min(args.steps, 20), warmup=3)
+        if dropin is not None:
+            legs["dropin"] = dropin
     out.update(legs)
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not args.config.startswith("cfg5"):

@@ -40,6 +40,12 @@ from .ops import LEAKY_SLOPE, round4
 RELU, LEAKY, NONE = _lib.PG_ACT_RELU, _lib.PG_ACT_LEAKY, _lib.PG_ACT_NONE
 
 
+def launch_group(site: str) -> str:
+    """Kernel group of a launch site name: every GEMM launch ('gemm.*') is 'gemm', the rest
+    their prefix ('spmm_max_fwd.l1' -> 'spmm_max_fwd')."""
+    return "gemm" if site.startswith("gemm") else site.split(".")[0]
+
+
 class _Flat:
     """Named views into one flat fp32 buffer (256-B aligned), plus named sub-views
     (row ranges / column prefixes) of those blocks."""
@@ -70,6 +76,10 @@ class _Flat:
 
 class TrainEngine:
     WIDTH_ALIGN = 4  # every padded width is a multiple of this
+    _cur = ""                      # launch site being issued (_t)
+    _filter: Optional[str] = None  # group_times: issue only this launch group
+    _issued = 0
+    _rec: Optional[list] = None    # gemm_bytes_per_step's dry-run record
 
     def __init__(self, graph: CSRGraph, features: torch.Tensor, labels: torch.Tensor,
                  dims: Sequence[int], class_weight, train_index, val_index=None,
@@ -285,85 +295,119 @@ class TrainEngine:
     # ------------------------------------------------------------------ timing
     @contextlib.contextmanager
     def _t(self, name: str, work: float = 0.0):
-        """HIP events around one launch on the engine's stream (diagnostic passes only).
-        While a step is being captured the events are external: they become event-record
-        nodes of the graph, so the timed launches are the graph's own."""
+        """Marks one launch site; in diagnostic passes, HIP events around it on the engine's
+        stream."""
+        self._cur = name
         if self._timing is None:
             yield
             return
         st = torch.cuda.current_stream(self.device)
-        ext = torch.cuda.is_current_stream_capturing()
-        a = torch.cuda.Event(enable_timing=True, external=ext)
-        b = torch.cuda.Event(enable_timing=True, external=ext)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
         a.record(st)
         yield
         b.record(st)
         self._timing.append((name, work, a, b))
 
-    def kernel_breakdown(self, reps: int = 5, graph: bool = True) -> Dict[str, Dict[str, float]]:
-        """Per-launch-site mean duration (ms) and work over `reps` steps, timed with HIP
-        events on the launch stream. Returns {name: {ms, work, calls}} per step, and the
-        method used under the key "_method". graph=True captures one step (forward,
-        backward, Adam) with an event-record node around every launch and replays it: the
-        launches are timed as the benchmark's replayed graph runs them. If the runtime
-        refuses timing events in a graph, eager steps are timed instead, each issued behind
-        a GPU spin (torch.cuda._sleep) so that the host has queued the whole step before
-        the GPU starts it (no host gaps inside the measured launches). A diagnostic of this
-        process alone: the steps run without the gradient all-reduce. Each timed step is a
-        real training step."""
-        acc: Dict[str, List[float]] = defaultdict(lambda: [0.0, 0.0, 0])
+    def _call(self, fn: str, *args) -> None:
+        """One library launch of the step (skipped when group_times captures another group)."""
+        if self._filter is not None and launch_group(self._cur) != self._filter:
+            return
+        self._issued += 1
+        call(fn, *args)
 
-        def collect(timing):
-            for name, work, a, b in timing:
+    def group_times(self, groups=("gemm", "spmm_max_fwd", "spmm_max_bwd", "head", "adam"), reps: int = 20,
+                    warm: int = 2, copies: int = 10) -> Dict[str, Dict[str, float]]:
+        """Time each launch group of the step AS THE REPLAYED GRAPH RUNS IT: for group g,
+        `copies` steps are captured into one graph with only g's launches (in step order, on
+        the step's own buffers), and that graph is replayed `reps` times back to back
+        between two HIP events on the replay stream (no events sit between the launches; the
+        graph launch overhead is spread over copies x launches). Returns {g: {ms (per
+        step), launches (per step)}}. Replays of the Adam group train the model; the
+        others recompute the step's buffers from their current inputs."""
+        out = {}
+        cur = torch.cuda.current_stream(self.device)
+        s = torch.cuda.Stream(self.device)
+        for gname in groups:
+            s.wait_stream(cur)
+            self._filter, self._issued = gname, 0
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(copies):
+                        self.forward()
+                        self.backward()
+                        self.adam()
+            finally:
+                self._filter = None
+            launches = self._issued // copies
+            if launches == 0:
+                continue
+            for _ in range(warm):
+                g.replay()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(reps):
+                g.replay()
+            b.record()
+            torch.cuda.synchronize(self.device)
+            out[gname] = {"ms": a.elapsed_time(b) / (reps * copies), "launches": launches}
+            del g
+        return out
+
+    def kernel_breakdown(self, reps: int = 5) -> Dict[str, Dict[str, float]]:
+        """Per-launch-site mean duration (ms) and work over `reps` eager steps, timed with
+        HIP events on the launch stream; each step is issued behind a GPU spin
+        (torch.cuda._sleep) so that the host has queued the whole step before the GPU starts
+        it. Returns {name: {ms, work, calls}} per step. A diagnostic of this process alone
+        (no gradient all-reduce); the event packets between launches add a few us to each
+        (group_times measures the replayed graph). Each timed step is a real training step."""
+        acc: Dict[str, List[float]] = defaultdict(lambda: [0.0, 0.0, 0])
+        for _ in range(reps):
+            self._timing = []
+            torch.cuda._sleep(20_000_000)
+            self.step_eager(None)
+            torch.cuda.synchronize(self.device)
+            for name, work, a, b in self._timing:
                 r = acc[name]
                 r[0] += a.elapsed_time(b)
                 r[1] += work
                 r[2] += 1
-
-        method = "eager+spin"
-        if graph:
-            try:
-                self._timing = []
-                g = torch.cuda.CUDAGraph()
-                s = torch.cuda.Stream(self.device)
-                s.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.graph(g, stream=s):
-                    self.forward()
-                    self.backward()
-                    self.adam()
-                timing, self._timing = self._timing, None
-                for _ in range(reps):
-                    g.replay()
-                    torch.cuda.synchronize(self.device)
-                    collect(timing)
-                    self.steps_done += 1
-                method = "graph"
-                del g
-            except Exception:  # noqa: BLE001 - timing nodes unsupported: time eager steps
-                self._timing = None
-                acc.clear()
-                torch.cuda.synchronize(self.device)
-        if method != "graph":
-            for _ in range(reps):
-                self._timing = []
-                torch.cuda._sleep(20_000_000)
-                self.step_eager(None)
-                torch.cuda.synchronize(self.device)
-                collect(self._timing)
-                self._timing = None
-        out = {k: {"ms": v[0] / reps, "work": v[1] / reps, "calls": v[2] / reps} for k, v in acc.items()}
-        out["_method"] = method
-        return out
+            self._timing = None
+        return {k: {"ms": v[0] / reps, "work": v[1] / reps, "calls": v[2] / reps} for k, v in acc.items()}
 
     # ------------------------------------------------------------------ kernels
     def _s(self):
         return _lib.stream_handle(self.device)
+
+    def _rec_gemm(self, A, B, C, M, N, K, beta, dact) -> None:
+        """gemm_bytes_per_step's dry run: the product's compulsory bytes (A, B read once, C
+        written once, + C read for beta != 0, + the activation operand of a fused act')."""
+        if self._rec is not None:
+            b = A.element_size() * M * K + B.element_size() * K * N + C.element_size() * M * N
+            b += (C.element_size() * M * N if beta != 0.0 else 0) + (dact.element_size() * M * N if dact is not None else 0)
+            self._rec.append(b)
+
+    def gemm_bytes_per_step(self) -> int:
+        """Compulsory HBM bytes of the step's GEMM launches (each operand read once, each
+        output written once, padded shapes), from a dry run that launches nothing."""
+        self._rec, self._filter = [], "__dry_run__"
+        jobs = list(getattr(self, "_jobs", []))
+        try:
+            self.forward()
+            self.backward()
+        finally:
+            out, self._rec, self._filter = sum(self._rec), None, None
+            if hasattr(self, "_jobs"):
+                self._jobs = jobs
+        return int(out)
 
     def _gemm(self, A, B, C, transa=False, transb=False, beta=0.0, bias=None, act=NONE, dact=None,
               rowsum=None, tag="gemm"):
         M = A.shape[1] if transa else A.shape[0]
         K = A.shape[0] if transa else A.shape[1]
         N = B.shape[0] if transb else B.shape[1]
+        self._rec_gemm(A, B, C, M, N, K, beta, dact)
         sk = self._gemm_plans.get((M, N, K), 1) if (bias is None and act == NONE and dact is None) else 1
         if sk > 1:
             self._gemm_partials(A, B, C, transa, transb, beta, rowsum, tag, M, N, K, sk)
@@ -371,7 +415,7 @@ class TrainEngine:
         ep = _lib.epilogue(bias, act, LEAKY_SLOPE, dact, rowsum)
         ws = self.ws
         with self._t(tag, 2.0 * M * N * K):
-            call("pg_gemm_f32", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
+            self._call("pg_gemm_f32", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
                  B.stride(0), beta, ptr(C), C.stride(0), ep, sk, ptr(ws), ws.numel(), self._s())
 
     def _gemm_partials(self, A, B, C, transa, transb, beta, rowsum, tag, M, N, K, sk) -> None:
@@ -386,7 +430,7 @@ class TrainEngine:
         used = ctypes.c_int(0)
         ep = _lib.epilogue(rowsum=rowsum)
         with self._t(tag, 2.0 * M * N * K):
-            call("pg_gemm_f32_partials", int(transa), int(transb), M, N, K, ptr(A), A.stride(0), ptr(B),
+            self._call("pg_gemm_f32_partials", int(transa), int(transb), M, N, K, ptr(A), A.stride(0), ptr(B),
                  B.stride(0), ep, sk, ptr(slab), slab.numel(), ctypes.byref(used), self._s())
         j = _lib.PgSplitkJob()
         j.ws, j.split_k, j.M, j.N = ptr(slab), used.value, M, N
@@ -399,7 +443,7 @@ class TrainEngine:
             part = jobs[i:i + 16]
             arr = (_lib.PgSplitkJob * len(part))(*part)
             with self._t("gemm.splitk_reduce"):
-                call("pg_gemm_splitk_reduce_batch", arr, len(part), self._s())
+                self._call("pg_gemm_splitk_reduce_batch", arr, len(part), self._s())
 
     def forward(self) -> None:
         """Logits (self.prob) and both losses; dZ = d train_loss / d z."""
@@ -415,7 +459,7 @@ class TrainEngine:
                        tag=f"gemm.fwd.pool.l{l + 1}")
             # M = max-aggregate(P) -> right half of HM
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
-                call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
+                self._call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
                      ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
             # Y = [H | M] Wcat^T + b (fc_self + fc_neigh + bias), leaky_relu -> next input
             Fo = pd[l + 1]
@@ -432,7 +476,7 @@ class TrainEngine:
         P, pd, C = self.P, self.pd, self.C
         cp = pd[-1]
         with self._t("head"):
-            call("pg_mlp_head", ptr(A4), A4.stride(0), self.N, pd[-2], a_dtype, ptr(P["liner2.W"]), pd[-2],
+            self._call("pg_mlp_head", ptr(A4), A4.stride(0), self.N, pd[-2], a_dtype, ptr(P["liner2.W"]), pd[-2],
                  ptr(P["liner2.b"]), C, ptr(self.labels), cp, ptr(self.cw), ptr(self.row_set), self.n_train,
                  self.n_val, ptr(self.prob), cp, ptr(dZ), cp, ptr(dZb), ptr(dA4), dA4.stride(0), LEAKY_SLOPE,
                  ptr(self.loss), ptr(self.ws), self.ws_bytes, self._s())
@@ -460,7 +504,7 @@ class TrainEngine:
             self._gemm(dY, P[p + "Wcat"][:, Fi:], self.dM[l], tag=f"gemm.dgrad.neigh.l{l + 1}")
             # max backward with relu' of fc_pool fused; zero maxima (M = 0) are skipped
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.dM[l]), Fi, Fi,
+                self._call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.dM[l]), Fi, Fi,
                      ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(dP), DYP.stride(0), ptr(self.ws),
                      self.ws_bytes, st)
             # d Wpool = dP^T H, d bpool = sum_nodes dP
@@ -476,8 +520,8 @@ class TrainEngine:
     def adam(self) -> None:
         st = self._s()
         with self._t("adam", 16.0 * self.flat.numel()):
-            call("pg_adam_prepare", ptr(self.adam_state), self.lr, self.betas[0], self.betas[1], st)
-            call("pg_adam_apply", ptr(self.flat), ptr(self.gflat), ptr(self.m), ptr(self.v),
+            self._call("pg_adam_prepare", ptr(self.adam_state), self.lr, self.betas[0], self.betas[1], st)
+            self._call("pg_adam_apply", ptr(self.flat), ptr(self.gflat), ptr(self.m), ptr(self.v),
                  self.flat.numel(), ptr(self.adam_state), self.betas[0], self.betas[1], self.eps, 0.0, st)
 
     def step_eager(self, allreduce=None) -> None:

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from ._lib import call, ptr
+from ._lib import ptr
 from .engine import LEAKY, NONE, RELU, TrainEngine, _Flat
 
 BF16, F32 = _lib.PG_DTYPE_BF16, _lib.PG_DTYPE_F32
@@ -94,7 +94,7 @@ class TrainEngineBF16(TrainEngine):
         self._cast_weights()
 
     def _cast_weights(self) -> None:
-        call("pg_cast_f32_bf16", ptr(self.flat), ptr(self.wb_map), self.wb.numel(), ptr(self.wb), self._s())
+        self._call("pg_cast_f32_bf16", ptr(self.flat), ptr(self.wb_map), self.wb.numel(), ptr(self.wb), self._s())
 
     def load_state_dict(self, sd) -> None:
         super().load_state_dict(sd)
@@ -129,13 +129,14 @@ class TrainEngineBF16(TrainEngine):
         M = A.shape[1] if transa else A.shape[0]
         K = A.shape[0] if transa else A.shape[1]
         N = B.shape[0] if transb else B.shape[1]
+        self._rec_gemm(A, B, C, M, N, K, beta, dact)
         obf = C.dtype == torch.bfloat16
         sk = 1
         if not obf and bias is None and act == NONE and dact is None:
             sk = self._gemm_plans.get((M, N, K), 1)
         ep = _lib.epilogue(bias, act, LEAKY_SLOPE, dact, rowsum)
         with self._t(tag, 2.0 * M * N * K):
-            call("pg_gemm_bf16", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
+            self._call("pg_gemm_bf16", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
                  B.stride(0), beta, ptr(C), C.stride(0), BF16 if obf else F32, ep, sk, ptr(self.ws),
                  self.ws.numel(), self._s())
 
@@ -150,7 +151,7 @@ class TrainEngineBF16(TrainEngine):
             self._gemm(HM[:, :Fi], W[p + "Wpool"], self.Pl[l], transb=True, bias=P[p + "bpool"], act=RELU,
                        tag=f"gemm.fwd.pool.l{l + 1}")
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
-                call("pg_spmm_max_fwd_bf16", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
+                self._call("pg_spmm_max_fwd_bf16", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
                      ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
             Fo = pd[l + 1]
             out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
@@ -181,7 +182,7 @@ class TrainEngineBF16(TrainEngine):
             # dM = dY Wneigh   (Wneigh = the right half of Wcat, read as a [Fo][Fi] k image)
             self._gemm(dY, W[p + "Wcat"][:, Fi:], self.dM[l], tag=f"gemm.dgrad.neigh.l{l + 1}")
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                call("pg_spmm_max_bwd_bf16", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.dM[l]),
+                self._call("pg_spmm_max_bwd_bf16", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.dM[l]),
                      Fi, Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(dP), DYP.stride(0),
                      ptr(self.ws), self.ws_bytes, st)
             self._gemm(dP, HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],

@@ -1,72 +1,60 @@
 """Build profiles/pmc_traffic.json from rocprofv3 --pmc passes over bench.py
-(scripts/pmc_round.sh): HBM-side bytes per engine launch for each kernel group, with the
-gfx950 corrections of MI355X_MICROARCH.md (FETCH_SIZE counts half of a wide coalesced
-read: x2; WRITE_SIZE exact; both in KB). Infinity-Cache hits are counted by these
-counters (they are L2-miss / fabric requests), so for tables that fit the 256 MiB MALL
-this is fabric traffic, an upper bound on true HBM bytes.
+(scripts/pmc_traffic.sh): HBM-side bytes per launch of each kernel group, with the gfx950
+corrections of MI355X_MICROARCH.md "HBM" (FETCH_SIZE counts half of a wide coalesced read:
+x2; WRITE_SIZE exact; both in KB): bytes = 2 FETCH_SIZE + WRITE_SIZE, summed over every
+dispatch of the group in the headline process and divided by its dispatch count: per
+launch, like bench.py's roofline "achieved". Infinity-Cache hits are counted by these
+counters (L2 memory-side requests), so for tables that fit the 256 MiB MALL this is fabric
+traffic, an upper bound on true HBM bytes. Groups: scripts/prof_groups.py's.
 
-Usage: python scripts/make_traffic.py gpurun_out/pmc cfg2 [--launches gemm_f32=23,...]
+Usage: python scripts/make_traffic.py <pmc root> <config> [--gemm-group gemm_bf16]
 """
 import argparse
 import csv
 import glob
 import json
 import os
+import sys
 from collections import defaultdict
 
-GROUPS = {
-    "gemm_f32_kernel": "gemm_f32", "gemm_dma_kernel": "gemm_f32", "splitk_reduce_kernel": "gemm_f32",
-    "splitk_reduce_batch_kernel": "gemm_f32",
-    "gemm_bf16_kernel": "gemm_f32", "head_kernel": "head", "head_final_kernel": "head",
-    "max_fwd_kernel": "spmm_max_fwd", "max_merge_kernel": "spmm_max_fwd",
-    "group_pack_kernel": "spmm_max_bwd", "max_bwd_pull_kernel": "spmm_max_bwd",
-    "max_bwd_kernel": "spmm_max_bwd", "sum_merge_kernel": "spmm_max_bwd",
-    "multi_loss_kernel": "loss", "multi_loss_final_kernel": "loss", "sigmoid_zero_kernel": "loss",
-    "adam_apply_kernel": "adam", "adam_prepare_kernel": "adam",
-}
-
-
-def group_of(name):
-    n = name.replace("(anonymous namespace)::", "").replace("pg_gemm::", "").replace("void ", "")
-    return GROUPS.get(n.split("(")[0].split("<")[0].strip())
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from prof_groups import group_of  # noqa: E402
 
 
 def collect(root, counter):
-    per_group = defaultdict(float)
-    steps = 0
+    """{group: [bytes, dispatches]} of the process with the most dispatches of `counter`."""
+    per_file = []
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        acc = defaultdict(lambda: [0.0, 0])
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 if r["Counter_Name"] != counter:
                     continue
-                g = group_of(r["Kernel_Name"])
-                if "adam_apply_kernel" in r["Kernel_Name"]:
-                    steps += 1
-                if g:
-                    per_group[g] += float(r["Counter_Value"])
-    return per_group, steps
+                a = acc[group_of(r["Kernel_Name"])]
+                a[0] += float(r["Counter_Value"]) * 1024.0
+                a[1] += 1
+        per_file.append(acc)
+    return max(per_file, key=lambda a: sum(v[1] for v in a.values())) if per_file else {}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("config")
-    ap.add_argument("--launches", default="", help="overrides of the per-step launch counts, e.g. gemm_f32=22")
     ap.add_argument("--gemm-group", default="gemm_f32", help="name of the GEMM group (gemm_bf16 for cfg5)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
-    launches = {"gemm_f32": 22.0, "spmm_max_fwd": 3.0, "spmm_max_bwd": 3.0, "head": 1.0, "adam": 1.0}
-    launches.update({k: float(v) for k, v in (kv.split("=") for kv in a.launches.split(",") if kv)})
-    fetch, s1 = collect(a.root, "FETCH_SIZE")
-    write, s2 = collect(a.root, "WRITE_SIZE")
+    fetch = collect(os.path.join(a.root, "fetch"), "FETCH_SIZE")
+    write = collect(os.path.join(a.root, "write"), "WRITE_SIZE")
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     cfg = {}
     for g in sorted(set(fetch) | set(write)):
-        per_step = (2 * fetch.get(g, 0.0) / max(s1, 1) + write.get(g, 0.0) / max(s2, 1)) * 1024
-        cfg[g] = per_step / launches.get(g, 1.0)
-    if a.gemm_group != "gemm_f32" and "gemm_f32" in cfg:
-        cfg[a.gemm_group] = cfg.pop("gemm_f32")
+        if g == "other":
+            continue
+        f = fetch.get(g, [0.0, 1])
+        w = write.get(g, [0.0, 1])
+        cfg[a.gemm_group if g == "gemm" else g] = 2.0 * f[0] / max(f[1], 1) + w[0] / max(w[1], 1)
     out[a.config] = cfg
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)

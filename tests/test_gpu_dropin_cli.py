@@ -1,0 +1,100 @@
+"""The drop-in path against the reference's own composition (tests/golden/dropin_cli.npz,
+made by tests/golden/gen_dropin.py from the UNMODIFIED code/main_normal.py run with -d cpu
+on this repository's dgl package).
+
+`replay` restates what main_normal.py + train.train() do up to the losses and logits
+(code/main_normal.py:11-16, 57-67; code/utils.py:28-51; code/train.py:141-207, 289):
+seed 70, the graph and features of create_graph, the KFold rounds and folds, a fresh
+GNN32(503, 400, 300, 200, 100, 12) and Adam(lr 5e-5) per fold, the epoch body, multi_loss
+on the train and val rows. The evaluation and logging of train.py:210-357 do not feed
+back into training and are left out.
+
+Bars (the same on both devices; the CPU run reproduces the fixture bit for bit on the
+machine that made it, and to float32 rounding elsewhere):
+* every epoch's train / val loss of all 10 rounds x 2 folds within 1e-4 relative
+  (north_star);
+* the first epoch's logits (the forward at the initial parameters) within 1e-5;
+* the final logits (the forward after two Adam steps) within 1e-3 at the worst entry and
+  2e-5 on average: Adam's first steps move every parameter by about lr = 5e-5 whatever the
+  size of its gradient, so a parameter whose gradient is at rounding level moves by up to
+  2 lr in different directions on two devices, and the logits follow.
+* CPU (`-m "not gpu"`): the harness is the reference's composition.
+* GPU: the same replay with -d cuda (the shim's HIP layers).
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "dropin_cli.npz")
+
+
+def replay(dev: str):
+    import dgl
+    from plagnn import data
+    from plagnn.model import GNN32
+    from plagnn.train import FOLD_SEEDS, fold_splits, multi_loss, weight_cal
+
+    fx = np.load(FIX)
+    n, epochs, folds = int(fx["n"]), int(fx["epochs"]), int(fx["folds"])
+    seed = int(fx["seed"])
+    random.seed(seed)  # code/main_normal.py:11-16
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    ds = data.make_dataset("s0", n=n, mean_deg=float(fx["mean_deg"]), seed=seed)
+    # create_graph (code/utils.py:41-49) and g.to(device) (main_normal.py:66)
+    g = dgl.add_self_loop(dgl.graph((list(ds.row), list(ds.col)), num_nodes=n)).to(dev)
+    features = torch.tensor(np.hstack((ds.expr, np.hstack((ds.gcn, ds.ecc)))), dtype=torch.float).to(dev)
+    labels = torch.from_numpy(ds.loc.astype(np.float32)).to(dev)
+    i_weight = weight_cal(ds.loc)
+    label = [int(i) for i in ds.labelled]
+    tl = np.zeros((10, folds, epochs))
+    vl = np.zeros((10, folds, epochs))
+    logits_at, logits0_at = {}, {}
+    want = {tuple(int(v) for v in p) for p in fx["logits_at"]}
+    for rnd, fseed in enumerate(FOLD_SEEDS, start=1):
+        for fold, (train_index, val_index) in enumerate(fold_splits(label, folds, fseed), start=1):
+            model = GNN32(features.shape[1], 400, 300, 200, 100, 12).to(dev)
+            optimizer = torch.optim.Adam(model.parameters(), lr=5e-5)
+            for e in range(epochs):
+                optimizer.zero_grad()
+                model.train()
+                logits = model(g, features)
+                if e == 0 and (rnd, fold) in want:
+                    logits0_at[(rnd, fold)] = logits.detach().float().cpu().numpy()
+                train_loss = multi_loss(logits[train_index], labels[train_index], i_weight)
+                train_loss.backward()
+                optimizer.step()
+                model.eval()
+                val_loss = multi_loss(logits[val_index], labels[val_index], i_weight)
+                tl[rnd - 1, fold - 1, e] = train_loss.item()
+                vl[rnd - 1, fold - 1, e] = val_loss.item()
+            if (rnd, fold) in want:
+                logits_at[(rnd, fold)] = logits.detach().float().cpu().numpy()
+    return fx, tl, vl, logits_at, logits0_at
+
+
+def _check(dev):
+    fx, tl, vl, logits_at, logits0_at = replay(dev)
+    rel = lambda a, b: float(np.max(np.abs(a - b) / np.abs(b)))  # noqa: E731
+    print(f"{dev}: train loss rel {rel(tl, fx['train_loss']):.2e}, val loss rel {rel(vl, fx['val_loss']):.2e}")
+    assert rel(tl, fx["train_loss"]) <= 1e-4 and rel(vl, fx["val_loss"]) <= 1e-4
+    for (rnd, fold), got in logits0_at.items():
+        err = float(np.abs(got - fx[f"logits0_{rnd}_{fold}"]).max())
+        print(f"  first-epoch logits round {rnd} fold {fold}: max abs err {err:.2e}")
+        assert err <= 1e-5, (rnd, fold, err)
+    for (rnd, fold), got in logits_at.items():
+        d = np.abs(got - fx[f"logits_{rnd}_{fold}"])
+        print(f"  final logits round {rnd} fold {fold}: max abs err {d.max():.2e}, mean {d.mean():.2e}")
+        assert d.max() <= 1e-3 and d.mean() <= 2e-5, (rnd, fold, d.max(), d.mean())
+
+
+def test_cpu_replay_reproduces_reference_cli():
+    _check("cpu")
+
+
+@pytest.mark.gpu
+def test_gpu_dropin_matches_reference_cli():
+    _check("cuda")
