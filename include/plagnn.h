@@ -160,11 +160,14 @@ int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, f
 /* Deterministic backward (gather over the transposed CSR gt of g; gt->epos required):
  *   dx[u,f] = sum_{(v,j) in gt row u, ascending v} [argpos[v,f] == j - g.ptr[v]] * ew[j] * dout[v,f]
  * then, if mask_src != NULL, dx[u,f] *= (mask_src[u,f] > 0)  (relu' of fc_pool).
- * fwd_out (optional, needs mask_src = the forward's input X): the forward's output. An
- * entry (v, f) with fwd_out[v,f] == 0 is skipped: its winner u has X[u,f] * w == 0, so it
- * is either masked (X[u,f] = 0) or weighted 0 — the result is unchanged, and the dead
- * features whose ties all sit at position 0 no longer crowd one list. (A +-inf maximum,
- * stored as 0, is skipped too.)
+ * fwd_out (optional, needs mask_src = the forward's input X, a relu output: X >= 0): the
+ * forward's output. An entry (v, f) with fwd_out[v,f] == 0 is skipped: its winner u has
+ * X[u,f] * w == 0, so it is either masked (X[u,f] = 0) or weighted 0 — the result is
+ * unchanged, and the dead features whose ties all sit at position 0 no longer crowd one
+ * list. (A +-inf maximum, stored as 0, is skipped too.) Every entry left has
+ * X[u,f] * w != 0, hence X[u,f] > 0: the mask is implied and mask_src is not read (an
+ * element no entry reaches is +0 either way). With X < 0 somewhere the result is
+ * undefined; pass fwd_out = NULL for such inputs.
  * Every dx element is written (no zero-fill needed). */
 size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F);
 int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
@@ -419,7 +422,8 @@ int pg_perturb_fill(const double* xc_normal, const double* xc_inter, const doubl
 /* ---------------- misc ---------------- */
 const char* pg_last_error_string(void);
 int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-kernel split-K
-                         (epilogue without splitk_cnt), no grouped SpMM pair */
+                         (epilogue without splitk_cnt), no grouped SpMM pair; 6: with fwd_out,
+                         pg_spmm_max_bwd[_bf16] takes mask_src >= 0 and does not read it */
 
 #ifdef __cplusplus
 }

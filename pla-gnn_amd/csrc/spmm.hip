@@ -417,6 +417,12 @@ constexpr int kGroupMaxF = 1024;
 #ifndef PG_BWD_DIRECT
 #define PG_BWD_DIRECT 0
 #endif
+struct GPack {
+  uint16_t* __restrict__ f16;  // features, grouped by winning position
+  float* __restrict__ val;     // their upstream gradients
+  __device__ __forceinline__ void put(int64_t pos, int f, float d) const { f16[pos] = (uint16_t)f; val[pos] = d; }
+  __device__ __forceinline__ void get(int64_t pos, int& f, float& d) const { f = f16[pos]; d = val[pos]; }
+};
 
 __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   const int per = (n + kBlock - 1) / kBlock;
@@ -451,8 +457,7 @@ template <typename A, typename T>
 __device__ __forceinline__ void pack_short_row(
     int v, int wave, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, uint16_t* __restrict__ gfeat, int2* __restrict__ glist,
-    float* __restrict__ dpack, int* __restrict__ lds) {
+    const T* __restrict__ fout, int64_t ldf, GPack gp, int2* __restrict__ glist, int* __restrict__ lds) {
   constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
   const int lane = lane_id();
   // every independent load first: the row bounds, the argmax record and the upstream
@@ -525,8 +530,7 @@ __device__ __forceinline__ void pack_short_row(
   for (int i = 0; i < MAXW; ++i)
     if (a[i] != arg_none<A>()) {
       const int pos = vF + atomicAdd(&hist[a[i]], 1);
-      gfeat[pos] = (uint16_t)(lane + i * kWave);
-      dpack[pos] = d[i];
+      gp.put(pos, lane + i * kWave, d[i]);
     }
 }
 
@@ -544,8 +548,7 @@ template <int NV, typename A, typename T>
 __device__ __forceinline__ void pack_short_row_v(
     int v, int wave, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, uint16_t* __restrict__ gfeat, int2* __restrict__ glist,
-    float* __restrict__ dpack, int* __restrict__ lds) {
+    const T* __restrict__ fout, int64_t ldf, GPack gp, int2* __restrict__ glist, int* __restrict__ lds) {
   const int lane = lane_id();
   const int rs = ptr[v];
   const int deg = ptr[v + 1] - rs;
@@ -625,8 +628,7 @@ __device__ __forceinline__ void pack_short_row_v(
   wave_lds_sync();
   const int total = __builtin_amdgcn_readlane(x, kWave - 1);
   for (int i = lane; i < total; i += kWave) {
-    gfeat[vF + i] = lf[i];
-    dpack[vF + i] = lv[i];
+    gp.put(vF + i, lf[i], lv[i]);
   }
 }
 
@@ -634,8 +636,7 @@ template <typename A, typename T>
 __device__ __forceinline__ void pack_long_row(
     int v, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, uint16_t* __restrict__ gfeat, int2* __restrict__ glist,
-    float* __restrict__ dpack, int* __restrict__ lds) {
+    const T* __restrict__ fout, int64_t ldf, GPack gp, int2* __restrict__ glist, int* __restrict__ lds) {
   int* hist = lds;
   uint16_t* feats = reinterpret_cast<uint16_t*>(lds + kHistMax + 8);
   int* wsum = lds + kHistMax + 8 + kGroupMaxF / 2;
@@ -696,8 +697,7 @@ __device__ __forceinline__ void pack_long_row(
     for (int i = 0; i < FPT; ++i)
       if (a[i] != arg_none<A>()) {
         const int64_t pos = vF + atomicAdd(&hist[a[i]], 1);
-        gfeat[pos] = (uint16_t)(threadIdx.x + i * kBlock);
-        dpack[pos] = d[i];
+        gp.put(pos, threadIdx.x + i * kBlock, d[i]);
       }
     return;
   } else {
@@ -751,8 +751,7 @@ __device__ __forceinline__ void pack_long_row(
   const T* dr = dout + (int64_t)v * ldd;
   for (int i = threadIdx.x; i < total; i += kBlock) {
     const int f = feats[i];
-    gfeat[vF + i] = (uint16_t)f;
-    dpack[vF + i] = to_f(dr[f]);
+    gp.put(vF + i, f, to_f(dr[f]));
   }
 }
 
@@ -768,24 +767,22 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
     const int32_t* __restrict__ einv, const A* __restrict__ arg, int64_t lda, int F,
     const T* __restrict__ dout, int64_t ldd, const T* __restrict__ fout, int64_t ldf,
-    uint16_t* __restrict__ gfeat,
-    int2* __restrict__ glist, float* __restrict__ dpack) {
+    GPack gp, int2* __restrict__ glist) {
   constexpr int kLds = NV > 0 && kWavesPerBlock * pack_wave_ints<NV>() > kPackLds
                            ? kWavesPerBlock * pack_wave_ints<NV>() : kPackLds;
   __shared__ __attribute__((aligned(16))) int lds[kLds];
   const int b = blockIdx.x;
   if (b < n_long) {
-    pack_long_row<A, T>(rows ? rows[b].x : b, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gfeat, glist,
-                        dpack, lds);
+    pack_long_row<A, T>(rows ? rows[b].x : b, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gp, glist, lds);
   } else {
     const int wave = wave_id_uniform();
     const int v = (b - n_long) * kWavesPerBlock + wave;
     if (v < n_rows)
     {
       if constexpr (NV > 0)
-        pack_short_row_v<NV, A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gfeat, glist, dpack, lds);
+        pack_short_row_v<NV, A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gp, glist, lds);
       else
-        pack_short_row<A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gfeat, glist, dpack, lds);
+        pack_short_row<A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gp, glist, lds);
     }
   }
 }
@@ -800,7 +797,7 @@ template <bool HAS_W, typename T = float>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const float* __restrict__ ew, const int32_t* __restrict__ tslot,
     const int4* __restrict__ items, int n_items, const int2* __restrict__ glist,
-    const uint16_t* __restrict__ gfeat, const float* __restrict__ dpack, int F,
+    GPack gp, int F,
     const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx,
     float* __restrict__ ws, int64_t ldw) {
 #ifndef PG_PULL_U
@@ -855,8 +852,9 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
         ie[u] = i;
         ne[u] = n;
         const bool on = lane < n;
-        fe[u] = on ? (int)gfeat[base + lane] : 0;
-        de[u] = on ? dpack[base + lane] : 0.f;
+        fe[u] = 0;
+        de[u] = 0.f;
+        if (on) gp.get(base + lane, fe[u], de[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1298,8 +1296,8 @@ int pg_spmm_max_fwd_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t 
                                  arg_kind, ws, ws_bytes, stream);
 }
 
-// [split-row partials][grouped path: gfeat N x F u16 | glist nnz x int2 | dpack N x F f32 |
-//  einv nnz x int32 (used when g->einv is NULL)]
+// [split-row partials][grouped path: list features N x F u16 | list values N x F f32 |
+//  glist nnz x int2 | einv nnz x int32 (used when g->einv is NULL)]
 static size_t bwd_partials_bytes(const pg_csr_t* gt, int64_t F) {
   return gt->n_slots > 0 ? round_up(gt->n_slots * ws_ld(F) * 4, 256) : 0;
 }
@@ -1309,7 +1307,7 @@ size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
   size_t b = bwd_partials_bytes(gt, F);
   if (F <= kGroupMaxF) {
     const int64_t N = gt->n_cols;
-    b += round_up(N * F * 2, 256) + round_up(gt->nnz * 8, 256) + round_up(N * F * 4, 256) +
+    b += round_up(N * F * 2, 256) + round_up(N * F * 4, 256) + round_up(gt->nnz * 8, 256) +
          round_up(gt->nnz * 4, 256);
   }
   return b;
@@ -1347,14 +1345,15 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
   // PG_BWD_DIRECT (variant builds): always the argmax-record gather over the transposed CSR
   if (arg_kind == PG_ARG_U16 && F <= kGroupMaxF && N * F < INT32_MAX && !PG_BWD_DIRECT) {
     char* p = (char*)ws + pbytes;
-    uint16_t* gfeat = (uint16_t*)p;
+    // the lists carry the upstream gradient as f32 even for bf16 storage: 2-B scattered
+    // placement stores measured 30 % slower for the whole backward (RMWs on partial lines)
+    GPack gp;
+    gp.f16 = (uint16_t*)p;
     p += round_up(N * F * 2, 256);
+    gp.val = (float*)p;
+    p += round_up(N * F * 4, 256);
     int2* glist = (int2*)p;
     p += round_up(g->nnz * 8, 256);
-    // the upstream gradient in list order, f32 even for bf16 storage: 2-B scattered
-    // placement stores measured 30 % slower for the whole backward (RMWs on partial lines)
-    float* dpack = (float*)p;
-    p += round_up(N * F * 4, 256);
     const int32_t* einv = g->einv;
     if (!einv) {
       int32_t* e = (int32_t*)p;
@@ -1378,19 +1377,23 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     auto pack = [&](auto nv_c) {
       constexpr int NV = decltype(nv_c)::value;
       hipLaunchKernelGGL((group_pack_kernel<uint16_t, T, NV>), pgrid, dim3(kBlock), 0, st, prow, n_long, (int)N,
-                         g->ptr, einv, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, gfeat, glist, dpack);
+                         g->ptr, einv, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, gp, glist);
       return PG_OK;
     };
     if (vec) dispatch_nc_vec((int)((F + 255) / 256), pack);
     else pack(std::integral_constant<int, 0>{});
     const int blocks = grid_for(gt->n_items);
+    // with fwd_out the relu' mask is implied (the contract: mask_src >= 0): every entry left
+    // in the lists has fwd_out = X[u,f] w != 0, so X[u,f] > 0; an element with no entries
+    // sums to +0, which the mask would leave +0
+    if (fwd_out) mask_src = nullptr;
     if (g->ew)
       hipLaunchKernelGGL((max_bwd_pull_kernel<true, T>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
-                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, glist, gfeat, dpack,
+                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, glist, gp,
                          (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F));
     else
       hipLaunchKernelGGL((max_bwd_pull_kernel<false, T>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
-                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, glist, gfeat, dpack,
+                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, glist, gp,
                          (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F));
     if (gt->n_merges > 0)
       hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,

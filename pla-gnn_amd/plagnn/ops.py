@@ -101,7 +101,8 @@ def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
     """dX of the max aggregation (DGL GSpMM.backward: scatter_add_ through argX),
     gathered per source in ascending destination order; optional fused relu' mask
     (mask[u,f] > 0). With `fwd_out` (the forward's output; needs mask = the forward's
-    input) entries whose maximum is 0 are skipped: they contribute nothing."""
+    input, a relu output >= 0) entries whose maximum is 0 are skipped: they contribute
+    nothing, and the mask is implied by the skip (not read)."""
     _check_device(dg, argpos, dout, ew_slots, mask)
     bf = dout.dtype == torch.bfloat16
     if bf and ((mask is not None and mask.dtype != torch.bfloat16) or not dg.is_cuda):

@@ -191,6 +191,47 @@ def test_gemm_f32(ta, tb, shape):
     assert (C - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item()), (C - ref).abs().max()
 
 
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(20004, 508, 1000), (20004, 252, 500)], ids=["x3_128x128", "x3_128x64"])
+def test_gemm_f32_x3_tiles(ta, tb, M, N, K):
+    """The unsplit 128 x 128 and 128 x 64 three-piece tiles (csrc/gemm.hip pick_tile_x3:
+    >= 512 tiles of 128 x 128, else >= 512 of 128 x 64) in every transpose combination, on
+    ragged extents: M and N not multiples of the tile, K not a multiple of the 16-k step.
+    Error bound per output: 1e-6 of sum_k |a b| (the f32 level, as
+    test_gemm_f32_is_f32_accurate)."""
+    from plagnn import ops
+
+    g = torch.Generator().manual_seed(M + 3 * N + K + 7 * ta + 11 * tb)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    a64 = A.double().t() if ta else A.double()
+    b64 = B.double().t() if tb else B.double()
+    C = ops.gemm(A.to(DEV), B.to(DEV), transa=ta, transb=tb).cpu().double()
+    err = ((C - a64 @ b64).abs() / (a64.abs() @ b64.abs())).max().item()
+    assert err <= 1e-6, err
+
+
+def test_gemm_f32_non_finite_contract():
+    """include/plagnn.h (pg_gemm_f32): the three-piece path takes finite operands with
+    |x| < 3.39e38; an Inf operand, or a finite one that rounds to Inf in bf16, gives NaN in
+    the outputs it feeds, and leaves every other output exact to the f32 level."""
+    from plagnn import ops
+
+    M, N, K = 3000, 504, 504
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    A[7, 3] = float("inf")
+    A[11, 100] = 3.4e38  # rounds to Inf in bf16
+    C = ops.gemm(A.to(DEV), B.to(DEV), transa=False, transb=True).cpu().double()
+    assert torch.isnan(C[7]).all() and torch.isnan(C[11]).all()
+    ok = torch.ones(M, dtype=torch.bool)
+    ok[[7, 11]] = False
+    a64, b64 = A[ok].double(), B.double().t()
+    err = ((C[ok] - a64 @ b64).abs() / (a64.abs() @ b64.abs())).max().item()
+    assert err <= 1e-6, err
+
+
 @pytest.mark.parametrize("ta,tb,M,N,K", [(False, True, 3000, 504, 504), (False, False, 3000, 512, 256),
                                          (True, False, 256, 1008, 24041), (True, True, 136, 200, 1000)])
 def test_gemm_f32_is_f32_accurate(ta, tb, M, N, K):
