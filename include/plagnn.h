@@ -85,6 +85,12 @@ typedef void* pg_stream_t; /* hipStream_t */
 /* element type of the per-(row, feature) argmax record */
 #define PG_ARG_U16 16 /* position of the winning edge inside its row, 0xFFFF = none */
 #define PG_ARG_I32 32 /* same, int32, -1 = none (rows with degree >= 65535) */
+/* flag OR-ed into arg_kind of pg_spmm_max_fwd[_bf16] / pg_spmm_max_bwd[_bf16] (ABI 6): the
+ * forward records "none" where the maximum is 0 (not DGL's argX there: for relu inputs
+ * whose gradient the relu' mask removes anyway); the backward then skips those entries
+ * as fwd_out would, without reading fwd_out, and takes mask_src (required, X >= 0) as
+ * implied. The other record consumers take the plain kind. */
+#define PG_ARG_DEAD_NONE 0x100
 
 /* activation codes for pg_bias_act / pg_gemm_f32 epilogues */
 /* storage types of pg_gemm_bf16's output */
@@ -423,7 +429,8 @@ int pg_perturb_fill(const double* xc_normal, const double* xc_inter, const doubl
 const char* pg_last_error_string(void);
 int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-kernel split-K
                          (epilogue without splitk_cnt), no grouped SpMM pair; 6: with fwd_out,
-                         pg_spmm_max_bwd[_bf16] takes mask_src >= 0 and does not read it */
+                         pg_spmm_max_bwd[_bf16] takes mask_src >= 0 and does not read it;
+                         PG_ARG_DEAD_NONE */
 
 #ifdef __cplusplus
 }

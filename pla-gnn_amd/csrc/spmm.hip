@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
     const int32_t* __restrict__ eslot, const float* __restrict__ ew,
     const int4* __restrict__ items, int n_items, const T* __restrict__ X, int64_t ldx, int F,
     T* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
-    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, int n_ftiles = 1, int ftile = 0) {
+    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, int n_ftiles, int ftile, int dead_none) {
   constexpr int U = EdgeU<W, NC>::value;
   // n_ftiles > 1: all feature tiles of F in one launch, block b -> (item block b / n_ftiles,
   // tile b % n_ftiles), so every tile's longest items start first
@@ -246,6 +246,13 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
 #pragma unroll
       for (int i = 0; i < W; ++i)
         if (__builtin_isinf(best[c][i])) best[c][i] = 0.f;
+    if (dead_none) {  // PG_ARG_DEAD_NONE: a zero maximum records no winner
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < W; ++i)
+          if (best[c][i] == 0.f) bpos[c][i] = arg_none<A>();
+    }
     T* orow = out + (int64_t)row * ldo;
     A* arow = arg + (int64_t)row * lda;
 #pragma unroll
@@ -275,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void max_merge_kernel(const int4* __restric
                                                            const A* __restrict__ ws_arg,
                                                            int64_t ldw, T* __restrict__ out,
                                                            int64_t ldo, A* __restrict__ arg,
-                                                           int64_t lda) {
+                                                           int64_t lda, int dead_none) {
   const int4 m = merges[blockIdx.x];
   const int row = m.x, s0 = m.y, ns = m.z;
   for (int f = threadIdx.x; f < F; f += kBlock) {
@@ -298,6 +305,7 @@ __global__ __launch_bounds__(kBlock) void max_merge_kernel(const int4* __restric
         }
     }
     if (__builtin_isinf(best)) best = 0.f;
+    if (dead_none && best == 0.f) bp = arg_none<A>();
     out[(int64_t)row * ldo + f] = from_f<T>(best);
     arg[(int64_t)row * lda + f] = (A)bp;
   }
@@ -1142,7 +1150,7 @@ inline TilePlan plan_tiles(int64_t F, std::initializer_list<int64_t> lds,
 template <typename A, typename T>
 int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
                    int64_t ldo, A* arg, int64_t lda, float* ws_val, A* ws_arg, int64_t ldw,
-                   hipStream_t st) {
+                   int dead_none, hipStream_t st) {
   // argpos rows: u16 x4 = 8 B -> need 8-B alignment only; treat via the same 16-B check on
   // the float operands and an 8-B check on arg.
   TilePlan tp = plan_tiles(F, {ldx, ldo, lda}, {X, out, ws_val});
@@ -1165,7 +1173,7 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
       hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T>), dim3((unsigned)blocks * n_ft), dim3(kBlock), 0, st,
                          g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
                          X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, n_ft,
-                         (int)tp.tile);
+                         (int)tp.tile, dead_none);
       return PG_OK;
     };
     int rc;
@@ -1182,7 +1190,7 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
     if (g->n_merges > 0) {
       hipLaunchKernelGGL((max_merge_kernel<A, T>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
                          (const int4*)g->merges, (int)g->n_merges, (int)F, ws_val + f0, ws_arg + f0,
-                         ldw, out + f0, ldo, arg + f0, lda);
+                         ldw, out + f0, ldo, arg + f0, lda, dead_none);
     }
   }
   return hip_status("pg_spmm_max_fwd");
@@ -1244,7 +1252,7 @@ size_t pg_spmm_max_fwd_workspace(const pg_csr_t* g, int64_t F, int arg_kind) {
   if (!g || g->n_slots <= 0 || F <= 0) return 0;
   const int64_t ldw = ws_ld(F);
   const size_t vals = round_up(g->n_slots * ldw * 4, 256);
-  const size_t args = round_up(g->n_slots * ldw * (int64_t)pg::arg_bytes(arg_kind), 256);
+  const size_t args = round_up(g->n_slots * ldw * (int64_t)pg::arg_bytes(arg_kind & ~PG_ARG_DEAD_NONE), 256);
   return vals + args;
 }
 
@@ -1257,6 +1265,8 @@ int max_fwd_entry(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
                   void* argpos, int64_t lda, int arg_kind, void* ws, size_t ws_bytes,
                   pg_stream_t stream) {
   PG_TRY(pg::check_csr(g, "pg_spmm_max_fwd", true));
+  const int dead_none = (arg_kind & PG_ARG_DEAD_NONE) != 0;
+  arg_kind &= ~PG_ARG_DEAD_NONE;
   if (!pg::valid_arg_kind(arg_kind))
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_fwd: bad arg_kind %d", arg_kind);
   if (F < 0 || ldx < F || ldo < F || lda < F)
@@ -1274,9 +1284,9 @@ int max_fwd_entry(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
   hipStream_t st = (hipStream_t)stream;
   if (arg_kind == PG_ARG_U16)
     return launch_max_fwd<uint16_t, T>(g, X, ldx, F, out, ldo, (uint16_t*)argpos, lda, ws_val,
-                                       (uint16_t*)ws_arg, ldw, st);
+                                       (uint16_t*)ws_arg, ldw, dead_none, st);
   return launch_max_fwd<int32_t, T>(g, X, ldx, F, out, ldo, (int32_t*)argpos, lda, ws_val,
-                                    (int32_t*)ws_arg, ldw, st);
+                                    (int32_t*)ws_arg, ldw, dead_none, st);
 }
 
 }  // namespace
@@ -1324,6 +1334,9 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
                   size_t ws_bytes, pg_stream_t stream) {
   PG_TRY(pg::check_csr(g, "pg_spmm_max_bwd", false));
   PG_TRY(pg::check_csr(gt, "pg_spmm_max_bwd", true));
+  // PG_ARG_DEAD_NONE: the records already leave out the zero maxima (fwd_out's filter)
+  const bool dead_none = (arg_kind & PG_ARG_DEAD_NONE) != 0;
+  arg_kind &= ~PG_ARG_DEAD_NONE;
   if (!pg::valid_arg_kind(arg_kind))
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: bad arg_kind %d", arg_kind);
   if (gt->n_cols != g->n_rows || gt->nnz != g->nnz)
@@ -1332,8 +1345,10 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: gt needs eslot and epos");
   if (F < 0 || ldd < F || ldx < F || lda < F || (mask_src && ldm < F) || (fwd_out && ldf < F))
     return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: bad F/leading dims");
-  if (fwd_out && !mask_src)
-    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: fwd_out (skip zero maxima) needs mask_src");
+  if ((fwd_out || dead_none) && !mask_src)
+    return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: fwd_out / PG_ARG_DEAD_NONE needs mask_src");
+  const bool mask_implied = fwd_out || dead_none;
+  if (dead_none) fwd_out = nullptr;
   if (F == 0 || gt->n_rows == 0) return pg::ok();
   if (!argpos || !dout || !dx) return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: NULL buffer");
   const size_t need = pg_spmm_max_bwd_workspace(gt, F);
@@ -1383,10 +1398,10 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     if (vec) dispatch_nc_vec((int)((F + 255) / 256), pack);
     else pack(std::integral_constant<int, 0>{});
     const int blocks = grid_for(gt->n_items);
-    // with fwd_out the relu' mask is implied (the contract: mask_src >= 0): every entry left
-    // in the lists has fwd_out = X[u,f] w != 0, so X[u,f] > 0; an element with no entries
-    // sums to +0, which the mask would leave +0
-    if (fwd_out) mask_src = nullptr;
+    // with fwd_out / dead-none records the relu' mask is implied (the contract: mask_src >=
+    // 0): every entry left in the lists has a maximum X[u,f] w != 0, so X[u,f] > 0; an
+    // element with no entries sums to +0, which the mask would leave +0
+    if (mask_implied) mask_src = nullptr;
     if (g->ew)
       hipLaunchKernelGGL((max_bwd_pull_kernel<true, T>), dim3(blocks), dim3(kBlock), 0, st, g->ew,
                          gt->eslot, (const int4*)gt->items, (int)gt->n_items, glist, gp,

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("PLAGNN_LIB") or os.path.join(_HERE, "libplagnn.so")
 
 PG_ARG_U16 = 16
 PG_ARG_I32 = 32
+PG_ARG_DEAD_NONE = 0x100  # flag: a zero maximum records no winner (include/plagnn.h)
 PG_DTYPE_F32 = 0
 PG_DTYPE_BF16 = 1
 PG_ACT_NONE = 0

@@ -33,7 +33,7 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from ._lib import call, ptr
+from ._lib import PG_ARG_DEAD_NONE as DEAD_NONE, call, ptr
 from .graph import CSRGraph, DeviceGraph
 from .ops import LEAKY_SLOPE, round4
 
@@ -460,7 +460,7 @@ class TrainEngine:
             # M = max-aggregate(P) -> right half of HM
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
                 self._call("pg_spmm_max_fwd", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
-                     ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
+                     ptr(self.arg[l]), Fi, self.dg.arg_kind | DEAD_NONE, ptr(self.ws), self.ws_bytes, st)
             # Y = [H | M] Wcat^T + b (fc_self + fc_neigh + bias), leaky_relu -> next input
             Fo = pd[l + 1]
             out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
@@ -502,10 +502,11 @@ class TrainEngine:
             self._gemm(dY, HM, G[p + "Wcat"], transa=True, rowsum=G[p + "b"], tag=f"gemm.wgrad.cat.l{l + 1}")
             # dM = dY Wneigh
             self._gemm(dY, P[p + "Wcat"][:, Fi:], self.dM[l], tag=f"gemm.dgrad.neigh.l{l + 1}")
-            # max backward with relu' of fc_pool fused; zero maxima (M = 0) are skipped
+            # max backward; the records say "none" where M = 0 (DEAD_NONE), so those entries are
+            # skipped and the relu' mask of fc_pool (P >= 0) is implied
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                self._call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.dM[l]), Fi, Fi,
-                     ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(dP), DYP.stride(0), ptr(self.ws),
+                self._call("pg_spmm_max_bwd", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind | DEAD_NONE, ptr(self.dM[l]), Fi, Fi,
+                     ptr(self.Pl[l]), Fi, None, 0, ptr(dP), DYP.stride(0), ptr(self.ws),
                      self.ws_bytes, st)
             # d Wpool = dP^T H, d bpool = sum_nodes dP
             self._gemm(dP, HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],

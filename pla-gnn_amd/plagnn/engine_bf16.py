@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from ._lib import ptr
+from ._lib import PG_ARG_DEAD_NONE as DEAD_NONE, ptr
 from .engine import LEAKY, NONE, RELU, TrainEngine, _Flat
 
 BF16, F32 = _lib.PG_DTYPE_BF16, _lib.PG_DTYPE_F32
@@ -152,7 +152,7 @@ class TrainEngineBF16(TrainEngine):
                        tag=f"gemm.fwd.pool.l{l + 1}")
             with self._t(f"spmm_max_fwd.l{l + 1}", self.spmm_bytes(l)):
                 self._call("pg_spmm_max_fwd_bf16", g, ptr(self.Pl[l]), Fi, Fi, ptr(HM[:, Fi:]), HM.stride(0),
-                     ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.ws), self.ws_bytes, st)
+                     ptr(self.arg[l]), Fi, self.dg.arg_kind | DEAD_NONE, ptr(self.ws), self.ws_bytes, st)
             Fo = pd[l + 1]
             out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
             self._gemm(HM, W[p + "Wcat"], out, transb=True, bias=P[p + "b"], act=LEAKY,
@@ -182,8 +182,8 @@ class TrainEngineBF16(TrainEngine):
             # dM = dY Wneigh   (Wneigh = the right half of Wcat, read as a [Fo][Fi] k image)
             self._gemm(dY, W[p + "Wcat"][:, Fi:], self.dM[l], tag=f"gemm.dgrad.neigh.l{l + 1}")
             with self._t(f"spmm_max_bwd.l{l + 1}", self.spmm_bwd_bytes(l)):
-                self._call("pg_spmm_max_bwd_bf16", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind, ptr(self.dM[l]),
-                     Fi, Fi, ptr(self.Pl[l]), Fi, ptr(HM[:, Fi:]), HM.stride(0), ptr(dP), DYP.stride(0),
+                self._call("pg_spmm_max_bwd_bf16", g, gt, ptr(self.arg[l]), Fi, self.dg.arg_kind | DEAD_NONE, ptr(self.dM[l]),
+                     Fi, Fi, ptr(self.Pl[l]), Fi, None, 0, ptr(dP), DYP.stride(0),
                      ptr(self.ws), self.ws_bytes, st)
             self._gemm(dP, HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
                        tag=f"gemm.wgrad.pool.l{l + 1}")

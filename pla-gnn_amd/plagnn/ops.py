@@ -65,10 +65,11 @@ def _check_device(dg: DeviceGraph, *ts):
 
 # ------------------------------------------------------------------ message passing
 def spmm_max(dg: DeviceGraph, X: torch.Tensor, ew_slots: Optional[torch.Tensor] = None,
-             out: Optional[torch.Tensor] = None, argpos: Optional[torch.Tensor] = None
-             ) -> Tuple[torch.Tensor, torch.Tensor]:
+             out: Optional[torch.Tensor] = None, argpos: Optional[torch.Tensor] = None,
+             dead_none: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """out[v] = max over in-edges of X[u] (* w), argpos = winning in-row position.
-    DGL update_all(copy_u|u_mul_e, max) (code/model.py:20,22,24)."""
+    DGL update_all(copy_u|u_mul_e, max) (code/model.py:20,22,24). `dead_none`
+    (PG_ARG_DEAD_NONE, GPU): a zero maximum records no winner."""
     if X.dtype not in (torch.float32, torch.bfloat16):
         raise TypeError("spmm_max: float32 or bfloat16 features expected")
     bf = X.dtype == torch.bfloat16
@@ -86,8 +87,9 @@ def spmm_max(dg: DeviceGraph, X: torch.Tensor, ew_slots: Optional[torch.Tensor] 
     if dg.is_cuda:
         ws_n = _lib.lib().pg_spmm_max_fwd_workspace(g, F, dg.arg_kind)
         ws = _workspace(ws_n, X.device)
+        kind = dg.arg_kind | (_lib.PG_ARG_DEAD_NONE if dead_none else 0)
         call("pg_spmm_max_fwd_bf16" if bf else "pg_spmm_max_fwd", g, ptr(X), _ld(X), F, ptr(out), _ld(out), ptr(argpos), _ld(argpos),
-             dg.arg_kind, ptr(ws), ws_n, _stream(X))
+             kind, ptr(ws), ws_n, _stream(X))
     else:
         call("pg_spmm_max_fwd_cpu", g, ptr(X), _ld(X), F, ptr(out), _ld(out), ptr(argpos),
              _ld(argpos), dg.arg_kind)
@@ -96,13 +98,14 @@ def spmm_max(dg: DeviceGraph, X: torch.Tensor, ew_slots: Optional[torch.Tensor] 
 
 def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
                       ew_slots: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
-                      dx: Optional[torch.Tensor] = None, fwd_out: Optional[torch.Tensor] = None
-                      ) -> torch.Tensor:
+                      dx: Optional[torch.Tensor] = None, fwd_out: Optional[torch.Tensor] = None,
+                      dead_none: bool = False) -> torch.Tensor:
     """dX of the max aggregation (DGL GSpMM.backward: scatter_add_ through argX),
     gathered per source in ascending destination order; optional fused relu' mask
     (mask[u,f] > 0). With `fwd_out` (the forward's output; needs mask = the forward's
     input, a relu output >= 0) entries whose maximum is 0 are skipped: they contribute
-    nothing, and the mask is implied by the skip (not read)."""
+    nothing, and the mask is implied by the skip (not read). `dead_none`: the records come
+    from spmm_max(..., dead_none=True) (the same skip without fwd_out; needs mask)."""
     _check_device(dg, argpos, dout, ew_slots, mask)
     bf = dout.dtype == torch.bfloat16
     if bf and ((mask is not None and mask.dtype != torch.bfloat16) or not dg.is_cuda):
@@ -117,7 +120,8 @@ def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
         ws_n = _lib.lib().pg_spmm_max_bwd_workspace(gt, F)
         ws = _workspace(ws_n, dout.device)
         ldf = _ld(fwd_out) if fwd_out is not None else 0
-        call("pg_spmm_max_bwd_bf16" if bf else "pg_spmm_max_bwd", g, gt, ptr(argpos), _ld(argpos), dg.arg_kind, ptr(dout), _ld(dout),
+        kind = dg.arg_kind | (_lib.PG_ARG_DEAD_NONE if dead_none else 0)
+        call("pg_spmm_max_bwd_bf16" if bf else "pg_spmm_max_bwd", g, gt, ptr(argpos), _ld(argpos), kind, ptr(dout), _ld(dout),
              F, ptr(mask), ldm, ptr(fwd_out), ldf, ptr(dx), _ld(dx), ptr(ws), ws_n, _stream(dout))
     else:
         call("pg_spmm_max_bwd_cpu", g, gt, ptr(argpos), _ld(argpos), dg.arg_kind, ptr(dout),

@@ -374,7 +374,8 @@ def test_gemm_fused_activation_backward():
 def test_spmm_max_bwd_skip_zero_maxima_is_exact(F, weighted):
     """fwd_out = the forward's output: entries whose maximum is 0 are skipped (their winner is
     relu-masked or weighted 0), and dx is bitwise unchanged — hub rows and dead features
-    (all-zero columns, whose ties all sit at position 0) included."""
+    (all-zero columns, whose ties all sit at position 0) included; the same with records
+    made by the forward with PG_ARG_DEAD_NONE (what TrainEngine runs)."""
     from plagnn import ops
 
     n = 800
@@ -393,11 +394,20 @@ def test_spmm_max_bwd_skip_zero_maxima_is_exact(F, weighted):
     a = ops.spmm_max_backward(dg, arg, dZ, ew, mask=P)
     b = ops.spmm_max_backward(dg, arg, dZ, ew, mask=P, fwd_out=out)
     assert torch.equal(a, b)
+    # PG_ARG_DEAD_NONE records: the same maxima, "none" where the maximum is 0, and the
+    # backward bitwise the same without fwd_out
+    out_d, arg_d = ops.spmm_max(dg, P, ew, dead_none=True)
+    assert torch.equal(out_d, out)
+    none = torch.full_like(arg, -1)
+    assert torch.equal(arg_d, torch.where(out == 0, none, arg))
+    assert torch.equal(ops.spmm_max_backward(dg, arg_d, dZ, ew, mask=P, dead_none=True), a)
     bf = P.to(torch.bfloat16)
     outb, argb = ops.spmm_max(dg, bf, ew)
     dZb = dZ.to(torch.bfloat16)
-    assert torch.equal(ops.spmm_max_backward(dg, argb, dZb, ew, mask=bf),
-                       ops.spmm_max_backward(dg, argb, dZb, ew, mask=bf, fwd_out=outb))
+    ab = ops.spmm_max_backward(dg, argb, dZb, ew, mask=bf)
+    assert torch.equal(ab, ops.spmm_max_backward(dg, argb, dZb, ew, mask=bf, fwd_out=outb))
+    _, argb_d = ops.spmm_max(dg, bf, ew, dead_none=True)
+    assert torch.equal(ops.spmm_max_backward(dg, argb_d, dZb, ew, mask=bf, dead_none=True), ab)
 
 
 @pytest.mark.parametrize("M,N,K,ta", [(256, 1024, 24041, True), (100, 256, 24041, True),
