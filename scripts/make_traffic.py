@@ -21,8 +21,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from prof_groups import group_of  # noqa: E402
 
 
-def collect(root, counter):
-    """{group: [bytes, dispatches]} of the process with the most dispatches of `counter`."""
+def collect(root, counter, key=None):
+    """{group: [bytes, dispatches]} of the process with the most dispatches of `counter`
+    (key: the grouping function, default the kernel group)."""
+    key = key or group_of
     per_file = []
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         acc = defaultdict(lambda: [0.0, 0])
@@ -30,7 +32,7 @@ def collect(root, counter):
             for r in csv.DictReader(fh):
                 if r["Counter_Name"] != counter:
                     continue
-                a = acc[group_of(r["Kernel_Name"])]
+                a = acc[key(r["Kernel_Name"])]
                 a[0] += float(r["Counter_Value"]) * 1024.0
                 a[1] += 1
         per_file.append(acc)
@@ -44,9 +46,17 @@ def main():
     ap.add_argument("--gemm-group", default="gemm_f32", help="name of the GEMM group (gemm_bf16 for cfg5)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
+    ap.add_argument("--by-kernel", action="store_true", help="also print bytes per dispatch of each kernel")
     a = ap.parse_args()
     fetch = collect(os.path.join(a.root, "fetch"), "FETCH_SIZE")
     write = collect(os.path.join(a.root, "write"), "WRITE_SIZE")
+    if a.by_kernel:
+        short = lambda n: n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:70]  # noqa: E731
+        fk = collect(os.path.join(a.root, "fetch"), "FETCH_SIZE", short)
+        wk = collect(os.path.join(a.root, "write"), "WRITE_SIZE", short)
+        for k in sorted(fk):
+            f, w = fk[k], wk.get(k, [0.0, 1])
+            print(f"{k:70s} n={f[1]:5d} fetch2x {2 * f[0] / f[1] / 1e6:9.2f} MB  write {w[0] / max(w[1], 1) / 1e6:9.2f} MB")
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     cfg = {}
     for g in sorted(set(fetch) | set(write)):

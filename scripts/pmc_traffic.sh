@@ -17,4 +17,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   [ $rc -eq 0 ] || exit $rc
 done
 GG=gemm_f32; [ $CONFIG = cfg5 ] && GG=gemm_bf16
-python3 scripts/make_traffic.py $OUT $CONFIG --gemm-group $GG
+python3 scripts/make_traffic.py $OUT $CONFIG --gemm-group $GG --by-kernel
