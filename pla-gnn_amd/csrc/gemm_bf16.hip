@@ -156,6 +156,58 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
+// one output quad (row gr, columns gc .. gc + 3) with the fused epilogue, or its split-K
+// partial (slab blockIdx.z)
+template <int EPI, bool OBF>
+__device__ __forceinline__ void store4(const float4 v, int gr, int gc, int M, int N, float alpha, float beta,
+                                       void* __restrict__ Cv, int64_t ldc, const float* __restrict__ bias,
+                                       float slope, const uint16_t* __restrict__ dact, int64_t lddact,
+                                       float* __restrict__ ws) {
+  if constexpr (EPI == EPI_SPLIT) {
+    *reinterpret_cast<float4*>(ws + ((int64_t)blockIdx.z * M + gr) * N + gc) = v;
+    return;
+  } else {
+    float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
+    float y[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
+      const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
+      y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
+    }
+    if constexpr (OBF) {
+      uint16_t* cp = (uint16_t*)Cv + (int64_t)gr * ldc + gc;
+      if (beta != 0.f) {
+        const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
+        o[0] = o[0] + beta * bf2f(c2.x & 0xFFFF); o[1] = o[1] + beta * bf2f(c2.x >> 16);
+        o[2] = o[2] + beta * bf2f(c2.y & 0xFFFF); o[3] = o[3] + beta * bf2f(c2.y >> 16);
+      }
+      if (bias) {
+        const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
+        o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
+      }
+      uint2 w;
+      w.x = (uint32_t)f2bf(epi_apply<EPI>(o[0], y[0], slope)) |
+            ((uint32_t)f2bf(epi_apply<EPI>(o[1], y[1], slope)) << 16);
+      w.y = (uint32_t)f2bf(epi_apply<EPI>(o[2], y[2], slope)) |
+            ((uint32_t)f2bf(epi_apply<EPI>(o[3], y[3], slope)) << 16);
+      *reinterpret_cast<uint2*>(cp) = w;
+    } else {
+      float* cp = (float*)Cv + (int64_t)gr * ldc + gc;
+      if (beta != 0.f) {
+        const float4 c4 = *reinterpret_cast<const float4*>(cp);
+        o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
+        o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
+      }
+      if (bias) {
+        const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
+        o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
+      }
+      *reinterpret_cast<float4*>(cp) =
+          make_float4(epi_apply<EPI>(o[0], y[0], slope), epi_apply<EPI>(o[1], y[1], slope),
+                      epi_apply<EPI>(o[2], y[2], slope), epi_apply<EPI>(o[3], y[3], slope));
+    }
+  }
+}
+
 // epilogue through LDS: the accumulator tile is transposed into a row-major f32 image and
 // written out 4 consecutive outputs per thread (16-B f32 / 8-B bf16 stores). A tile whose
 // f32 image does not fit the staging array (256 x 256) goes in PASSES row bands: in pass
@@ -207,53 +259,7 @@ __device__ __forceinline__ void finish_tile(const f32x16 (&acc)[BM / WM / 32][BN
       const int gr = m0 + pass * BAND + row, gc = n0 + c;
       if (gr >= M || gc >= N) continue;
       const float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
-      if constexpr (SPLIT) {
-        *reinterpret_cast<float4*>(ws + ((int64_t)blockIdx.z * M + gr) * N + gc) = v;
-      } else {
-        float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
-        if constexpr (OBF) {
-          uint16_t* cp = (uint16_t*)Cv + (int64_t)gr * ldc + gc;
-          if (beta != 0.f) {
-            const uint2 c2 = *reinterpret_cast<const uint2*>(cp);
-            o[0] = o[0] + beta * bf2f(c2.x & 0xFFFF); o[1] = o[1] + beta * bf2f(c2.x >> 16);
-            o[2] = o[2] + beta * bf2f(c2.y & 0xFFFF); o[3] = o[3] + beta * bf2f(c2.y >> 16);
-          }
-          if (bias) {
-            const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
-            o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
-          }
-          float y[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
-            const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
-            y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
-          }
-          uint2 w;
-          w.x = (uint32_t)f2bf(epi_apply<EPI>(o[0], y[0], slope)) |
-                ((uint32_t)f2bf(epi_apply<EPI>(o[1], y[1], slope)) << 16);
-          w.y = (uint32_t)f2bf(epi_apply<EPI>(o[2], y[2], slope)) |
-                ((uint32_t)f2bf(epi_apply<EPI>(o[3], y[3], slope)) << 16);
-          *reinterpret_cast<uint2*>(cp) = w;
-        } else {
-          float* cp = (float*)Cv + (int64_t)gr * ldc + gc;
-          if (beta != 0.f) {
-            const float4 c4 = *reinterpret_cast<const float4*>(cp);
-            o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
-            o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
-          }
-          if (bias) {
-            const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
-            o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
-          }
-          float y[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
-            const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
-            y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
-          }
-          *reinterpret_cast<float4*>(cp) =
-              make_float4(epi_apply<EPI>(o[0], y[0], slope), epi_apply<EPI>(o[1], y[1], slope),
-                          epi_apply<EPI>(o[2], y[2], slope), epi_apply<EPI>(o[3], y[3], slope));
-        }
-      }
+      store4<EPI, OBF>(v, gr, gc, M, N, alpha, beta, Cv, ldc, bias, slope, dact, lddact, ws);
     }
     if (PASSES > 1) __syncthreads();
   }
@@ -390,6 +396,195 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
                                 beta, C, ldc, bias, slope, dact, lddact, rowsum, ws, ws_rowsum);
 }
 
+// ---- 256 x 256 ping-pong kernel for A[m][k] x B[n][k]^T (both operands row images) -----
+// Eight waves (2 x 4, two per SIMD), each owning 128 x 64 outputs as 8 x 4 tiles of
+// v_mfma_f32_16x16x32_bf16. A K tile (64 k) is four phases; phase q covers one 64 x 32
+// quadrant of every wave's block (snake order (0,0) (0,1) (1,1) (1,0), so one operand's
+// fragments carry over) in two sections: R (the quadrant's fragment reads, ds_read_b128,
+// plus a share of the next K tile's LDS-DMA) and M (16 MFMAs between s_setprio 1/0).
+// Wave row 1 runs one barrier behind wave row 0, so on every SIMD one wave's R section
+// sits beside the other's M section (cdna_hip_programming.md §5, the 256² template).
+// LDS: two K-tile buffers [A 256 x 64 | B 256 x 64] (128 KiB), filled by LDS-DMA with the
+// row-image swizzle. Each quarter of a buffer (the A rows or B columns of one quadrant row /
+// column) is restaged two phases after its last read — the MFMAs that consumed those reads
+// have finished in both wave rows by then — so a tile's pieces go out up to six phases
+// before they are read; one counted vmcnt per K tile (phase 4) retires tile t + 1 while
+// tile t + 2's first pieces stay in flight. (With B stored [k][n] — a k image every phase
+// reads whole — this schedule measured slower than the two-phase kernel: DESIGN.md §7.)
+// Raw s_barrier throughout (a __syncthreads would wait vmcnt(0) at every barrier).
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+// end of a section. RETIRE: lgkmcnt(0) first (this wave's fragment reads and zero fills
+// done), so a buffer read in this section may be restaged right after the barrier; else the
+// reads stay in flight across it (the MFMAs' own waits retire them)
+template <bool RETIRE>
+__device__ __forceinline__ void pp_bar() {
+  if constexpr (RETIRE) __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int EPI, bool OBF>
+__global__ __launch_bounds__(512) void gemm_bf16_pp_kernel(
+    int M, int N, int K, int tiles_n, int tiles, float alpha, const uint16_t* __restrict__ A, int64_t lda,
+    const uint16_t* __restrict__ B, int64_t ldb, float beta, void* __restrict__ C, int64_t ldc,
+    const float* __restrict__ bias, float slope, const uint16_t* __restrict__ dact, int64_t lddact) {
+  constexpr int IMG = 256 * 64;  // one operand's K-tile image (u16)
+  constexpr int BUF = 2 * IMG;   // [A | B]
+  constexpr int EPS = 260;       // f32 epilogue image row stride (floats; 16-B aligned rows)
+  static_assert(64 * EPS * 4 <= 2 * BUF * 2, "epilogue band fits");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+
+  const int b = blockIdx.x;
+  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
+  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int m0 = (tile / tiles_n) * 256, n0 = (tile % tiles_n) * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int l16 = lane & 15, kq = 8 * (lane >> 4);
+  const int nk = (K + 63) / 64;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // LDS-DMA of one 1-KiB piece (8 rows x 64 k) of a row image; lanes past K zero-fill
+  auto piece_row = [&](const uint16_t* P, int64_t ld, int r0, int R, int k0, uint16_t* img, int piece) {
+    const int u = piece * 64 + lane;
+    const int row = u >> 3;
+    const int c = (u & 7) ^ ((row >> 1) & 7);
+    const uint16_t* src = P + (int64_t)min(r0 + row, R - 1) * ld + k0 + 8 * c;
+    if (K - k0 >= 64 || 8 * c < K - k0) __builtin_amdgcn_global_load_lds(src, img + piece * 512, 16, 0, 0);
+    else *reinterpret_cast<uint4*>(img + u * 8) = make_uint4(0u, 0u, 0u, 0u);
+  };
+  // A rows of quadrant row s of both wave rows: pieces 8 s .. 8 s + 7 and 16 + the same
+  auto stage_a = [&](int t, int buf, int sub) {
+    uint16_t* img = lds + buf * BUF;
+    piece_row(A, lda, m0, M, t * 64, img, sub * 8 + wave);
+    piece_row(A, lda, m0, M, t * 64, img, 16 + sub * 8 + wave);
+  };
+  // B (row image) columns of quadrant column s of every wave column: rows wc 64 + 32 s ..
+  auto stage_b = [&](int t, int buf, int sub) {
+    uint16_t* img = lds + buf * BUF + IMG;
+    const int pc = (wave >> 1) * 8 + sub * 4 + (wave & 1) * 2;
+    piece_row(B, ldb, n0, N, t * 64, img, pc);
+    piece_row(B, ldb, n0, N, t * 64, img, pc + 1);
+  };
+  bf16x8 fa[4][2], fb[2][2];
+  auto read_a = [&](const uint16_t* S, int asub) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fa[i][ks] = *reinterpret_cast<const bf16x8*>(
+            S + img_off<256, false, 64>(wr * 128 + asub * 64 + i * 16 + l16, 32 * ks + kq));
+  };
+  auto read_b = [&](const uint16_t* S, int bsub) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fb[j][ks] = *reinterpret_cast<const bf16x8*>(
+            S + IMG + img_off<256, false, 64>(wc * 64 + bsub * 32 + j * 16 + l16, 32 * ks + kq));
+  };
+  auto mfma = [&](int asub, int bsub) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc[asub * 4 + i][bsub * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][ks], fb[j][ks], acc[asub * 4 + i][bsub * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if (nk > 0) {
+    // prologue: tile 0, and tile 1's pieces that steady state stages one tile early
+    stage_a(0, 0, 0);
+    stage_a(0, 0, 1);
+    stage_b(0, 0, 0);
+    stage_b(0, 0, 1);
+    if (nk > 1) {
+      stage_a(1, 1, 0);
+      stage_b(1, 1, 1);
+      wait_vmcnt<4>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    pp_bar<true>();
+    if (wr == 1) pp_bar<false>();  // wave row 1 runs one barrier behind
+    for (int t = 0; t < nk; ++t) {
+      const int c = t & 1;
+      const uint16_t* S = lds + c * BUF;
+      // phase 1: quadrant (0, 0); A rows of quadrant row 1 of tile t + 1 (their last reads,
+      // phase 3 of tile t - 1, were consumed by MFMAs both wave rows finished before this)
+      read_a(S, 0);
+      read_b(S, 0);
+      if (t + 1 < nk) stage_a(t + 1, c ^ 1, 1);
+      pp_bar<false>();
+      mfma(0, 0);
+      pp_bar<false>();
+      // phase 2: (0, 1); B columns of quadrant column 0 of tile t + 1 (last read in phase 4)
+      read_b(S, 1);
+      if (t + 1 < nk) stage_b(t + 1, c ^ 1, 0);
+      pp_bar<false>();
+      mfma(0, 1);
+      pp_bar<false>();
+      // phase 3: (1, 1); A rows of quadrant row 0 of tile t + 2 (last read in phase 1)
+      read_a(S, 1);
+      if (t + 2 < nk) stage_a(t + 2, c, 0);
+      pp_bar<false>();
+      mfma(1, 1);
+      pp_bar<false>();
+      // phase 4: (1, 0); B quadrant column 1 of tile t + 2 (last read in phase 2); then
+      // every piece of tile t + 1 retired (only tile t + 2's pieces stay in flight) and the
+      // zero fills done, before the section's barrier
+      read_b(S, 0);
+      if (t + 2 < nk) {
+        stage_b(t + 2, c, 1);
+        wait_vmcnt<4>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      pp_bar<true>();
+      mfma(1, 0);
+      pp_bar<false>();
+    }
+    if (wr == 0) pp_bar<false>();
+  }
+  __syncthreads();  // every wave past its last fragment read: the epilogue reuses the LDS
+
+  // epilogue in four 64-row bands (band p = wave row p / 2, A half p % 2)
+  float* img = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (wr == (p >> 1)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            img[(i * 16 + 4 * (lane >> 4) + e) * EPS + wc * 64 + j * 16 + l16] = acc[(p & 1) * 4 + i][j][e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 64 * 64 / 512; ++it) {
+      const int u = it * 512 + tid;
+      const int row = u >> 6, c = (u & 63) * 4;
+      const int gr = m0 + p * 64 + row, gc = n0 + c;
+      if (gr < M && gc < N)
+        store4<EPI, OBF>(*reinterpret_cast<const float4*>(img + row * EPS + c), gr, gc, M, N, alpha, beta, C,
+                         ldc, bias, slope, dact, lddact, nullptr);
+    }
+    __syncthreads();
+  }
+}
+
 struct Args {
   int M, N, K, kps, tiles_n, tiles;
   float alpha;
@@ -450,6 +645,29 @@ int launch_tile(bool ta, bool tb, bool obf, int epi, dim3 grid, hipStream_t st, 
   if (ta && !tb) PG_T(true, false);
   PG_T(true, true);
 #undef PG_T
+}
+
+#ifndef PG_BF16_PP
+#define PG_BF16_PP 1  // 0 (variant builds): the two-phase 256 x 256 kernel for A B^T as well
+#endif
+int launch_pp(bool obf, int epi, hipStream_t st, const Args& a) {
+#define PG_P(EPI_, OBF_)                                                                                    \
+  hipLaunchKernelGGL((gemm_bf16_pp_kernel<EPI_, OBF_>), dim3((unsigned)a.tiles), dim3(512), 0, st, a.M, a.N, a.K, \
+                     a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb, a.beta, a.C, a.ldc, a.bias, a.slope,  \
+                     a.dact, a.lddact)
+#define PG_PO(EPI_) \
+  if (obf) PG_P(EPI_, true); else PG_P(EPI_, false)
+  switch (epi) {
+    case EPI_NONE: PG_PO(EPI_NONE); break;
+    case EPI_RELU: PG_PO(EPI_RELU); break;
+    case EPI_LEAKY: PG_PO(EPI_LEAKY); break;
+    case EPI_DRELU: PG_PO(EPI_DRELU); break;
+    case EPI_DLEAKY: PG_PO(EPI_DLEAKY); break;
+    default: return PG_ERR_INVALID;
+  }
+#undef PG_PO
+#undef PG_P
+  return PG_OK;
 }
 
 // Tile choice. The bf16 MFMA rate (4096 flop/clk/CU) needs ~64 flop per byte staged
@@ -568,7 +786,8 @@ int pg_gemm_bf16(int transa, int transb, int64_t M, int64_t N, int64_t K, float 
                         : ep->dact ? (act == PG_ACT_RELU ? EPI_DRELU : EPI_DLEAKY)
                                    : (act == PG_ACT_RELU ? EPI_RELU : act == PG_ACT_LEAKY ? EPI_LEAKY : EPI_NONE);
   int rc;
-  if (bm == 256 && bn == 256) rc = launch_tile<256, 256, PG_BF16_WM, PG_BF16_WN>(ta, tb, obf, epi, grid, st, a);
+  if (PG_BF16_PP && bm == 256 && bn == 256 && !ta && tb && !split && !ep->rowsum) rc = launch_pp(obf, epi, st, a);
+  else if (bm == 256 && bn == 256) rc = launch_tile<256, 256, PG_BF16_WM, PG_BF16_WN>(ta, tb, obf, epi, grid, st, a);
   else if (bm == 256) rc = launch_tile<256, 128, 2, 2>(ta, tb, obf, epi, grid, st, a);
   else if (bm == 128 && bn == 128) rc = launch_tile<128, 128, 2, 2>(ta, tb, obf, epi, grid, st, a);
   else if (bm == 128) rc = launch_tile<128, 64, 2, 2>(ta, tb, obf, epi, grid, st, a);

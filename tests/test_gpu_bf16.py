@@ -32,7 +32,8 @@ def _ref(A, B, ta, tb):
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(1000, 256, 512), (4104, 520, 264), (200, 72, 1000), (64, 8, 8),
-                                   (65544, 520, 136)])  # the last one on 256 x 256 tiles
+                                   (65544, 520, 136), (36000, 512, 576)])  # the last two on 256 x 256 tiles
+                                   # (A B^T there: the ping-pong kernel)
 def test_gemm_bf16_f32_out(ta, tb, M, N, K):
     from plagnn import ops
 
