@@ -184,6 +184,19 @@ def test_full_size_step_matches_oracle(oracle_mod, s0_cfg2, dims):
     _check_step(oracle_mod, s0_cfg2, dims, sd)
 
 
+def test_mode_a_job_step_matches_oracle(oracle_mod):
+    """bench.py --mode replicas (Mode A): rank r trains the reference's job r (round r // 10,
+    fold r % 10: code/train.py:162-178) from its own initial parameters. One such job (round
+    4, fold 8) on the full S0 graph against the oracle, with its own train / val rows."""
+    from plagnn import workload
+
+    wl = workload.build("cfg2", device=DEV, job=37)
+    base = workload.build("cfg2", device=DEV, job=0)
+    assert not np.array_equal(np.sort(wl.train_index), np.sort(base.train_index))
+    sd = oracle_mod.init_params(wl.dims, seed=37)
+    _check_step(oracle_mod, wl, wl.dims, sd)
+
+
 def test_cfg3_edge_weighted_step_matches_oracle(oracle_mod):
     """cfg3: GSE30931's PPI_inter of S0 (pg_perturb), ECC_inter edge weights (u_mul_e max),
     hidden 512."""
