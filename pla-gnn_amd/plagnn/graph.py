@@ -25,8 +25,11 @@ from ._lib import PgCsr, call
 DEFAULT_CHUNK = 256
 # out-CSR entries per backward work item, its work is data-dependent (CSRGraph(chunk_bwd=...);
 # None = by graph size). Measured whole steps: S0 (24 041 nodes) 64-96 best (1.97 ms), 128
-# 1.99, 32 2.01, 256 2.11; RMAT x16 (384 656 nodes) 128 24.3 ms vs 64 25.2 ms: finer items
-# pay off only while the graph alone does not fill the chip.
+# 1.99, 32 2.01, 256 2.11 (round 2); again in round 3 with the cheaper pull: the cfg2
+# step's backward 0.259 ms at 64 vs 0.285 at 128, although the isolated kernel on random
+# relu inputs (scripts/bwd_chunk_sweep.py) prefers 128. RMAT x16 (384 656 nodes): 128
+# 24.3 ms per step vs 64 25.2 ms: finer items pay off only while the graph alone does not
+# fill the chip.
 DEFAULT_CHUNK_BWD = None
 
 
