@@ -239,14 +239,16 @@ def _roofline(engine, gt, bf16):
                          peak_f32_mfma=PEAK_F32_TFLOPS, frac_vs_f32_mfma=round(ach / PEAK_F32_TFLOPS, 4))
             return r
         ach = g["work"] / sec / 1e9
-        r = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-             "frac": round(ach / PEAK_HBM_GBS, 4), **base, "bytes_per_step": int(g["work"])}
         if gname == "spmm_max_fwd":
-            # the per-edge gathers of a feature matrix that fits the 256 MiB Infinity Cache are
-            # served by L2 / MALL, not HBM: also against the L2-served gather ceiling
-            r["ceiling_l2_gather_gbs"] = L2_GATHER_GBS
-            r["frac_vs_l2_gather"] = round(ach / L2_GATHER_GBS, 4)
-        return r
+            # per-edge row gathers (SURVEY.md §8d bytes) are served mostly by the L2s and the
+            # 256 MiB Infinity Cache, not HBM (PMC: the fabric sees a quarter of them on S0):
+            # the bound is the L2-served random-row gather rate; the HBM figure stays beside it
+            return {"bound": "l2_gather", "achieved": round(ach, 1), "peak": L2_GATHER_GBS, "unit": "GB/s",
+                    "frac": round(ach / L2_GATHER_GBS, 4), **base, "bytes_per_step": int(g["work"]),
+                    "peak_is": "L2-served random-row gather ceiling (MI355X_MICROARCH.md, indexed rows)",
+                    "peak_hbm": PEAK_HBM_GBS, "frac_vs_hbm": round(ach / PEAK_HBM_GBS, 4)}
+        return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(ach / PEAK_HBM_GBS, 4), **base, "bytes_per_step": int(g["work"])}
 
     return groups, roof
 
