@@ -98,6 +98,23 @@ def test_gemm_bf16_rowsum_and_split_k():
     assert torch.equal(a, b)  # deterministic
 
 
+@pytest.mark.parametrize("ta,tb", [(True, False), (False, False), (True, True)])
+def test_gemm_bf16_256_tiles_rowsum_unsplit(ta, tb):
+    """256 x 256 tiles without split-K (>= 256 tiles) in the k-image transpositions (the
+    two-phase kernel), with the row sums of op(A) and a ragged K tail."""
+    from plagnn import ops
+
+    M, N, K = 2056, 8192, 520
+    A = _bf((K, M) if ta else (M, K), 21)
+    B = _bf((N, K) if tb else (K, N), 22)
+    rs = torch.empty(M, device=DEV)
+    got = ops.gemm_bf16(A, B, ta, tb, rowsum=rs, split_k=1).double()
+    ref, mag = _ref(A, B, ta, tb)
+    assert bool(((got - ref).abs() <= 2e-6 * np.sqrt(K) * mag + 1e-30).all())
+    a64 = A.double().t() if ta else A.double()
+    assert bool(((rs.double() - a64.sum(1)).abs() <= 2e-6 * np.sqrt(K) * a64.abs().sum(1)).all())
+
+
 def test_gemm_bf16_rejects_unaligned_extents():
     from plagnn import _lib, ops
 
