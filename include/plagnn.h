@@ -128,8 +128,9 @@ typedef struct pg_csr {
   int64_t n_slots;
   int32_t max_deg;
   int32_t chunk;
-  const int32_t* einv;   /* [nnz] in-CSR only, optional: index of every in-CSR slot in the
-                            transposed CSR (the inverse permutation of its eslot) */
+  const int32_t* einv;   /* [nnz] in-CSR only, optional and unread since ABI 7 (the max
+                            backward's list descriptors sit at in-CSR slots); kept so the
+                            struct layout does not change */
 } pg_csr_t;
 
 /* ---------------- host: graph construction (code/utils.py:44-45) ---------------- */
@@ -430,7 +431,8 @@ const char* pg_last_error_string(void);
 int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-kernel split-K
                          (epilogue without splitk_cnt), no grouped SpMM pair; 6: with fwd_out,
                          pg_spmm_max_bwd[_bf16] takes mask_src >= 0 and does not read it;
-                         PG_ARG_DEAD_NONE */
+                         PG_ARG_DEAD_NONE; 7: pg_spmm_max_bwd reads no einv, smaller
+                         workspace */
 
 #ifdef __cplusplus
 }

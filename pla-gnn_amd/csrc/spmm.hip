@@ -408,23 +408,26 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
 // position p, giving
 //   gfeat[v F + i]  the features, grouped by p (any order inside a group),
 //   dpack[v F + i]  = dout[v][gfeat[v F + i]]   (the upstream gradient in list order),
-//   glist[t]        = {v F + start_p, count_p} for the edge at in-CSR slot ptr[v] + p,
-//                     stored at that edge's index t = einv[slot] in the transposed CSR.
+//   glist[s]        = {v F + start_p, count_p} for the edge at in-CSR slot s = ptr[v] + p
+//                     (a row's descriptors are contiguous: coalesced stores).
 // Rows of in-degree <= kPackWaveMax: one wave per row (wave-private LDS histogram, wave
 // scan, LDS-atomic placement); longer rows: one workgroup per row (block histogram, or a
 // bitonic sort of (p << 16 | f) keys past kHistMax entries).
 // Pass 2 (pull), one wave per source row u: for each out-edge of u, ascending destination
-// v (the transposed CSR order), read its descriptor glist[t] (coalesced over the window)
-// and add dpack[list] (* w) into an LDS row accumulator at gfeat[list]. A list never
+// v (the transposed CSR order), read its descriptor glist[tslot[t]] (the transposed
+// entry's in-CSR slot; loaded a window ahead) and add dpack[list] (* w) into an LDS row accumulator at gfeat[list]. A list never
 // repeats a feature, so one instruction's lanes hit distinct LDS words and every
 // feature's terms are summed in ascending v, the order of the sequential scatter_add_:
-// the order inside a list does not matter. Traffic per edge: one 8-B descriptor and two
-// short contiguous runs (~F/deg entries).
+// the order inside a list does not matter. Traffic per edge: its 4-B slot, one 8-B
+// descriptor and two short contiguous runs (~F/deg entries). (Descriptors stored at the
+// transposed index instead, read coalesced but written scattered by the pack: the cfg2
+// backward 259 vs 256 us per step.)
 constexpr int kHistMax = 4096;
 constexpr int kGroupMaxF = 1024;
 #ifndef PG_BWD_DIRECT
 #define PG_BWD_DIRECT 0
 #endif
+
 struct GPack {
   uint16_t* __restrict__ f16;  // features, grouped by winning position
   float* __restrict__ val;     // their upstream gradients
@@ -463,7 +466,7 @@ __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
 
 template <typename A, typename T>
 __device__ __forceinline__ void pack_short_row(
-    int v, int wave, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
+    int v, int wave, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
     const T* __restrict__ fout, int64_t ldf, GPack gp, int2* __restrict__ glist, int* __restrict__ lds) {
   constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
@@ -498,7 +501,7 @@ __device__ __forceinline__ void pack_short_row(
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int p = lane * B + q;
-    ei[q] = (q < B && p < deg) ? einv[rs + p] : 0;
+    ei[q] = (q < B && p < deg) ? rs + p : 0;
   }
   int* hist = lds + wave * (kPackWaveMax + 4);
   for (int p = lane; p < deg; p += kWave) hist[p] = 0;
@@ -554,7 +557,7 @@ constexpr int pack_wave_ints() { return kPackWaveMax + 4 + NV * 384; }  // hist 
 
 template <int NV, typename A, typename T>
 __device__ __forceinline__ void pack_short_row_v(
-    int v, int wave, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
+    int v, int wave, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
     const T* __restrict__ fout, int64_t ldf, GPack gp, int2* __restrict__ glist, int* __restrict__ lds) {
   const int lane = lane_id();
@@ -584,7 +587,7 @@ __device__ __forceinline__ void pack_short_row_v(
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int p = lane * B + q;
-    ei[q] = (q < B && p < deg) ? einv[rs + p] : 0;
+    ei[q] = (q < B && p < deg) ? rs + p : 0;
   }
   int* hist = lds + wave * pack_wave_ints<NV>();
   uint16_t* lf = reinterpret_cast<uint16_t*>(hist + kPackWaveMax + 4);
@@ -642,7 +645,7 @@ __device__ __forceinline__ void pack_short_row_v(
 
 template <typename A, typename T>
 __device__ __forceinline__ void pack_long_row(
-    int v, const int32_t* __restrict__ ptr, const int32_t* __restrict__ einv,
+    int v, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
     const T* __restrict__ fout, int64_t ldf, GPack gp, int2* __restrict__ glist, int* __restrict__ lds) {
   int* hist = lds;
@@ -688,7 +691,7 @@ __device__ __forceinline__ void pack_long_row(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int p = p0 + j * kBlock;
-        e[j] = p < deg ? einv[rs + p] : 0;
+        e[j] = p < deg ? rs + p : 0;
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -748,7 +751,7 @@ __device__ __forceinline__ void pack_long_row(
     for (int p = threadIdx.x; p < deg; p += kBlock) {
       const int st = lower((uint32_t)p << 16);
       const int en = lower((uint32_t)(p + 1) << 16);
-      glist[einv[rs + p]] = make_int2((int)(vF + st), en - st);
+      glist[rs + p] = make_int2((int)(vF + st), en - st);
     }
     if (threadIdx.x == 0) wsum[0] = lower(0xFFFFFFFFu);
     __syncthreads();
@@ -773,7 +776,7 @@ static_assert(kPackLds >= kWavesPerBlock * (kPackWaveMax + 4), "pack LDS");
 template <typename A, typename T = float, int NV = 0>
 __global__ __launch_bounds__(kBlock) void group_pack_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
-    const int32_t* __restrict__ einv, const A* __restrict__ arg, int64_t lda, int F,
+    const A* __restrict__ arg, int64_t lda, int F,
     const T* __restrict__ dout, int64_t ldd, const T* __restrict__ fout, int64_t ldf,
     GPack gp, int2* __restrict__ glist) {
   constexpr int kLds = NV > 0 && kWavesPerBlock * pack_wave_ints<NV>() > kPackLds
@@ -781,24 +784,32 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
   __shared__ __attribute__((aligned(16))) int lds[kLds];
   const int b = blockIdx.x;
   if (b < n_long) {
-    pack_long_row<A, T>(rows ? rows[b].x : b, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gp, glist, lds);
+    pack_long_row<A, T>(rows ? rows[b].x : b, ptr, arg, lda, F, dout, ldd, fout, ldf, gp, glist, lds);
   } else {
     const int wave = wave_id_uniform();
     const int v = (b - n_long) * kWavesPerBlock + wave;
     if (v < n_rows)
     {
       if constexpr (NV > 0)
-        pack_short_row_v<NV, A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gp, glist, lds);
+        pack_short_row_v<NV, A, T>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, gp, glist, lds);
       else
-        pack_short_row<A, T>(v, wave, ptr, einv, arg, lda, F, dout, ldd, fout, ldf, gp, glist, lds);
+        pack_short_row<A, T>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, gp, glist, lds);
     }
   }
 }
 
-__global__ __launch_bounds__(kBlock) void invert_slots_kernel(const int32_t* __restrict__ tslot,
-                                                              int64_t nnz, int32_t* __restrict__ einv) {
-  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < nnz; t += (int64_t)gridDim.x * kBlock)
-    einv[tslot[t]] = (int32_t)t;
+#ifndef PG_PULL_DENSE
+#define PG_PULL_DENSE 0
+#endif
+// inclusive max-scan over the 64 lanes (DPP: row shifts, then row broadcasts 15 and 31)
+__device__ __forceinline__ int wave_incl_max(int x) {
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return x;
 }
 
 template <bool HAS_W, typename T = float>
@@ -813,10 +824,16 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
 #endif
   constexpr int U = PG_PULL_U;  // list segments in flight per wave
   __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
+#if PG_PULL_DENSE
+  __shared__ int marks[kWavesPerBlock][kWave];
+#endif
   const int wave = wave_id_uniform();
   const int it = blockIdx.x * kWavesPerBlock + wave;
   if (it >= n_items) return;
   float* acc = accs[wave];
+#if PG_PULL_DENSE
+  volatile int* mk = marks[wave];
+#endif
   const int4 item = items[it];
   const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
   const int lane = lane_id();
@@ -829,14 +846,74 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   // nothing. Segment t belongs to the edge i with excl_i <= t < excl_i + nseg_i, i.e.
   // i = popcount(ballot(excl <= t)) - 1.
   // the next window's descriptors are loaded while the current window is processed
-  int2 gl_next = glist[t0 + min(lane, max(0, t1 - t0 - 1))];
+  // descriptors sit at the in-CSR slots (the pack's stores are coalesced): tslot two
+  // windows ahead, the descriptors one window ahead
+  int ts_cur = tslot[t0 + min(lane, max(0, t1 - t0 - 1))];
+  int2 gl_next = glist[ts_cur];
+  int ts_next = t0 + kWave < t1 ? tslot[t0 + kWave + min(lane, t1 - t0 - kWave - 1)] : 0;
   for (int tw = t0; tw < t1; tw += kWave) {
     const int nw = min(kWave, t1 - tw);
-    const int tl = tw + min(lane, nw - 1);
     const int2 gl = gl_next;
-    if (tw + kWave < t1) gl_next = glist[tw + kWave + min(lane, t1 - tw - kWave - 1)];
     float wv = 1.f;
-    if constexpr (HAS_W) wv = ew[tslot[tl]];
+    if constexpr (HAS_W) wv = ew[ts_cur];
+    if (tw + kWave < t1) {
+      gl_next = glist[ts_next];
+      ts_cur = ts_next;
+      if (tw + 2 * kWave < t1) ts_next = tslot[tw + 2 * kWave + min(lane, t1 - tw - 2 * kWave - 1)];
+    }
+#if PG_PULL_DENSE
+    // Dense segments: the window's lists laid end to end (edge-major, ascending
+    // destination) and cut into 64-entry segments, so a segment carries entries of several
+    // short lists. Lane x of a segment finds its edge by an inclusive max-scan over start
+    // markers (edge i marks its first flat position); entries of different lists may hit
+    // the same feature inside one instruction, so they are added with LDS float atomics,
+    // which apply one instruction's lanes in ascending lane order = ascending destination.
+    const int c = lane < nw ? gl.y : 0;
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    const int excl = incl - c;
+    const int total = bcast(incl, kWave - 1);
+    const int ebase = gl.x - excl;  // entry at flat position x of this lane's list: ebase + x
+    for (int p0 = 0; p0 < total; p0 += U * kWave) {
+      // the edge holding flat position p0 (carried into the first segment's scan)
+      int carry = 63 - __clzll(__ballot(c > 0 && excl <= p0));
+      int me[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int ps = p0 + u * kWave;
+        me[u] = carry;
+        if (ps < total) {
+          mk[lane] = -1;
+          __builtin_amdgcn_wave_barrier();
+          if (c > 0 && excl >= ps && excl < ps + kWave) mk[excl - ps] = lane;
+          __builtin_amdgcn_wave_barrier();
+          int m = mk[lane];
+          __builtin_amdgcn_wave_barrier();
+          m = max(wave_incl_max(m), carry);
+          carry = bcast(m, kWave - 1);
+          me[u] = m;
+        }
+      }
+      int fe[U];
+      float de[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int x = p0 + u * kWave + lane;
+        const int addr = __shfl(ebase, me[u]) + x;
+        fe[u] = 0;
+        de[u] = 0.f;
+        if (x < total) gp.get(addr, fe[u], de[u]);
+        if constexpr (HAS_W) de[u] = __shfl(wv, me[u]) * de[u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (p0 + u * kWave + lane < total) atomicAdd(&acc[fe[u]], de[u]);
+    }
+#else
     const int nseg = lane < nw ? (gl.y + kWave - 1) / kWave : 0;
     int incl = nseg;
 #pragma unroll
@@ -873,6 +950,7 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
         }
       }
     }
+#endif
   }
   wave_lds_sync();
   if (slot < 0) {
@@ -1307,7 +1385,7 @@ int pg_spmm_max_fwd_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t 
 }
 
 // [split-row partials][grouped path: list features N x F u16 | list values N x F f32 |
-//  glist nnz x int2 | einv nnz x int32 (used when g->einv is NULL)]
+//  glist nnz x int2]
 static size_t bwd_partials_bytes(const pg_csr_t* gt, int64_t F) {
   return gt->n_slots > 0 ? round_up(gt->n_slots * ws_ld(F) * 4, 256) : 0;
 }
@@ -1317,8 +1395,7 @@ size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
   size_t b = bwd_partials_bytes(gt, F);
   if (F <= kGroupMaxF) {
     const int64_t N = gt->n_cols;
-    b += round_up(N * F * 2, 256) + round_up(N * F * 4, 256) + round_up(gt->nnz * 8, 256) +
-         round_up(gt->nnz * 4, 256);
+    b += round_up(N * F * 2, 256) + round_up(N * F * 4, 256) + round_up(gt->nnz * 8, 256);
   }
   return b;
 }
@@ -1369,14 +1446,6 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     p += round_up(N * F * 4, 256);
     int2* glist = (int2*)p;
     p += round_up(g->nnz * 8, 256);
-    const int32_t* einv = g->einv;
-    if (!einv) {
-      int32_t* e = (int32_t*)p;
-      const int blocks = (int)std::min<int64_t>(4096, (g->nnz + kBlock - 1) / kBlock);
-      if (blocks > 0)
-        hipLaunchKernelGGL(invert_slots_kernel, dim3(blocks), dim3(kBlock), 0, st, gt->eslot, g->nnz, e);
-      einv = e;
-    }
     const auto* arg16 = (const uint16_t*)argpos;
     // rows past kPackWaveMax: the schedule's split rows when its chunk guarantees they are
     // a superset, else every row
@@ -1392,7 +1461,7 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     auto pack = [&](auto nv_c) {
       constexpr int NV = decltype(nv_c)::value;
       hipLaunchKernelGGL((group_pack_kernel<uint16_t, T, NV>), pgrid, dim3(kBlock), 0, st, prow, n_long, (int)N,
-                         g->ptr, einv, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, gp, glist);
+                         g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, gp, glist);
       return PG_OK;
     };
     if (vec) dispatch_nc_vec((int)((F + 255) / 256), pack);
