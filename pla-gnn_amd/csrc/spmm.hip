@@ -435,6 +435,31 @@ struct GPack {
   __device__ __forceinline__ void get(int64_t pos, int& f, float& d) const { f = f16[pos]; d = val[pos]; }
 };
 
+#ifndef PG_SCAN_DPP
+#define PG_SCAN_DPP 1
+#endif
+// inclusive prefix sum over the 64 lanes: DPP row shifts, then row broadcasts 15 and 31
+// (six VALU ops; the __shfl_up form is six dependent ds_bpermute round trips)
+__device__ __forceinline__ int wave_incl_add(int x) {
+#if PG_SCAN_DPP
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+#else
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  return x;
+#endif
+}
+
 __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   const int per = (n + kBlock - 1) / kBlock;
   const int b = threadIdx.x * per;
@@ -443,11 +468,7 @@ __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   for (int i = 0; i < per; ++i)
     if (b + i < n) local += s[b + i];
   int x = local;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
+  x = wave_incl_add(x);
   if (lane == kWave - 1) wsum[wave] = x;
   __syncthreads();
   int pre = 0;
@@ -519,11 +540,7 @@ __device__ __forceinline__ void pack_short_row(
     local += c[q];
   }
   int x = local;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
+  x = wave_incl_add(x);
   int run = x - local;
   const int vF = v * F;
 #pragma unroll
@@ -609,11 +626,7 @@ __device__ __forceinline__ void pack_short_row_v(
     local += cq[q];
   }
   int x = local;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
+  x = wave_incl_add(x);
   int run = x - local;
   const int vF = v * F;
   wave_lds_sync();
@@ -798,20 +811,6 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
   }
 }
 
-#ifndef PG_PULL_DENSE
-#define PG_PULL_DENSE 0
-#endif
-// inclusive max-scan over the 64 lanes (DPP: row shifts, then row broadcasts 15 and 31)
-__device__ __forceinline__ int wave_incl_max(int x) {
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));  // row_shr:1
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));  // row_shr:2
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));  // row_shr:4
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));  // row_shr:8
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return x;
-}
-
 template <bool HAS_W, typename T = float>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const float* __restrict__ ew, const int32_t* __restrict__ tslot,
@@ -822,18 +821,15 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
 #ifndef PG_PULL_U
 #define PG_PULL_U 8  // measured on S0 (scripts/spmm_variants.sh): 4-8 best, 16 +6 %, 32 +25 %
 #endif
+#ifndef PG_PULL_Q
+#define PG_PULL_Q 1
+#endif
   constexpr int U = PG_PULL_U;  // list segments in flight per wave
   __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
-#if PG_PULL_DENSE
-  __shared__ int marks[kWavesPerBlock][kWave];
-#endif
   const int wave = wave_id_uniform();
   const int it = blockIdx.x * kWavesPerBlock + wave;
   if (it >= n_items) return;
   float* acc = accs[wave];
-#if PG_PULL_DENSE
-  volatile int* mk = marks[wave];
-#endif
   const int4 item = items[it];
   const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
   const int lane = lane_id();
@@ -861,96 +857,51 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
       ts_cur = ts_next;
       if (tw + 2 * kWave < t1) ts_next = tslot[tw + 2 * kWave + min(lane, t1 - tw - 2 * kWave - 1)];
     }
-#if PG_PULL_DENSE
-    // Dense segments: the window's lists laid end to end (edge-major, ascending
-    // destination) and cut into 64-entry segments, so a segment carries entries of several
-    // short lists. Lane x of a segment finds its edge by an inclusive max-scan over start
-    // markers (edge i marks its first flat position); entries of different lists may hit
-    // the same feature inside one instruction, so they are added with LDS float atomics,
-    // which apply one instruction's lanes in ascending lane order = ascending destination.
-    const int c = lane < nw ? gl.y : 0;
-    int incl = c;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const int y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
-    const int excl = incl - c;
-    const int total = bcast(incl, kWave - 1);
-    const int ebase = gl.x - excl;  // entry at flat position x of this lane's list: ebase + x
-    for (int p0 = 0; p0 < total; p0 += U * kWave) {
-      // the edge holding flat position p0 (carried into the first segment's scan)
-      int carry = 63 - __clzll(__ballot(c > 0 && excl <= p0));
-      int me[U];
+    // Q pieces of PW = 64 / Q lanes per load instruction: lane group q of an instruction
+    // carries its own list piece, so one load brings Q short lists; their LDS adds run in
+    // Q passes, piece by piece in list order (pieces of different lists may share features).
+    constexpr int Q = PG_PULL_Q, PW = kWave / Q;
+    const int qh = lane / PW, ql = lane % PW;
+    const int nseg = lane < nw ? (gl.y + PW - 1) / PW : 0;
+    int incl = nseg;
+    incl = wave_incl_add(incl);
+    const int excl = incl - nseg;
+    const int nseg_all = bcast(incl, kWave - 1);
+    for (int s0 = 0; s0 < nseg_all; s0 += U * Q) {
+      const int nv = min(U * Q, nseg_all - s0);
+      int fe[U], ne[U];
+      float de[U], we[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int ps = p0 + u * kWave;
-        me[u] = carry;
-        if (ps < total) {
-          mk[lane] = -1;
-          __builtin_amdgcn_wave_barrier();
-          if (c > 0 && excl >= ps && excl < ps + kWave) mk[excl - ps] = lane;
-          __builtin_amdgcn_wave_barrier();
-          int m = mk[lane];
-          __builtin_amdgcn_wave_barrier();
-          m = max(wave_incl_max(m), carry);
-          carry = bcast(m, kWave - 1);
-          me[u] = m;
+        int base = 0, n = 0;
+        float w = 1.f;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int t = s0 + min(u * Q + q, nv - 1);
+          const int i = __popcll(__ballot(excl <= t)) - 1;
+          const int seg = t - bcast(excl, i);
+          const int bq = bcast(gl.x, i) + seg * PW;
+          const int nq = u * Q + q < nv ? min(PW, bcast(gl.y, i) - seg * PW) : 0;
+          float wq = 1.f;
+          if constexpr (HAS_W) wq = bcastf(wv, i);
+          if (Q == 1 || qh == q) {
+            base = bq;
+            n = nq;
+            w = wq;
+          }
         }
-      }
-      int fe[U];
-      float de[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int x = p0 + u * kWave + lane;
-        const int addr = __shfl(ebase, me[u]) + x;
+        ne[u] = n;
+        we[u] = w;
         fe[u] = 0;
         de[u] = 0.f;
-        if (x < total) gp.get(addr, fe[u], de[u]);
-        if constexpr (HAS_W) de[u] = __shfl(wv, me[u]) * de[u];
+        if (ql < n) gp.get(base + ql, fe[u], de[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (p0 + u * kWave + lane < total) atomicAdd(&acc[fe[u]], de[u]);
-    }
-#else
-    const int nseg = lane < nw ? (gl.y + kWave - 1) / kWave : 0;
-    int incl = nseg;
 #pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const int y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
+        for (int q = 0; q < Q; ++q)
+          if ((Q == 1 || qh == q) && ql < ne[u]) acc[fe[u]] += HAS_W ? we[u] * de[u] : de[u];
     }
-    const int excl = incl - nseg;
-    const int nseg_all = bcast(incl, kWave - 1);
-    for (int s0 = 0; s0 < nseg_all; s0 += U) {
-      const int nv = min(U, nseg_all - s0);
-      int fe[U], ie[U], ne[U];
-      float de[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int t = s0 + min(u, nv - 1);
-        const int i = __popcll(__ballot(excl <= t)) - 1;
-        const int seg = t - bcast(excl, i);
-        const int base = bcast(gl.x, i) + seg * kWave;
-        const int n = min(kWave, bcast(gl.y, i) - seg * kWave);
-        ie[u] = i;
-        ne[u] = n;
-        const bool on = lane < n;
-        fe[u] = 0;
-        de[u] = 0.f;
-        if (on) gp.get(base + lane, fe[u], de[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (u < nv && lane < ne[u]) {
-          float w = 1.f;
-          if constexpr (HAS_W) w = bcastf(wv, ie[u]);
-          acc[fe[u]] += HAS_W ? w * de[u] : de[u];
-        }
-      }
-    }
-#endif
   }
   wave_lds_sync();
   if (slot < 0) {

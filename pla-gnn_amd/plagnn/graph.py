@@ -58,8 +58,8 @@ def _schedule(ptr: np.ndarray, chunk: int):
 class HostCsr:
     """One CSR direction with its schedule, in host memory (numpy int32)."""
 
-    def __init__(self, ptr, col, eslot, n_cols: int, chunk: int, epos=None, einv=None):
-        self.ptr, self.col, self.eslot, self.epos, self.einv = ptr, col, eslot, epos, einv
+    def __init__(self, ptr, col, eslot, n_cols: int, chunk: int, epos=None):
+        self.ptr, self.col, self.eslot, self.epos = ptr, col, eslot, epos
         self.n_rows = len(ptr) - 1
         self.n_cols = int(n_cols)
         self.nnz = int(len(col))
@@ -77,7 +77,6 @@ class DeviceCsr:
 
         self.device = device
         self.ptr, self.col, self.eslot, self.epos = up(h.ptr), up(h.col), up(h.eslot), up(h.epos)
-        self.einv = up(h.einv)
         self.items, self.merges = up(h.items), up(h.merges)
         self.n_rows, self.n_cols, self.nnz = h.n_rows, h.n_cols, h.nnz
         self.n_items, self.n_merges, self.n_slots = h.n_items, h.n_merges, h.n_slots
@@ -107,7 +106,7 @@ class DeviceCsr:
         s.n_slots = self.n_slots
         s.max_deg = self.max_deg
         s.chunk = self.chunk
-        s.einv = _lib.ptr(self.einv)
+        s.einv = 0  # unread since ABI 7
         return s
 
 
@@ -137,10 +136,7 @@ class CSRGraph:
         self.num_nodes = n
         self.num_edges = E
         self.eid = eid  # in-CSR slot -> edge id
-        # in-CSR slot -> position in the transposed CSR (the inverse of tslot)
-        einv = np.empty(max(E, 1), np.int32)
-        einv[tslot[:E]] = np.arange(E, dtype=np.int32)
-        self.fwd = HostCsr(ptr, col, None, n, chunk, einv=einv[:E])
+        self.fwd = HostCsr(ptr, col, None, n, chunk)
         if chunk_bwd is None:
             chunk_bwd = default_chunk_bwd(n)
         self.bwd = HostCsr(tptr, tcol[:E], tslot[:E], n, min(chunk, chunk_bwd), epos=tpos[:E])

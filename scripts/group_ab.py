@@ -28,7 +28,7 @@ def main():
     for _ in range(5):
         e.step()
     torch.cuda.synchronize()
-    groups = tuple(os.environ.get("GROUPS", "gemm,spmm_max_fwd,spmm_max_bwd").split(","))
+    groups = tuple(os.environ.get("PG_GROUPS", "gemm,spmm_max_fwd,spmm_max_bwd").split(","))
     res = {g: [] for g in groups}
     for _ in range(int(os.environ.get("ROUNDS", "3"))):
         gt = e.group_times(groups=groups, reps=10)
