@@ -583,11 +583,21 @@ __device__ __forceinline__ void pack_short_row_v(
   if (deg > kPackWaveMax || deg == 0) return;
   int a[NV][4];
   float d[NV][4];
+  // straight-line loads at clamped columns (F % 4 == 0 here), masked afterwards: no branch
+  // between the record and gradient loads, so both are in flight before the first wait
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
     const int f = (c * kWave + lane) * 4;
-    load_arg<4, A>(arg + (int64_t)v * lda, f, F, a[c]);
-    load_tile<4, T>(dout + (int64_t)v * ldd, f, F, d[c], 0.f);
+    const int fc = min(f, F - 4);
+    int ac[4];
+    float dc[4];
+    load_arg<4, A>(arg + (int64_t)v * lda, fc, F, ac);
+    load_tile<4, T>(dout + (int64_t)v * ldd, fc, F, dc, 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[c][i] = f < F ? ac[i] : arg_none<A>();
+      d[c][i] = f < F ? dc[i] : 0.f;
+    }
   }
   if (fout) {  // a zero maximum: its winner's relu mask is 0, the entry contributes nothing
 #pragma unroll
@@ -651,8 +661,15 @@ __device__ __forceinline__ void pack_short_row_v(
       }
   wave_lds_sync();
   const int total = __builtin_amdgcn_readlane(x, kWave - 1);
-  for (int i = lane; i < total; i += kWave) {
-    gp.put(vF + i, lf[i], lv[i]);
+  // 4 entries per lane: 8-B feature and 16-B value stores (vF and the LDS images are
+  // 16-B aligned: F % 4 == 0 on this path)
+  for (int i = lane * 4; i < total; i += 4 * kWave) {
+    if (i + 4 <= total) {
+      *reinterpret_cast<uint2*>(gp.f16 + vF + i) = *reinterpret_cast<const uint2*>(lf + i);
+      *reinterpret_cast<float4*>(gp.val + vF + i) = *reinterpret_cast<const float4*>(lv + i);
+    } else {
+      for (int k = i; k < total; ++k) gp.put(vF + k, lf[k], lv[k]);
+    }
   }
 }
 
@@ -821,9 +838,6 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
 #ifndef PG_PULL_U
 #define PG_PULL_U 8  // measured on S0 (scripts/spmm_variants.sh): 4-8 best, 16 +6 %, 32 +25 %
 #endif
-#ifndef PG_PULL_Q
-#define PG_PULL_Q 1
-#endif
   constexpr int U = PG_PULL_U;  // list segments in flight per wave
   __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
   const int wave = wave_id_uniform();
@@ -857,50 +871,37 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
       ts_cur = ts_next;
       if (tw + 2 * kWave < t1) ts_next = tslot[tw + 2 * kWave + min(lane, t1 - tw - 2 * kWave - 1)];
     }
-    // Q pieces of PW = 64 / Q lanes per load instruction: lane group q of an instruction
-    // carries its own list piece, so one load brings Q short lists; their LDS adds run in
-    // Q passes, piece by piece in list order (pieces of different lists may share features).
-    constexpr int Q = PG_PULL_Q, PW = kWave / Q;
-    const int qh = lane / PW, ql = lane % PW;
-    const int nseg = lane < nw ? (gl.y + PW - 1) / PW : 0;
+    const int nseg = lane < nw ? (gl.y + kWave - 1) / kWave : 0;
     int incl = nseg;
     incl = wave_incl_add(incl);
     const int excl = incl - nseg;
     const int nseg_all = bcast(incl, kWave - 1);
-    for (int s0 = 0; s0 < nseg_all; s0 += U * Q) {
-      const int nv = min(U * Q, nseg_all - s0);
-      int fe[U], ne[U];
-      float de[U], we[U];
+    for (int s0 = 0; s0 < nseg_all; s0 += U) {
+      const int nv = min(U, nseg_all - s0);
+      int fe[U], ie[U], ne[U];
+      float de[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        int base = 0, n = 0;
-        float w = 1.f;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          const int t = s0 + min(u * Q + q, nv - 1);
-          const int i = __popcll(__ballot(excl <= t)) - 1;
-          const int seg = t - bcast(excl, i);
-          const int bq = bcast(gl.x, i) + seg * PW;
-          const int nq = u * Q + q < nv ? min(PW, bcast(gl.y, i) - seg * PW) : 0;
-          float wq = 1.f;
-          if constexpr (HAS_W) wq = bcastf(wv, i);
-          if (Q == 1 || qh == q) {
-            base = bq;
-            n = nq;
-            w = wq;
-          }
-        }
+        const int t = s0 + min(u, nv - 1);
+        const int i = __popcll(__ballot(excl <= t)) - 1;
+        const int seg = t - bcast(excl, i);
+        const int base = bcast(gl.x, i) + seg * kWave;
+        const int n = min(kWave, bcast(gl.y, i) - seg * kWave);
+        ie[u] = i;
         ne[u] = n;
-        we[u] = w;
-        fe[u] = 0;
-        de[u] = 0.f;
-        if (ql < n) gp.get(base + ql, fe[u], de[u]);
+        // every lane loads (lanes past n a valid entry of the same segment): straight-line
+        // loads, so the waits are counted instead of a vmcnt(0) behind each branch, which
+        // also waited out the next window's descriptor prefetch
+        gp.get(base + min(lane, n - 1), fe[u], de[u]);
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-          if ((Q == 1 || qh == q) && ql < ne[u]) acc[fe[u]] += HAS_W ? we[u] * de[u] : de[u];
+      for (int u = 0; u < U; ++u) {
+        if (u < nv && lane < ne[u]) {
+          float w = 1.f;
+          if constexpr (HAS_W) w = bcastf(wv, ie[u]);
+          acc[fe[u]] += HAS_W ? w * de[u] : de[u];
+        }
+      }
     }
   }
   wave_lds_sync();
