@@ -12,7 +12,8 @@
 //
 // Tiling: BM x BN per 256-thread workgroup, 2 x 2 waves of (BM/2) x (BN/2) = TM x TN MFMA
 // tiles of 32 x 32, one MFMA k-step (16 k) per K step. K tiles go global -> registers
-// (float4 per thread and unit, issued one K step ahead), are split in registers and
+// (float4 per thread and unit, issued one K step ahead; two for tiles of <= 128 x 64, the
+// loads unconditional so the waits are counted), are split in registers and
 // stored as three bf16 images per operand (ds_write_b64 per piece) into the other half of
 // a double-buffered LDS array: one barrier per K step.
 // Images (u16 units), per piece:
@@ -92,6 +93,8 @@ __device__ __forceinline__ void split4(const float4 v, uint2 (&out)[3]) {
 
 // One operand's K tile: ROWS x KS, float4 units; row image unit = (row, 4 k), k image unit
 // = (k, 4 rows).
+__device__ float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written
+
 template <int ROWS, bool KMAJ>
 struct Stage {
   static constexpr int UNITS = ROWS * KS / 4;
@@ -116,13 +119,12 @@ struct Stage {
       int row, k;
       unit_pos(tid + i * NT, row, k);
       const int gk = k0 + k;
-      if (gk < kz1) {
-        const float* p = !KMAJ ? P + (int64_t)min(r0 + row, R - 1) * ld + gk
-                               : P + (int64_t)gk * ld + min(r0 + row, R - 4);
-        v[i] = *reinterpret_cast<const float4*>(p);
-      } else {
-        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      // straight-line: a unit past kz1 reads a 16-B zero word in global memory instead of
+      // being zeroed behind a branch, so every load is unconditional and the compiler
+      // counts the waits
+      const float* p = !KMAJ ? P + (int64_t)min(r0 + row, R - 1) * ld + gk
+                             : P + (int64_t)gk * ld + min(r0 + row, R - 4);
+      v[i] = *reinterpret_cast<const float4*>(gk < kz1 ? p : g_zero4);
     }
   }
   // split and store the three pieces (images of IMG u16 each, consecutive)
@@ -232,8 +234,13 @@ __device__ unsigned long long pg_x3_stamp[64][66][4];
   } while (0)
 #endif
 
+// Tiles of <= 128 x 64 keep two K tiles in flight in registers (DEPTH 2), capped at 128
+// registers per lane so four workgroups still fit a CU (their LDS allows four).
+template <int BM, int BN>
+constexpr int x3_depth() { return BM * BN <= 128 * 64 ? 2 : 1; }
+
 template <int BM, int BN, bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(NT)
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_depth<BM, BN>() == 2 ? 4 : 1)))
 void gemm_x3_kernel(
     int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
@@ -304,7 +311,47 @@ void gemm_x3_kernel(
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
       }
   };
-  if (nk > 0) {
+  if (x3_depth<BM, BN>() == 2 && nk > 0) {
+    // tiles two K steps ahead in registers (two stage slots, the loop unrolled by two so
+    // the slots are static): step t loads tile t + 2 (clamped to the last tile, so the
+    // loads are unconditional) into the slot tile t left, and stores tile t + 1. Measured
+    // on the cfg2 step: GEMM 916 -> 902 us (the split waits for a tile issued a step
+    // earlier instead of during the same step's MFMAs)
+    Stage<BM, AK> sa2;
+    Stage<BN, BKM> sb2;
+    sa.load(A, lda, m0, M, kz0, kz1, tid);
+    sb.load(B, ldb, n0, N, kz0, kz1, tid);
+    const int k1c = kz0 + min(1, nk - 1) * KS;
+    sa2.load(A, lda, m0, M, k1c, kz1, tid);
+    sb2.load(B, ldb, n0, N, k1c, kz1, tid);
+    if (do_rs) sa.rowsum(rs);
+    sa.template store<IA>(lds, tid);
+    sb.template store<IB>(lds + 3 * IA, tid);
+    __syncthreads();
+    // loads sit outside every branch (only MFMAs and stores are conditional), so the
+    // compiler's wait counts stay exact across the loop
+    auto kstep = [&](int t, Stage<BM, AK>& la, Stage<BN, BKM>& lb, Stage<BM, AK>& na, Stage<BN, BKM>& nb) {
+      const int cur = t & 1;
+      const int kl = kz0 + min(t + 2, nk - 1) * KS;
+      la.load(A, lda, m0, M, kl, kz1, tid);
+      lb.load(B, ldb, n0, N, kl, kz1, tid);
+      if (t < nk) {
+        const uint16_t* As = lds + cur * BUF;
+        mfmas(As, As + 3 * IA);
+      }
+      if (t + 1 < nk) {
+        if (do_rs) na.rowsum(rs);
+        uint16_t* nx = lds + (cur ^ 1) * BUF;
+        na.template store<IA>(nx, tid);
+        nb.template store<IB>(nx + 3 * IA, tid);
+      }
+      __syncthreads();
+    };
+    for (int t = 0; t < nk; t += 2) {
+      kstep(t, sa, sb, sa2, sb2);
+      kstep(t + 1, sa2, sb2, sa, sb);
+    }
+  } else if (nk > 0) {
     X3_STAMP(0, 0);
     sa.load(A, lda, m0, M, kz0, kz1, tid);
     sb.load(B, ldb, n0, N, kz0, kz1, tid);
