@@ -379,7 +379,9 @@ int pg_adam_apply(float* param, const float* grad, float* exp_avg, float* exp_av
   if (n == 0) return pg::ok();
   if (!param || !grad || !exp_avg || !exp_avg_sq)
     return pg::set_error(PG_ERR_INVALID, "pg_adam_apply: NULL buffer");
-  hipLaunchKernelGGL(adam_apply_kernel, dim3(grid_1d(n, 2048)), dim3(kBlock), 0, (hipStream_t)stream,
+  // one element per thread (up to 2^15 blocks): every thread's four loads are in flight at
+  // once instead of 2-3 dependent grid-stride rounds
+  hipLaunchKernelGGL(adam_apply_kernel, dim3(grid_1d(n, 32768)), dim3(kBlock), 0, (hipStream_t)stream,
                      param, grad, exp_avg, exp_avg_sq, n, state, (float)beta1, (float)beta2,
                      (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, (float)weight_decay);
   return hip_status("pg_adam_apply");

@@ -200,8 +200,18 @@ __global__ __launch_bounds__(64 * kMaxC) void head_final_kernel(const float* __r
   const int set = blockIdx.x, c = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t ns = set == 0 ? n_train : n_val;
   float s = 0.f;
-  if (c < C)
-    for (int b = lane; b < nb; b += 64) s += part[((int64_t)set * C + c) * nb + b];
+  if (c < C) {
+    // 8 blocks' loads in flight per lane, summed in the same order as one at a time
+    const float* pp = part + ((int64_t)set * C + c) * nb;
+    for (int b0 = lane; b0 < nb; b0 += 8 * 64) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = pp[min(b0 + e * 64, nb - 1)];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (b0 + e * 64 < nb) s += v[e];
+    }
+  }
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if (lane == 0 && c < C) cls[c] = ns > 0 ? -s / (float)ns : 0.f;
   __syncthreads();
