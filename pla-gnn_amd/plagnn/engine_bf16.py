@@ -32,6 +32,9 @@ LEAKY_SLOPE = ops.LEAKY_SLOPE
 
 class TrainEngineBF16(TrainEngine):
     WIDTH_ALIGN = 8
+    # the stacked input-gradient weights as [Fi][Fo + Fi] (B^T, a row image: the A B^T
+    # ping-pong kernel of pg_gemm_bf16 takes the product) instead of [Fo + Fi][Fi] (a k image)
+    STACK_T = True
 
     # ------------------------------------------------------------------ buffers
     def _alloc_buffers(self, features: torch.Tensor) -> None:
@@ -64,7 +67,10 @@ class TrainEngineBF16(TrainEngine):
             Fi, Fo = pd[l], pd[l + 1]
             wl.add(f"conv{l + 1}.Wpool", (Fi, Fi))
             wl.add(f"conv{l + 1}.Wcat", (Fo, 2 * Fi))
-            wl.add(f"conv{l + 1}.Wstack", (Fo + Fi, Fi))  # [Wself ; Wpool]
+            if self.STACK_T:
+                wl.add(f"conv{l + 1}.WstackT", (Fi, Fo + Fi))  # [Wself ; Wpool]^T
+            else:
+                wl.add(f"conv{l + 1}.Wstack", (Fo + Fi, Fi))  # [Wself ; Wpool]
         wl.add("liner1.W", (pd[-2], pd[-3]))
         idx = np.full(wl.size, -1, np.int64)
         flat_ids = self.flat_layout.views(torch.arange(self.flat_layout.size))  # flat index of every entry
@@ -85,7 +91,11 @@ class TrainEngineBF16(TrainEngine):
             wc = ids(p + "Wcat", (Fo, 2 * Fi))
             put(p + "Wpool", wp)
             put(p + "Wcat", wc)
-            put(p + "Wstack", np.concatenate([wc[:, :Fi], wp], axis=0))
+            stack = np.concatenate([wc[:, :Fi], wp], axis=0)
+            if self.STACK_T:
+                put(p + "WstackT", np.ascontiguousarray(stack.T))
+            else:
+                put(p + "Wstack", stack)
         put("liner1.W", ids("liner1.W", (pd[-2], pd[-3])))
         self.wb_layout = wl
         self.wb_map = torch.from_numpy(idx.astype(np.int32)).to(self.device)
@@ -189,8 +199,12 @@ class TrainEngineBF16(TrainEngine):
                        tag=f"gemm.wgrad.pool.l{l + 1}")
             if l > 0:
                 # dH = ([dY | dP] [Wself ; Wpool]) * leaky'(H) -> the lower layer's dY
-                self._gemm(DYP, W[p + "Wstack"], self.DYP[l - 1][:, :Fi], act=LEAKY, dact=HM[:, :Fi],
-                           tag=f"gemm.dgrad.stack.l{l + 1}")
+                if self.STACK_T:
+                    self._gemm(DYP, W[p + "WstackT"], self.DYP[l - 1][:, :Fi], transb=True, act=LEAKY,
+                               dact=HM[:, :Fi], tag=f"gemm.dgrad.stack.l{l + 1}")
+                else:
+                    self._gemm(DYP, W[p + "Wstack"], self.DYP[l - 1][:, :Fi], act=LEAKY, dact=HM[:, :Fi],
+                               tag=f"gemm.dgrad.stack.l{l + 1}")
 
     def adam(self) -> None:
         super().adam()

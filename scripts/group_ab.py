@@ -21,6 +21,9 @@ def main():
     cfg = os.environ.get("CONFIG", "cfg2")
     wl = W.build(cfg, device="cuda")
     Engine = plagnn.TrainEngineBF16 if wl.bf16 else plagnn.TrainEngine
+    if wl.bf16 and os.environ.get("PG_STACK_T") is not None:  # A/B of the stacked-weight layout
+        plagnn.TrainEngineBF16.STACK_T = os.environ["PG_STACK_T"] == "1"
+        label += f"+stackT{os.environ['PG_STACK_T']}"
     e = Engine(wl.graph(), torch.from_numpy(wl.ds.feat), torch.from_numpy(wl.ds.loc.astype(np.float32)),
                wl.dims, wl.class_weight, wl.train_index, wl.val_index, lr=5e-5, device="cuda",
                edge_weight=wl.edge_weight)
