@@ -11,8 +11,11 @@ cp gpurun_out/prof_$TAG.json $DST/bench_default_under_rocprof.json
 cp $SRC.groups.json $DST/rocprof_groups_default_bench.json
 cp $SRC.groups.txt $DST/rocprof_groups_default_bench.txt
 HEAD=$(python3 -c "import json;print(json.loads(open('gpurun_out/prof_$TAG.json').read().splitlines()[-1])['pid'])")
-for f in $SRC/*_kernel_stats.csv; do
-  pid=$(basename $f _kernel_stats.csv)
+# only the processes of the last profiled run (gpurun_out/ keeps earlier runs' files too)
+PIDS=$(sed -n 's/^# process \([0-9]*\).*/\1/p' $SRC.groups.txt)
+for pid in $PIDS; do
+  f=$SRC/${pid}_kernel_stats.csv
+  [ -f $f ] || continue
   if [ "$pid" = "$HEAD" ]; then cp $f $DST/rocprof_kernel_stats_cfg2_headline.csv
   else cp $f $DST/rocprof_kernel_stats_child_${pid}.csv; fi
 done
