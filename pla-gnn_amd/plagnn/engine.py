@@ -75,6 +75,7 @@ class _Flat:
 
 
 class TrainEngine:
+    REDUCE_INLINE = False  # True: each split-K combine right after its partials (A/B knob)
     WIDTH_ALIGN = 4  # every padded width is a multiple of this
     _cur = ""                      # launch site being issued (_t)
     _filter: Optional[str] = None  # group_times: issue only this launch group
@@ -436,6 +437,8 @@ class TrainEngine:
         j.ws, j.split_k, j.M, j.N = ptr(slab), used.value, M, N
         j.alpha, j.beta, j.C, j.ldc, j.rowsum = 1.0, beta, ptr(C), C.stride(0), ptr(rowsum)
         self._jobs.append(j)
+        if self.REDUCE_INLINE:  # combine now, while the slabs are still in the caches
+            self._reduce_deferred()
 
     def _reduce_deferred(self) -> None:
         jobs, self._jobs = self._jobs, []

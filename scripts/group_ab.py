@@ -21,6 +21,9 @@ def main():
     cfg = os.environ.get("CONFIG", "cfg2")
     wl = W.build(cfg, device="cuda")
     Engine = plagnn.TrainEngineBF16 if wl.bf16 else plagnn.TrainEngine
+    if os.environ.get("PG_REDUCE_INLINE") is not None:  # A/B of the split-K combine placement
+        plagnn.TrainEngine.REDUCE_INLINE = os.environ["PG_REDUCE_INLINE"] == "1"
+        label += f"+inline{os.environ['PG_REDUCE_INLINE']}"
     if wl.bf16 and os.environ.get("PG_STACK_T") is not None:  # A/B of the stacked-weight layout
         plagnn.TrainEngineBF16.STACK_T = os.environ["PG_STACK_T"] == "1"
         label += f"+stackT{os.environ['PG_STACK_T']}"
