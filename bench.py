@@ -176,8 +176,34 @@ def dropin_leg(wl, dims, dev, steps: int, warmup: int):
         tl, vl = epoch()
     torch.cuda.synchronize(dev)
     ms = (time.perf_counter() - t0) / steps * 1e3
+    # the device time of the shim model's forward + backward alone (without the reference's
+    # multi_loss host loop and Adam): one graph holding model(g, features).backward(G) with a
+    # fixed upstream gradient G, replayed between two HIP events
+    dlog = torch.randn(wl.n, dims[-1], device=dev) * 1e-3
+    for p in model.parameters():
+        p.grad = torch.zeros_like(p)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            model(g, features).backward(dlog)
+    torch.cuda.current_stream(dev).wait_stream(side)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        model(g, features).backward(dlog)
+    for _ in range(3):
+        gr.replay()
+    ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    ea.record()
+    for _ in range(reps):
+        gr.replay()
+    eb.record()
+    torch.cuda.synchronize(dev)
+    model_ms = ea.elapsed_time(eb) / reps
     L = len(dims) - 3
     return {"ms_per_step": round(ms, 4), "value": round(L * (len(wl.src)) / ms * 1e3, 1), "unit": "edges/s",
+            "model_fwd_bwd_device_ms": round(model_ms, 4),
             "loss": {"train": float(tl.detach()), "val": float(vl.detach())},
             "what": "unmodified reference epoch body on the dgl shim: plagnn.model + multi_loss + autograd + "
                     "torch.optim.Adam (code/train.py:197-207)"}
@@ -258,7 +284,7 @@ def _traffic(config, group, engine):
     PMC passes (profiles/pmc_traffic.json, scripts/pmc_traffic.sh: 2 FETCH_SIZE + WRITE_SIZE
     per KERNEL dispatch), or None. A GEMM call is one kernel; a max-aggregation call is the
     max kernel (+ the merge kernel when the graph has split rows), a max-backward call the
-    pack and pull kernels (+ the merge)."""
+    count, scan, place and stream kernels (+ the merge)."""
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(tfile):
         return None
@@ -266,7 +292,7 @@ def _traffic(config, group, engine):
         b = json.load(f).get(config, {}).get(group)
     if b is None:
         return None
-    per_call = {"spmm_max_fwd": 1 + (engine.dg.fwd.n_merges > 0), "spmm_max_bwd": 2 + (engine.dg.bwd.n_merges > 0)}
+    per_call = {"spmm_max_fwd": 1 + (engine.dg.fwd.n_merges > 0), "spmm_max_bwd": 4 + (engine.dg.bwd.n_merges > 0)}
     return round(b * per_call.get(group, 1))
 
 
@@ -274,8 +300,14 @@ def _job_of(rank, mode):
     return rank if mode == "replicas" else 0
 
 
-def run(args, rank, world, dev, dist, mode):
-    """Build, capture and time one config; returns the result dict (rank 0) or None."""
+def _median_ms(evs):
+    return float(np.median([a.elapsed_time(b) for a, b in evs])) if evs else None
+
+
+def run(args, rank, world, dev, dist, mode, breakdown=True):
+    """Build, capture and time one config; returns the result dict (rank 0) or None.
+    breakdown=False (the N > 1 dp leg beside the replicas headline): no per-group timing,
+    the line's timing fields plus the all-reduce's own time."""
     import plagnn
     from plagnn import workload as W
 
@@ -344,6 +376,18 @@ def run(args, rank, world, dev, dist, mode):
                  "p10_ms": round(float(np.percentile(per_step, 10)), 4),
                  "p90_ms": round(float(np.percentile(per_step, 90)), 4),
                  "value_at_median": round(edges.item() / (med / 1e3), 1)}
+    allreduce_ms = None
+    if allreduce is not None and not args.eager:
+        # the gradient all-reduce alone: HIP events around it on the replay stream, over as
+        # many more steps (each rank's median, then the max over ranks)
+        engine.ar_events = []
+        for _ in range(n_med):
+            step()
+        torch.cuda.synchronize(dev)
+        ar = torch.tensor([_median_ms(engine.ar_events)], dtype=torch.float64, device=dev)
+        engine.ar_events = None
+        dist.all_reduce(ar, op=dist.ReduceOp.MAX)
+        allreduce_ms = ar.item()
     loss_tr, loss_va = engine.losses()
     if not (np.isfinite(loss_tr) and np.isfinite(loss_va)):
         raise SystemExit(f"non-finite loss after training: {loss_tr}, {loss_va}")
@@ -360,6 +404,21 @@ def run(args, rank, world, dev, dist, mode):
         dist.barrier()
     if rank != 0:
         return None
+    ar_info = None
+    if allreduce_ms is not None:
+        nbytes = engine.gflat.numel() * engine.gflat.element_size()
+        ar_info = {"ms_per_step": round(allreduce_ms, 4), "bytes": nbytes, "op": "AVG (one flat f32 bucket)",
+                   "timing": "HIP events around the eager all-reduce between the two replayed graphs, "
+                             "median over steps, max over ranks",
+                   "share_of_step": round(allreduce_ms / med, 4)}
+    if not breakdown:
+        return {"value": round(value, 1), "unit": "edges/s", "ms_per_step": round(t_max / args.steps * 1e3, 4),
+                "step_distribution": step_dist,
+                "scaling": "strong" if not summed else "weak",
+                "what": ("one shared model; every rank runs the full-graph step on its shard of the train rows, "
+                         "one RCCL all-reduce of the gradients per step; value = ONE model's edges/s"
+                         if not summed else "a different graph per rank; value sums the ranks"),
+                "allreduce": ar_info, "loss": {"train": loss_tr, "val": loss_va}}
 
     # per-group times after the timed region, on rank 0 only (without the collective): each
     # group's launches of one step captured as a graph and replayed back to back
@@ -404,6 +463,7 @@ def run(args, rank, world, dev, dist, mode):
         # the GEMM group's own roofline when another group dominates (cfg5)
         "gemm_roofline": roof(gemm_name) if gemm_name in groups and gemm_name != dom else None,
         "kernels_ms_per_step": {k: round(v["ms"], 4) for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])},
+        "allreduce": ar_info,
         "loss": {"train": loss_tr, "val": loss_va},
         "_engine": engine,
         "_wl": wl,
@@ -488,15 +548,37 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    dist_info = None
+    if dist is not None:
+        props = torch.cuda.get_device_properties(dev)
+        me = {"rank": rank, "local_rank": local_rank, "device": dev.index, "name": props.name,
+              "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", ""))}
+        every = [None] * world
+        dist.all_gather_object(every, me)
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "ranks": every}
     out = run(args, rank, world, dev, dist, mode)
+    # N > 1: the RCCL data-parallel leg in the same job, after the replicas headline
+    dp_leg = None
+    if world > 1 and mode == "replicas" and args.mode == "auto":
+        dp_leg = run(args, rank, world, dev, dist, "dp", breakdown=False)
     if out is None:
         dist.destroy_process_group()
         return
     engine, wl = out.pop("_engine"), out.pop("_wl")
+    if dist_info is not None:
+        out["dist"] = dist_info
+    if dp_leg is not None:
+        out["dp"] = dp_leg
     legs = {}
     if world == 1 and not args.no_legs:
         legs["epoch_with_eval_ms"] = epoch_with_eval_leg(engine, wl, dev)
         if dropin is not None:
+            # the engine's forward + backward (every group but Adam; the head includes its
+            # fused loss) against the shim model's forward + backward device time
+            eng = sum(v for k, v in out["kernels_ms_per_step"].items() if k != "adam")
+            dropin["engine_fwd_bwd_device_ms"] = round(eng, 4)
+            if dropin.get("model_fwd_bwd_device_ms"):
+                dropin["model_vs_engine"] = round(dropin["model_fwd_bwd_device_ms"] / eng, 3)
             legs["dropin"] = dropin
     out.update(legs)
     cpu = None

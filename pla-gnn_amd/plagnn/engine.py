@@ -177,6 +177,9 @@ class TrainEngine:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_adam: Optional[torch.cuda.CUDAGraph] = None
         self.allreduce = None
+        # [(start, end)] HIP events around each replayed step's gradient all-reduce, when a
+        # list is set (bench.py's dp leg)
+        self.ar_events: Optional[list] = None
         self.steps_done = 0
         self._timing: Optional[list] = None  # [(name, work, start_event, end_event)]
 
@@ -570,7 +573,14 @@ class TrainEngine:
             return
         self.graph.replay()
         if self.graph_adam is not None:
-            self.allreduce(self.gflat)
+            if self.ar_events is not None:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                self.allreduce(self.gflat)
+                b.record()
+                self.ar_events.append((a, b))
+            else:
+                self.allreduce(self.gflat)
             self.graph_adam.replay()
         self.steps_done += 1
 

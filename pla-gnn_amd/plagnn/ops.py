@@ -348,17 +348,69 @@ def _padded(n: int, F: int, device) -> torch.Tensor:
     return buf
 
 
+def sage_width(F: int) -> int:
+    """TrainEngine's SAGE input width: a multiple of 64 when that costs <= 2 % more columns
+    (503 -> 512: whole SpMM feature tiles, the three-piece GEMM's aligned operands), else a
+    multiple of 4. Pads are zero."""
+    r64 = -(-F // 64) * 64
+    return r64 if r64 <= 1.02 * F else round4(F)
+
+
+# layer inputs that take no gradient (the features: the same tensor every epoch) keep their
+# padded [H | M] buffer: {key: [HM, version, busy]}. A buffer whose forward saved it for a
+# backward that has not run yet is busy (its M half must not be overwritten): another
+# forward then gets a fresh buffer.
+_HM_CACHE: dict = {}
+
+
+def _hm_buffer(h: torch.Tensor, Fp: int, keep: bool):
+    """([H | M] (N x 2Fp, H and its zero pad in the left half) for a SAGE layer's input h,
+    the cache key it was marked busy under or None)."""
+    N, Fin = h.shape
+    key = (h.data_ptr(), tuple(h.shape), str(h.device), Fp) if not h.requires_grad else None
+    if key is not None:
+        hit = _HM_CACHE.get(key)
+        if hit is not None and hit[1] == h._version and not hit[2]:
+            hit[2] = keep
+            return hit[0], (key if keep else None)
+    HM = torch.empty(N, 2 * Fp, dtype=torch.float32, device=h.device)
+    HM[:, :Fin].copy_(h)
+    if Fp > Fin:
+        HM[:, Fin:Fp].zero_()
+    if key is not None and (key not in _HM_CACHE or not _HM_CACHE[key][2]):
+        if len(_HM_CACHE) > 8:
+            _HM_CACHE.clear()
+        _HM_CACHE[key] = [HM, h._version, keep]
+        return HM, (key if keep else None)
+    return HM, None
+
+
+def _hm_release(key) -> None:
+    hit = _HM_CACHE.get(key) if key is not None else None
+    if hit is not None:
+        hit[2] = False
+
+
 class SagePool(torch.autograd.Function):
     """One DGL 0.8.2 SAGEConv(in, out, 'pool') layer, forward and backward, on the
     engine's kernels (code/model.py:13-15):
         P = relu(h @ Wpool^T + bpool); M = max-aggregate(P); Y = h @ Wself^T + M @ Wneigh^T + b
-    """
+
+    On a HIP device it runs TrainEngine's layouts: the input padded to sage_width (503 ->
+    512, so the layer-1 products run the three-piece GEMM), fc_self + fc_neigh as ONE
+    K = 2F product [H | M] [Wself | Wneigh]^T, dead-none max records (the backward reads no
+    relu' mask), the weight gradients of fc_self and fc_neigh as one product dY^T [H | M],
+    and the input gradient as one stacked product [dY | dP] [Wself ; Wpool]. On the CPU
+    device: the plain composition (DGL's CPU backend role)."""
 
     @staticmethod
     def forward(ctx, h, w_pool, b_pool, w_self, w_neigh, bias, dg, ew_slots):
         h = h.contiguous()
+        ctx.dg = dg
+        ctx.has_bias = bias is not None
+        if h.device.type == "cuda":
+            return SagePool._forward_gpu(ctx, h, w_pool, b_pool, w_self, w_neigh, bias, dg, ew_slots)
         N, Fin = h.shape
-        Fout = w_self.shape[0]
         Fp = round4(Fin)
         Pb = _padded(N, Fin, h.device)
         gemm(h, w_pool, transb=True, out=Pb[:, :Fin], bias=b_pool, act=_lib.PG_ACT_RELU)
@@ -367,13 +419,35 @@ class SagePool(torch.autograd.Function):
         spmm_max(dg, Pb, ew_slots, out=Mb, argpos=argpos)
         Y = gemm(h, w_self, transb=True)
         gemm(Mb[:, :Fin], w_neigh, transb=True, out=Y, beta=1.0, bias=bias)
-        ctx.dg = dg
+        ctx.gpu = False
         ctx.save_for_backward(h, w_pool, w_self, w_neigh, Pb, Mb, argpos, ew_slots)
-        ctx.has_bias = bias is not None
+        return Y
+
+    @staticmethod
+    def _forward_gpu(ctx, h, w_pool, b_pool, w_self, w_neigh, bias, dg, ew_slots):
+        N, Fin = h.shape
+        Fp = sage_width(Fin)
+        fpad = Fp - Fin
+        keep = torch.is_grad_enabled() and any(ctx.needs_input_grad[:6])
+        HM, ctx.hm_key = _hm_buffer(h, Fp, keep)
+        Wpool = torch.nn.functional.pad(w_pool, (0, fpad, 0, fpad)) if fpad else w_pool.contiguous()
+        bpool = torch.nn.functional.pad(b_pool, (0, fpad)) if fpad else b_pool.contiguous()
+        Wcat = torch.cat([torch.nn.functional.pad(w_self, (0, fpad)), torch.nn.functional.pad(w_neigh, (0, fpad))], 1) \
+            if fpad else torch.cat([w_self, w_neigh], 1)
+        P = torch.empty(N, Fp, dtype=torch.float32, device=h.device)
+        gemm(HM[:, :Fp], Wpool, transb=True, out=P, bias=bpool, act=_lib.PG_ACT_RELU)
+        argpos = torch.empty(N, Fp, dtype=dg.arg_dtype, device=h.device)
+        spmm_max(dg, P, ew_slots, out=HM[:, Fp:], argpos=argpos, dead_none=True)
+        Y = gemm(HM, Wcat, transb=True, bias=bias)
+        ctx.gpu = True
+        ctx.save_for_backward(HM, P, argpos, Wpool, Wcat, ew_slots)
+        ctx.fin = Fin
         return Y
 
     @staticmethod
     def backward(ctx, dY):
+        if ctx.gpu:
+            return SagePool._backward_gpu(ctx, dY)
         h, w_pool, w_self, w_neigh, Pb, Mb, argpos, ew_slots = ctx.saved_tensors
         dg = ctx.dg
         dY = dY.contiguous()
@@ -398,4 +472,47 @@ class SagePool(torch.autograd.Function):
         if need_h:
             d_h = gemm(dY, w_self)
             gemm(dP, w_pool, out=d_h, beta=1.0)
+        return d_h, d_wp, d_bp, d_ws, d_wn, d_b, None, None
+
+    @staticmethod
+    def _backward_gpu(ctx, dY):
+        HM, P, argpos, Wpool, Wcat, ew_slots = ctx.saved_tensors
+        dg, Fin = ctx.dg, ctx.fin
+        try:
+            return SagePool._backward_gpu_body(ctx, dY, HM, P, argpos, Wpool, Wcat, ew_slots, dg, Fin)
+        finally:
+            _hm_release(ctx.hm_key)
+
+    @staticmethod
+    def _backward_gpu_body(ctx, dY, HM, P, argpos, Wpool, Wcat, ew_slots, dg, Fin):
+        N, Fp = P.shape
+        Fo = dY.shape[1]
+        need_h, need_wp, need_bp, need_ws, need_wn, need_b = ctx.needs_input_grad[:6]
+        # [dY | dP]: dY copied in, dP written by the max backward
+        DYP = torch.empty(N, Fo + Fp, dtype=torch.float32, device=dY.device)
+        DYP[:, :Fo].copy_(dY)
+        dY = DYP[:, :Fo]
+        d_b = torch.empty(Fo, dtype=torch.float32, device=dY.device) if (need_b and ctx.has_bias) else None
+        d_ws = d_wn = None
+        if need_ws or need_wn:
+            d_wcat = gemm(dY, HM, transa=True, rowsum=d_b)  # [d Wself | d Wneigh] in one product
+            d_ws, d_wn = d_wcat[:, :Fin], d_wcat[:, Fp:Fp + Fin]
+        elif d_b is not None:
+            d_b = col_sum(dY)
+        dM = gemm(dY, Wcat[:, Fp:])
+        # dead-none records: the relu' mask of P is implied (P is not read)
+        spmm_max_backward(dg, argpos, dM, ew_slots, mask=P, dx=DYP[:, Fo:], dead_none=True)
+        dP = DYP[:, Fo:]
+        d_bp_p = torch.empty(Fp, dtype=torch.float32, device=dY.device) if need_bp else None
+        d_wp = d_bp = None
+        if need_wp:
+            d_wp = gemm(dP, HM[:, :Fp], transa=True, rowsum=d_bp_p)[:Fin, :Fin]
+        elif d_bp_p is not None:
+            d_bp_p = col_sum(dP)
+        if d_bp_p is not None:
+            d_bp = d_bp_p[:Fin]
+        d_h = None
+        if need_h:  # one stacked product [dY | dP] [Wself ; Wpool]
+            Wstack = torch.cat([Wcat[:, :Fp], Wpool], 0)
+            d_h = gemm(DYP, Wstack)[:, :Fin]
         return d_h, d_wp, d_bp, d_ws, d_wn, d_b, None, None

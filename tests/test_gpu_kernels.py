@@ -146,6 +146,75 @@ def test_spmm_empty_rows_and_edges():
     assert torch.equal(dX[2], torch.ones(4)) and dX[1].sum() == 0 and dX[0].sum() == 0
 
 
+@pytest.mark.parametrize("dead", [False, True])
+@pytest.mark.parametrize("F", [4, 256])
+def test_spmm_max_bwd_sources_without_out_edges(oracle_mod, F, dead):
+    """The highest-numbered nodes send no edges (their transposed rows are empty at the end
+    of the entry range), and a graph with no edges at all: every dx row is still written
+    (zeros for the empty ones), with and without dead-none records."""
+    from plagnn import ops
+
+    n, n_src = 300, 240
+    rng = np.random.default_rng(F + dead)
+    src = rng.integers(0, n_src, 2000).astype(np.int64)
+    dst = rng.integers(0, n, 2000).astype(np.int64)
+    g = _graph(src, dst, n)
+    assert np.all(g.out_degrees()[n_src:] == 0) and np.any(g.in_degrees()[n_src:] > 0)
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False)
+    X = np.maximum(rng.standard_normal((n, F)), 0).astype(np.float32)
+    dZ = rng.standard_normal((n, F)).astype(np.float32)
+    dg = g.on(DEV)
+    Xd = torch.from_numpy(X).to(DEV)
+    _, argpos = ops.spmm_max(dg, Xd, dead_none=dead)
+    _, argx, arge = oracle_mod.spmm_max(og, X)
+    ref = np.where(X > 0, oracle_mod.spmm_max_bwd(og, argx, arge, dZ), 0.0)
+    dx = torch.full((n, F), float("nan"), device=DEV)
+    ops.spmm_max_backward(dg, argpos, torch.from_numpy(dZ).to(DEV), mask=Xd, dx=dx, dead_none=dead)
+    np.testing.assert_array_equal(dx.cpu().numpy(), ref)
+    assert np.all(dx.cpu().numpy()[n_src:] == 0)
+    # no edges at all
+    e = np.zeros(0, np.int64)
+    g0 = _graph(e, e, 7)
+    dg0 = g0.on(DEV)
+    X0 = torch.rand(7, F, device=DEV)
+    out0, arg0 = ops.spmm_max(dg0, X0, dead_none=dead)
+    assert torch.all(out0 == 0)
+    dx0 = torch.full((7, F), float("nan"), device=DEV)
+    ops.spmm_max_backward(dg0, arg0, torch.rand(7, F, device=DEV), mask=X0, dx=dx0, dead_none=dead)
+    assert torch.all(dx0 == 0)
+
+
+@pytest.mark.parametrize("F", [65, 256])
+def test_spmm_max_bwd_hub_past_lds_histogram(oracle_mod, F):
+    """A destination with 6 000 in-edges (u16 records; past the 4 096-entry LDS histogram of
+    the count and place passes, whose list counters are then global integer atomics) and a
+    source with 6 000 out-edges: bit-exact on unsplit rows."""
+    from plagnn import ops
+
+    n = 3000
+    src, dst = hub_graph(n, 6000, seed=F)
+    g = _graph(src, dst, n)
+    assert g.in_degrees().max() > 4096 and g.arg_kind == 16
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False)
+    rng = np.random.default_rng(F)
+    X = np.maximum(rng.standard_normal((n, F)), 0).astype(np.float32)
+    dZ = rng.standard_normal((n, F)).astype(np.float32)
+    dg = g.on(DEV)
+    Xd = torch.from_numpy(X).to(DEV)
+    _, argx, arge = oracle_mod.spmm_max(og, X)
+    dX_ref = oracle_mod.spmm_max_bwd(og, argx, arge, dZ)
+    split_rows = set(g.bwd.merges.reshape(-1, 4)[: g.bwd.n_merges, 0].tolist())
+    exact = np.array([u not in split_rows for u in range(n)])
+    mag = np.abs(oracle_mod.spmm_max_bwd(og, argx, arge, np.abs(dZ)))
+    for dead in (False, True):
+        _, argpos = ops.spmm_max(dg, Xd, dead_none=dead)
+        dX = ops.spmm_max_backward(dg, argpos, torch.from_numpy(dZ).to(DEV), mask=Xd,
+                                   dead_none=dead).cpu().numpy()
+        ref = np.where(X > 0, dX_ref, 0.0)
+        np.testing.assert_array_equal(dX[exact], ref[exact])
+        assert np.all(np.abs(dX - ref) <= 1e-5 * mag + 1e-6)
+
+
 @pytest.mark.parametrize("mean", [False, True])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_spmm_sum_fwd_bwd(oracle_mod, mean, weighted):
