@@ -292,7 +292,7 @@ def _traffic(config, group, engine):
         b = json.load(f).get(config, {}).get(group)
     if b is None:
         return None
-    per_call = {"spmm_max_fwd": 1 + (engine.dg.fwd.n_merges > 0), "spmm_max_bwd": 4 + (engine.dg.bwd.n_merges > 0)}
+    per_call = {"spmm_max_fwd": 1 + (engine.dg.fwd.n_merges > 0), "spmm_max_bwd": 4 + (engine.dg.bwd_stream.n_merges > 0)}
     return round(b * per_call.get(group, 1))
 
 

@@ -128,9 +128,9 @@ typedef struct pg_csr {
   int64_t n_slots;
   int32_t max_deg;
   int32_t chunk;
-  const int32_t* einv;   /* [nnz] in-CSR only, optional and unread since ABI 7 (the max
-                            backward's list descriptors sit at in-CSR slots); kept so the
-                            struct layout does not change */
+  const int32_t* einv;   /* [nnz] in-CSR only: the transposed index of in-CSR slot k
+                            (einv[tslot[t]] = t); required by pg_spmm_max_bwd[_bf16] (its
+                            place pass finds each edge's list there, ABI 8), else unread */
 } pg_csr_t;
 
 /* ---------------- host: graph construction (code/utils.py:44-45) ---------------- */
@@ -167,15 +167,15 @@ int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, f
 /* Deterministic backward (gather over the transposed CSR gt of g; gt->epos required):
  *   dx[u,f] = sum_{(v,j) in gt row u, ascending v} [argpos[v,f] == j - g.ptr[v]] * ew[j] * dout[v,f]
  * then, if mask_src != NULL, dx[u,f] *= (mask_src[u,f] > 0)  (relu' of fc_pool).
- * fwd_out (optional, needs mask_src = the forward's input X, a relu output: X >= 0): the
- * forward's output. An entry (v, f) with fwd_out[v,f] == 0 is skipped: its winner u has
- * X[u,f] * w == 0, so it is either masked (X[u,f] = 0) or weighted 0 — the result is
- * unchanged, and the dead features whose ties all sit at position 0 no longer crowd one
- * list. (A +-inf maximum, stored as 0, is skipped too.) Every entry left has
- * X[u,f] * w != 0, hence X[u,f] > 0: the mask is implied and mask_src is not read (an
- * element no entry reaches is +0 either way). With X < 0 somewhere the result is
- * undefined; pass fwd_out = NULL for such inputs.
- * Every dx element is written (no zero-fill needed). */
+ * fwd_out (optional, needs mask_src = the forward's input X): the forward's output. An
+ * entry (v, f) with fwd_out[v,f] == 0 is skipped: its winner u has X[u,f] * w == 0, so it
+ * is either masked (X[u,f] = 0) or weighted 0 — the result is unchanged. (A +-inf
+ * maximum, stored as 0, is skipped too.) The mask is still applied.
+ * PG_ARG_DEAD_NONE records (the same skip made by the forward; needs mask_src = X, a relu
+ * output, X >= 0): every entry left has X[u,f] * w != 0, hence X[u,f] > 0, so the mask is
+ * implied and mask_src is not read (an element no entry reaches is +0 either way). With
+ * X < 0 somewhere the result is undefined.
+ * The u16 / F <= 1024 path needs g->einv. Every dx element is written (no zero-fill). */
 size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F);
 int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
                     int arg_kind, const float* dout, int64_t ldd, int64_t F,
@@ -432,7 +432,9 @@ int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-
                          (epilogue without splitk_cnt), no grouped SpMM pair; 6: with fwd_out,
                          pg_spmm_max_bwd[_bf16] takes mask_src >= 0 and does not read it;
                          PG_ARG_DEAD_NONE; 7: pg_spmm_max_bwd reads no einv, smaller
-                         workspace */
+                         workspace; 8: source-ordered max backward (reads g->einv);
+                         with fwd_out alone the relu' mask is applied, only
+                         PG_ARG_DEAD_NONE implies it */
 
 #ifdef __cplusplus
 }

@@ -93,7 +93,7 @@ __device__ __forceinline__ void split4(const float4 v, uint2 (&out)[3]) {
 
 // One operand's K tile: ROWS x KS, float4 units; row image unit = (row, 4 k), k image unit
 // = (k, 4 rows).
-__device__ float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written
+__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written; read as a float4
 
 template <int ROWS, bool KMAJ>
 struct Stage {

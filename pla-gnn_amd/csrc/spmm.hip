@@ -413,17 +413,21 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
 //             slot s = ptr[v] + p (a wave per row with an LDS histogram; rows longer than
 //             kPackWaveMax: a workgroup);
 //   2. scan   (transposed order t, one pass with decoupled look-back): off_t[t] = the sum
-//             of cnt over the transposed entries before t, off_s[tslot[t]] = off_t[t];
-//   3. place  (per destination row v): each live (v, f) goes to rec[off_s[s] + rank] =
-//             {w * dout[v,f], f}; rank comes from an LDS atomic on the list's running
-//             offset (the order inside a list is free: a list never repeats a feature);
-//   4. stream (a wave per transposed item {u, t0, t1}): rec[off_t[t0] .. off_t[t1]) is
-//             read as contiguous 64-entry groups and added into an LDS row with ds_add_f32.
-//             One wave's LDS instructions execute in order, and lanes of one instruction
-//             that hit the same word are applied in ascending lane order
-//             (scripts/probes/lds_atomic_order.hip), so every feature's terms are summed
-//             in ascending v, the order of the sequential scatter_add_: bit-exact on rows
-//             that are not split across items.
+//             of cnt over the transposed entries before t;
+//   3. place  (per destination row v): each live (v, f) goes to rec[off_t[einv[s]] + rank]
+//             = {w * dout[v,f], f}; rank comes from an LDS integer atomic on the list's
+//             running offset (the order inside a list is free: a list never repeats a
+//             feature);
+//   4. stream (persistent waves over the transposed items {u, t0, t1}): rec[off_t[t0] ..
+//             off_t[t1]) is read as contiguous 64-record groups and added into an LDS row
+//             in order: each lane reads its word, adds, and swaps the sum in with
+//             ds_cmpst (compare-and-swap); lanes of one instruction that hit the same word
+//             are applied in ascending lane order, so of two records of one feature the
+//             earlier one's swap succeeds and the later one retries on its result. Every
+//             feature's terms are thus summed in ascending v, the order of the sequential
+//             scatter_add_: bit-exact on rows that are not split across items. (LDS float
+//             atomics, ds_add_f32, keep the same order but run at 1/16 of the integer
+//             atomics' rate on gfx950: scripts/probes/lds_rmw_probe.hip.)
 // The scatter that round 3's pull did with reads (one random descriptor line and two
 // random list lines per edge, 292 MB fetched per F = 256 launch for ~60 MB of lists) is
 // done by the place pass's writes instead; the stream pass reads sequential lines only.
@@ -431,9 +435,6 @@ constexpr int kHistMax = 4096;  // longest row whose lists a workgroup counts in
 constexpr int kGroupMaxF = 1024;
 #ifndef PG_BWD_DIRECT
 #define PG_BWD_DIRECT 0
-#endif
-#ifndef PG_BWD_REC8
-#define PG_BWD_REC8 1  // one 8-B record {value, feature} per entry (else u16 + f32 arrays)
 #endif
 #ifndef PG_STREAM_PROBE
 #define PG_STREAM_PROBE 0  // timing-only probes (wrong results): 1 no atomics, 2 no record loads, 3 no stores
@@ -445,9 +446,11 @@ constexpr int kGroupMaxF = 1024;
 #define PG_STREAM_U 4  // 64-entry groups in flight per wave in the stream pass
 #endif
 
+// one record per entry: {value f32, feature} in 8 B; for bf16 storage without edge weights
+// the value is a bf16 upstream gradient taken as is, so {value bf16, feature u16} in 4 B
 struct BRecs {
-#if PG_BWD_REC8
   uint2* __restrict__ r;
+  static constexpr int kBytes = 8;
   __device__ __forceinline__ void put(int pos, int f, float d) const {
     r[pos] = make_uint2(__float_as_uint(d), (uint32_t)f);
   }
@@ -456,12 +459,18 @@ struct BRecs {
     d = __uint_as_float(x.x);
     f = (int)x.y;
   }
-#else
-  uint16_t* __restrict__ f16;
-  float* __restrict__ val;
-  __device__ __forceinline__ void put(int pos, int f, float d) const { f16[pos] = (uint16_t)f; val[pos] = d; }
-  __device__ __forceinline__ void get(int pos, int& f, float& d) const { f = f16[pos]; d = val[pos]; }
-#endif
+};
+struct BRecs4 {
+  uint32_t* __restrict__ r;
+
+  __device__ __forceinline__ void put(int pos, int f, float d) const {
+    r[pos] = (__float_as_uint(d) & 0xFFFF0000u) | (uint32_t)f;  // d is a bf16 value: exact
+  }
+  __device__ __forceinline__ void get(int pos, int& f, float& d) const {
+    const uint32_t x = r[pos];
+    d = __uint_as_float(x & 0xFFFF0000u);
+    f = (int)(x & 0xFFFFu);
+  }
 };
 
 // inclusive prefix sum over the 64 lanes: DPP row shifts, then row broadcasts 15 and 31
@@ -546,24 +555,23 @@ __device__ __forceinline__ void load_row(int v, int lane, int deg, const A* __re
 }
 
 // Passes 1 and 3 for a row of in-degree 1..kPackWaveMax, one wave. PLACE = false: count
-// into cnt[s]; PLACE = true: `offs` holds the lists' offsets, each live entry takes the
-// next place of its list.
-template <int NV, bool PLACE, typename A, typename T>
-__device__ __forceinline__ void bwd_short_row(int v, int lane, int* __restrict__ hist,
-                                              const int32_t* __restrict__ ptr,
+// into cnt[s]; PLACE = true: the list of slot s starts at off_t[einv[s]] (einv: in-CSR slot
+// -> transposed index), each live entry takes the next place of its list.
+template <int NV, bool PLACE, typename A, typename T, typename R>
+__device__ __forceinline__ void bwd_short_row(int v, int rs, int deg, int lane, int* __restrict__ hist,
                                               const A* __restrict__ arg, int64_t lda, int F,
                                               const T* __restrict__ dout, int64_t ldd,
                                               const T* __restrict__ fout, int64_t ldf,
                                               const float* __restrict__ ew,
-                                              int32_t* __restrict__ offs, BRecs recs) {
+                                              int32_t* __restrict__ cnt,
+                                              const int32_t* __restrict__ einv,
+                                              const int32_t* __restrict__ off_t, R recs) {
   constexpr int K = RowLanes<NV>::K;
-  const int rs = ptr[v];
-  const int deg = ptr[v + 1] - rs;
   if (deg > kPackWaveMax || deg == 0) return;
   int a[K];
   float d[K];
   load_row<NV, PLACE>(v, lane, deg, arg, lda, F, dout, ldd, fout, ldf, a, d);
-  for (int p = lane; p < deg; p += kWave) hist[p] = PLACE ? offs[rs + p] : 0;
+  for (int p = lane; p < deg; p += kWave) hist[p] = PLACE ? off_t[einv[rs + p]] : 0;
   if constexpr (PLACE) {
     if (ew) {  // the edge weight folded into the value: the product the pull formed, w * d
       float w[K];
@@ -583,20 +591,22 @@ __device__ __forceinline__ void bwd_short_row(int v, int lane, int* __restrict__
     for (int k = 0; k < K; ++k)
       if (a[k] >= 0) atomicAdd(&hist[a[k]], 1);
     wave_lds_sync();
-    for (int p = lane; p < deg; p += kWave) offs[rs + p] = hist[p];
+    for (int p = lane; p < deg; p += kWave) cnt[rs + p] = hist[p];
   }
 }
 
 // The same for a row longer than kPackWaveMax, one workgroup (thread t owns features
 // t + 256 i). Past kHistMax entries the counters are global integer atomics (order-free).
-template <bool PLACE, typename A, typename T>
+template <bool PLACE, typename A, typename T, typename R>
 __device__ __forceinline__ void bwd_long_row(int v, int* __restrict__ hist,
                                              const int32_t* __restrict__ ptr,
                                              const A* __restrict__ arg, int64_t lda, int F,
                                              const T* __restrict__ dout, int64_t ldd,
                                              const T* __restrict__ fout, int64_t ldf,
                                              const float* __restrict__ ew,
-                                             int32_t* __restrict__ offs, BRecs recs) {
+                                             int32_t* __restrict__ cnt,
+                                             const int32_t* __restrict__ einv,
+                                             const int32_t* __restrict__ off_t, R recs) {
   constexpr int FPT = kGroupMaxF / kBlock;
   const int rs = ptr[v];
   const int deg = ptr[v + 1] - rs;
@@ -614,7 +624,7 @@ __device__ __forceinline__ void bwd_long_row(int v, int* __restrict__ hist,
     if (PLACE && ew && a[i] >= 0) d[i] = ew[rs + a[i]] * d[i];
   }
   if (deg <= kHistMax) {
-    for (int p = threadIdx.x; p < deg; p += kBlock) hist[p] = PLACE ? offs[rs + p] : 0;
+    for (int p = threadIdx.x; p < deg; p += kBlock) hist[p] = PLACE ? off_t[einv[rs + p]] : 0;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < FPT; ++i)
@@ -624,20 +634,18 @@ __device__ __forceinline__ void bwd_long_row(int v, int* __restrict__ hist,
       }
     if (!PLACE) {
       __syncthreads();
-      for (int p = threadIdx.x; p < deg; p += kBlock) offs[rs + p] = hist[p];
+      for (int p = threadIdx.x; p < deg; p += kBlock) cnt[rs + p] = hist[p];
     }
   } else {
-    if (!PLACE) {
-      for (int p = threadIdx.x; p < deg; p += kBlock) offs[rs + p] = 0;
-      __threadfence();
-      __syncthreads();
-    }
-    // PLACE: off_s is not read after this pass, so its entries serve as the counters
+    // the row's counters in cnt (the scan has read it by the place pass), cleared first
+    for (int p = threadIdx.x; p < deg; p += kBlock) cnt[rs + p] = 0;
+    __threadfence();
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < FPT; ++i)
       if (a[i] >= 0) {
-        const int pos = atomicAdd(&offs[rs + a[i]], 1);
-        if (PLACE) recs.put(pos, threadIdx.x + i * kBlock, d[i]);
+        const int rank = atomicAdd(&cnt[rs + a[i]], 1);
+        if (PLACE) recs.put(off_t[einv[rs + a[i]]] + rank, threadIdx.x + i * kBlock, d[i]);
       }
   }
 }
@@ -647,36 +655,54 @@ __device__ __forceinline__ void bwd_long_row(int v, int* __restrict__ hist,
 // <= kPackWaveMax; NULL = every row, short ones exit at once) so the long rows start first;
 // the remaining blocks take 4 rows each, one wave per row. The count pass also clears the
 // scan's look-back words (lb, n_lb of them) for this call.
-template <int NV, bool PLACE, typename A, typename T>
+template <int NV, bool PLACE, typename A, typename T, typename R>
 __global__ __launch_bounds__(kBlock) void bwd_rows_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
     const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew,
-    int32_t* __restrict__ offs, BRecs recs, unsigned long long* __restrict__ lb, int n_lb) {
+    int32_t* __restrict__ cnt, const int32_t* __restrict__ einv, const int32_t* __restrict__ off_t,
+    R recs, unsigned long long* __restrict__ lb, int n_lb) {
   __shared__ __attribute__((aligned(16))) int lds[kHistMax];
   static_assert(kHistMax >= kWavesPerBlock * kPackWaveMax, "short-row histograms");
   if (!PLACE)
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n_lb; i += gridDim.x * kBlock) lb[i] = 0ull;
   const int b = blockIdx.x;
   if (b < n_long) {
-    bwd_long_row<PLACE, A, T>(rows ? rows[b].x : b, lds, ptr, arg, lda, F, dout, ldd, fout, ldf, ew,
-                              offs, recs);
+    bwd_long_row<PLACE, A, T, R>(rows ? rows[b].x : b, lds, ptr, arg, lda, F, dout, ldd, fout, ldf, ew,
+                              cnt, einv, off_t, recs);
   } else {
+    // persistent waves over the short rows: wave w takes rows w, w + W, ...; its 64 lanes
+    // fetch 64 rows' bounds at once (one round trip per 64 rows instead of one in front of
+    // every row)
     const int wave = wave_id_uniform();
-    const int v = (b - n_long) * kWavesPerBlock + wave;
-    if (v < n_rows)
-      bwd_short_row<NV, PLACE, A, T>(v, lane_id(), lds + wave * kPackWaveMax, ptr, arg, lda, F, dout,
-                                     ldd, fout, ldf, ew, offs, recs);
+    const int lane = lane_id();
+    const int W = ((int)gridDim.x - n_long) * kWavesPerBlock;
+    for (int base = (b - n_long) * kWavesPerBlock + wave; base < n_rows; base += kWave * W) {
+      const int my = base + lane * W;
+      int rs_l = 0, re_l = 0;
+      if (my < n_rows) {
+        rs_l = ptr[my];
+        re_l = ptr[my + 1];
+      }
+      const int nb = min(kWave, (n_rows - base + W - 1) / W);
+      for (int j = 0; j < nb; ++j) {
+        const int rs = bcast(rs_l, j);
+        bwd_short_row<NV, PLACE, A, T, R>(base + j * W, rs, bcast(re_l, j) - rs, lane, lds + wave * kPackWaveMax,
+                                          arg, lda, F, dout, ldd, fout, ldf, ew, cnt, einv, off_t, recs);
+      }
+    }
   }
 }
 
-// Pass 2: exclusive scan of cnt in the transposed order, one pass. Tiles of kScanTile
+// Pass 2: exclusive scan of cnt in the transposed order, one pass (off_t only: the place
+// pass gathers its lists' offsets through einv; scattering them to in-CSR slots here
+// instead was slower). Tiles of kScanTile
 // entries are taken in ticket order (an atomic counter, so every tile's predecessors are
 // already running); each publishes its sum, then its inclusive prefix, in one 64-bit word
 // {status:2 | value:62} (a single atomic store carries both, no fence needed). Wave 0
 // looks back over 64 predecessors at a time. The spin is bounded, so a broken invariant
 // gives wrong offsets (caught by the tests), never a hung GPU.
-constexpr int kScanIpt = 8;
+constexpr int kScanIpt = 4;
 constexpr int kScanTile = kBlock * kScanIpt;
 constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62;
 constexpr unsigned long long kLbVal = (1ull << 62) - 1;
@@ -690,8 +716,7 @@ __device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long lo
 
 __global__ __launch_bounds__(kBlock) void bwd_scan_kernel(
     const int32_t* __restrict__ tslot, int nnz, const int32_t* __restrict__ cnt,
-    int32_t* __restrict__ off_s, int32_t* __restrict__ off_t, unsigned long long* __restrict__ lb,
-    int ntiles) {
+    int32_t* __restrict__ off_t, unsigned long long* __restrict__ lb, int ntiles) {
   __shared__ int s_tile, s_prefix;
   __shared__ int wsum[kWavesPerBlock];
   if (threadIdx.x == 0)
@@ -753,10 +778,7 @@ __global__ __launch_bounds__(kBlock) void bwd_scan_kernel(
   int run = s_prefix + wave_pre + incl - local;
 #pragma unroll
   for (int j = 0; j < kScanIpt; ++j) {
-    if (t0 + j < nnz) {
-      off_t[t0 + j] = run;
-      off_s[ts[j]] = run;
-    }
+    if (t0 + j < nnz) off_t[t0 + j] = run;
     run += c[j];
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) off_t[nnz] = s_prefix + agg;
@@ -766,9 +788,9 @@ __global__ __launch_bounds__(kBlock) void bwd_scan_kernel(
 // contiguous run). A wave takes items it, it + W, it + 2W, ... (W = waves in the grid); the
 // 64 lanes first fetch 64 of its items and their record ranges at once (two round trips per
 // 64 items instead of two dependent ones in front of every item), then the wave walks them.
-template <typename T>
+template <typename T, typename R>
 __global__ __launch_bounds__(kBlock) void bwd_stream_kernel(
-    const int4* __restrict__ items, int n_items, const int32_t* __restrict__ off_t, BRecs recs,
+    const int4* __restrict__ items, int n_items, const int32_t* __restrict__ off_t, R recs,
     int F, const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx,
     float* __restrict__ ws, int64_t ldw) {
   constexpr int U = PG_STREAM_U;
@@ -814,12 +836,18 @@ __global__ __launch_bounds__(kBlock) void bwd_stream_kernel(
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const bool in = e + u * kWave + lane < e1;
-#if PG_STREAM_PROBE == 1
-          acc[in ? fe[u] : kGroupMaxF + lane] = in ? de[u] : 0.f;
-#else
-          atomicAdd(&acc[in ? fe[u] : kGroupMaxF + lane], in ? de[u] : 0.f);
-#endif
+          bool pend = e + u * kWave + lane < e1;
+          unsigned* w = reinterpret_cast<unsigned*>(acc + (pend ? fe[u] : kGroupMaxF + lane));
+          float cur = *reinterpret_cast<const float*>(w);
+          // in-order add: same-word lanes retry on the earlier lane's sum (see the header)
+          while (__ballot(pend)) {
+            if (pend) {
+              const unsigned want = __float_as_uint(cur);
+              const unsigned got = atomicCAS(w, want, __float_as_uint(cur + de[u]));
+              pend = got != want;
+              cur = __uint_as_float(got);
+            }
+          }
         }
       }
       wave_lds_sync();
@@ -1287,22 +1315,20 @@ int pg_spmm_max_fwd_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t 
                                  arg_kind, ws, ws_bytes, stream);
 }
 
-// [split-row partials][source-ordered path: cnt nnz | off_s nnz | off_t nnz + 1 |
+// [split-row partials][source-ordered path: cnt nnz | off_t nnz + 1 |
 //  look-back words ntiles + 1 (u64) | records N x F]
 static size_t bwd_partials_bytes(const pg_csr_t* gt, int64_t F) {
   return gt->n_slots > 0 ? round_up(gt->n_slots * ws_ld(F) * 4, 256) : 0;
 }
 static int64_t bwd_scan_tiles(int64_t nnz) { return (nnz + kScanTile - 1) / kScanTile; }
-static size_t bwd_rec_bytes(int64_t n) {
-  return PG_BWD_REC8 ? round_up(n * 8, 256) : round_up(n * 2, 256) + round_up(n * 4, 256);
-}
+static size_t bwd_rec_bytes(int64_t n) { return round_up(n * BRecs::kBytes, 256); }
 
 size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
   if (!gt || F <= 0) return 0;
   size_t b = bwd_partials_bytes(gt, F);
   if (F <= kGroupMaxF) {
     const int64_t N = gt->n_cols, E = gt->nnz;
-    b += 2 * round_up(E * 4, 256) + round_up((E + 1) * 4, 256) +
+    b += round_up(E * 4, 256) + round_up((E + 1) * 4, 256) +
          round_up((bwd_scan_tiles(E) + 1) * 8, 256) + bwd_rec_bytes(N * F);
   }
   return b;
@@ -1343,68 +1369,74 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
   const int64_t N = g->n_rows;
   // PG_BWD_DIRECT (variant builds): always the argmax-record gather over the transposed CSR
   if (arg_kind == PG_ARG_U16 && F <= kGroupMaxF && N * F < INT32_MAX && !PG_BWD_DIRECT) {
+    if (g->nnz > 0 && !g->einv)
+      return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: g needs einv (in-CSR slot -> transposed index)");
     char* p = (char*)ws + pbytes;
     const int64_t E = g->nnz;
     const int ntiles = (int)bwd_scan_tiles(E);
     int32_t* cnt = (int32_t*)p;
     p += round_up(E * 4, 256);
-    int32_t* off_s = (int32_t*)p;
-    p += round_up(E * 4, 256);
     int32_t* off_t = (int32_t*)p;
     p += round_up((E + 1) * 4, 256);
     auto* lb = (unsigned long long*)p;
     p += round_up((ntiles + 1) * 8, 256);
-    // the records carry the upstream gradient as f32 even for bf16 storage (one rounding of
-    // dx at the end, as the oracle's f32 sums)
-    BRecs recs;
-#if PG_BWD_REC8
-    recs.r = (uint2*)p;
-#else
-    recs.f16 = (uint16_t*)p;
-    recs.val = (float*)(p + round_up(N * F * 2, 256));
-#endif
-    const auto* arg16 = (const uint16_t*)argpos;
-    // rows past kPackWaveMax: the schedule's split rows when its chunk guarantees they are
-    // a superset, else every row
-    const bool listed = g->merges != nullptr && g->chunk > 0 && g->chunk <= kPackWaveMax;
-    const int n_long = (int)(listed ? g->n_merges : N);
-    const int n_short_blocks = (int)((N + kWavesPerBlock - 1) / kWavesPerBlock);
-    // 4 features per lane (vector loads) when every row is 4-aligned
-    constexpr uintptr_t kTa = 4 * sizeof(T) - 1;
-    const bool vec = F % 4 == 0 && lda % 4 == 0 && ldd % 4 == 0 && (!fwd_out || ldf % 4 == 0) &&
-                     ((uintptr_t)argpos & 7) == 0 && ((uintptr_t)dout & kTa) == 0 && ((uintptr_t)fwd_out & kTa) == 0;
-    const dim3 pgrid((unsigned)(n_long + n_short_blocks));
-    const int4* prow = listed ? (const int4*)g->merges : nullptr;
-    if (E > 0) {
-      auto rows = [&](auto nv_c, auto place_c) {
-        constexpr int NV = decltype(nv_c)::value;
-        constexpr bool PL = decltype(place_c)::value;
-        hipLaunchKernelGGL((bwd_rows_kernel<NV, PL, uint16_t, T>), pgrid, dim3(kBlock), 0, st, prow, n_long,
-                           (int)N, g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, g->ew,
-                           PL ? off_s : cnt, recs, lb, PL ? 0 : ntiles + 1);
-        return PG_OK;
-      };
-      auto pass = [&](auto place_c) {
-        if (vec) dispatch_nc_vec((int)((F + 255) / 256), [&](auto n) { return rows(n, place_c); });
-        else rows(std::integral_constant<int, 0>{}, place_c);
-      };
-      pass(std::false_type{});
-      hipLaunchKernelGGL(bwd_scan_kernel, dim3((unsigned)ntiles), dim3(kBlock), 0, st, gt->eslot, (int)E, cnt,
-                         off_s, off_t, lb, ntiles);
-      pass(std::true_type{});
+    // records: {f32 value, feature} (8 B); bf16 storage without edge weights: the bf16
+    // upstream gradient itself, {bf16 value, u16 feature} (4 B). The sums are f32 either way
+    // (one rounding of dx at the end, as the oracle's f32 sums).
+    auto run = [&](auto recs) {
+      using R = decltype(recs);
+      const auto* arg16 = (const uint16_t*)argpos;
+      // rows past kPackWaveMax: the schedule's split rows when its chunk guarantees they are
+      // a superset, else every row
+      const bool listed = g->merges != nullptr && g->chunk > 0 && g->chunk <= kPackWaveMax;
+      const int n_long = (int)(listed ? g->n_merges : N);
+      const int n_short_blocks = (int)((N + kWavesPerBlock - 1) / kWavesPerBlock);
+      // 4 features per lane (vector loads) when every row is 4-aligned
+      constexpr uintptr_t kTa = 4 * sizeof(T) - 1;
+      const bool vec = F % 4 == 0 && lda % 4 == 0 && ldd % 4 == 0 && (!fwd_out || ldf % 4 == 0) &&
+                       ((uintptr_t)argpos & 7) == 0 && ((uintptr_t)dout & kTa) == 0 && ((uintptr_t)fwd_out & kTa) == 0;
+      const dim3 pgrid((unsigned)(n_long + std::min<int64_t>(n_short_blocks, resident_blocks(8))));
+      const int4* prow = listed ? (const int4*)g->merges : nullptr;
+      if (E > 0) {
+        auto rows = [&](auto nv_c, auto place_c) {
+          constexpr int NV = decltype(nv_c)::value;
+          constexpr bool PL = decltype(place_c)::value;
+          hipLaunchKernelGGL((bwd_rows_kernel<NV, PL, uint16_t, T, R>), pgrid, dim3(kBlock), 0, st, prow, n_long,
+                             (int)N, g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, g->ew,
+                             cnt, g->einv, off_t, recs, lb, PL ? 0 : ntiles + 1);
+          return PG_OK;
+        };
+        auto pass = [&](auto place_c) {
+          if (vec) dispatch_nc_vec((int)((F + 255) / 256), [&](auto n) { return rows(n, place_c); });
+          else rows(std::integral_constant<int, 0>{}, place_c);
+        };
+        pass(std::false_type{});
+        hipLaunchKernelGGL(bwd_scan_kernel, dim3((unsigned)ntiles), dim3(kBlock), 0, st, gt->eslot, (int)E, cnt,
+                           off_t, lb, ntiles);
+        pass(std::true_type{});
+      }
+      // dead-none records imply the relu' mask (the contract: mask_src >= 0): every entry
+      // left has a maximum X[u,f] w != 0, so X[u,f] > 0; an element no entry reaches sums to
+      // +0, which the mask would leave +0. With fwd_out alone the mask is applied.
+      const T* mk = dead_none ? nullptr : mask_src;
+      const int sblocks = (int)std::min<int64_t>(grid_for(gt->n_items), (int64_t)resident_blocks(8));
+      hipLaunchKernelGGL((bwd_stream_kernel<T, R>), dim3(sblocks), dim3(kBlock), 0, st,
+                         (const int4*)gt->items, (int)gt->n_items, off_t, recs, (int)F, mk, ldm, dx,
+                         ldx, w, ws_ld(F));
+      if (gt->n_merges > 0)
+        hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
+                           (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
+                           mk, ldm, dx, ldx);
+    };
+    if (sizeof(T) == 2 && !g->ew) {
+      BRecs4 r4;
+      r4.r = (uint32_t*)p;
+      run(r4);
+    } else {
+      BRecs r8;
+      r8.r = (uint2*)p;
+      run(r8);
     }
-    // dead-none records imply the relu' mask (the contract: mask_src >= 0): every entry left
-    // has a maximum X[u,f] w != 0, so X[u,f] > 0; an element no entry reaches sums to +0,
-    // which the mask would leave +0. With fwd_out alone the mask is applied.
-    if (dead_none) mask_src = nullptr;
-    const int sblocks = (int)std::min<int64_t>(grid_for(gt->n_items), (int64_t)resident_blocks(8));
-    hipLaunchKernelGGL((bwd_stream_kernel<T>), dim3(sblocks), dim3(kBlock), 0, st,
-                       (const int4*)gt->items, (int)gt->n_items, off_t, recs, (int)F, mask_src, ldm, dx,
-                       ldx, w, ws_ld(F));
-    if (gt->n_merges > 0)
-      hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
-                         (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
-                         mask_src, ldm, dx, ldx);
     return hip_status("pg_spmm_max_bwd");
   }
   if constexpr (sizeof(T) == 4) {

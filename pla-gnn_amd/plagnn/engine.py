@@ -214,7 +214,7 @@ class TrainEngine:
         for l in range(self.L):
             Fi = pd[l]
             need = max(need, L.pg_spmm_max_fwd_workspace(self.dg.fwd.struct(self.ews), Fi, self.dg.arg_kind))
-            need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd.struct(None), Fi))
+            need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd_stream.struct(None), Fi))
         self._gemm_plans = {}
         # weight gradients' split-K combines deferred to one batched launch per step
         self._slabs: Dict[str, torch.Tensor] = {}
@@ -327,11 +327,26 @@ class TrainEngine:
         the step's own buffers), and that graph is replayed `reps` times back to back
         between two HIP events on the replay stream (no events sit between the launches; the
         graph launch overhead is spread over copies x launches). Returns {g: {ms (per
-        step), launches (per step)}}. Replays of the Adam group train the model; the
-        others recompute the step's buffers from their current inputs."""
+        step), launches (per step)}}. The others recompute the step's buffers from their
+        current inputs; the Adam group's replays would train the model, so the parameters,
+        moments and step count are restored afterwards (later measurements see the model the
+        timed steps left)."""
         out = {}
         cur = torch.cuda.current_stream(self.device)
         s = torch.cuda.Stream(self.device)
+        saved = [t.clone() for t in (self.flat, self.m, self.v, self.adam_state)] if "adam" in groups else None
+        try:
+            self._group_times(groups, reps, warm, copies, cur, s, out)
+        finally:
+            if saved is not None:
+                torch.cuda.synchronize(self.device)
+                for t, c in zip((self.flat, self.m, self.v, self.adam_state), saved):
+                    t.copy_(c)
+                self.params_updated()
+                torch.cuda.synchronize(self.device)
+        return out
+
+    def _group_times(self, groups, reps, warm, copies, cur, s, out) -> None:
         for gname in groups:
             s.wait_stream(cur)
             self._filter, self._issued = gname, 0
@@ -357,7 +372,6 @@ class TrainEngine:
             torch.cuda.synchronize(self.device)
             out[gname] = {"ms": a.elapsed_time(b) / (reps * copies), "launches": launches}
             del g
-        return out
 
     def kernel_breakdown(self, reps: int = 5) -> Dict[str, Dict[str, float]]:
         """Per-launch-site mean duration (ms) and work over `reps` eager steps, timed with
@@ -491,7 +505,7 @@ class TrainEngine:
         st = self._s()
         G, P, pd = self.G, self.P, self.pd
         g = self.dg.fwd.struct(self.ews)
-        gt = self.dg.bwd.struct(None)
+        gt = self.dg.bwd_stream.struct(None)
         # liner2: dW2 = dZ^T A4 (+ db2 = row sums of dZ^T); dA4 came from the fused head
         self._gemm(self.dZ, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
         # liner1

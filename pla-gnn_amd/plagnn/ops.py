@@ -103,9 +103,10 @@ def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
     """dX of the max aggregation (DGL GSpMM.backward: scatter_add_ through argX),
     gathered per source in ascending destination order; optional fused relu' mask
     (mask[u,f] > 0). With `fwd_out` (the forward's output; needs mask = the forward's
-    input, a relu output >= 0) entries whose maximum is 0 are skipped: they contribute
-    nothing, and the mask is implied by the skip (not read). `dead_none`: the records come
-    from spmm_max(..., dead_none=True) (the same skip without fwd_out; needs mask)."""
+    input) entries whose maximum is 0 are skipped: they contribute nothing (the mask is
+    still applied). `dead_none`: the records come from spmm_max(..., dead_none=True) (the
+    same skip made by the forward; needs mask = a relu output >= 0, which is then implied
+    and not read)."""
     _check_device(dg, argpos, dout, ew_slots, mask)
     bf = dout.dtype == torch.bfloat16
     if bf and ((mask is not None and mask.dtype != torch.bfloat16) or not dg.is_cuda):
@@ -114,7 +115,7 @@ def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
     if dx is None:
         dx = torch.empty(n, F, dtype=dout.dtype, device=dout.device)
     g = dg.fwd.struct(ew_slots)
-    gt = dg.bwd.struct(None)
+    gt = (dg.bwd_stream if dg.is_cuda else dg.bwd).struct(None)
     ldm = _ld(mask) if mask is not None else 0
     if dg.is_cuda:
         ws_n = _lib.lib().pg_spmm_max_bwd_workspace(gt, F)

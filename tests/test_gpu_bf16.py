@@ -32,8 +32,10 @@ def _ref(A, B, ta, tb):
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(1000, 256, 512), (4104, 520, 264), (200, 72, 1000), (64, 8, 8),
-                                   (65544, 520, 136), (36000, 512, 576)])  # the last two on 256 x 256 tiles
-                                   # (A B^T there: the ping-pong kernel)
+                                   (65544, 520, 136), (36000, 512, 576), (36000, 520, 584)])
+# (36000, 512, 576) and (36000, 520, 584) run on 256 x 256 tiles (pick_tile needs K >= 384;
+# A B^T there: the ping-pong kernel), the latter with a ragged N and K % 64 != 0 (its
+# partial store and K-tail zero fill)
 def test_gemm_bf16_f32_out(ta, tb, M, N, K):
     from plagnn import ops
 

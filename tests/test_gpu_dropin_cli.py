@@ -14,8 +14,9 @@ machine that made it, and to float32 rounding elsewhere):
 * every epoch's train / val loss of all 10 rounds x 2 folds within 1e-4 relative
   (north_star);
 * the first epoch's logits (the forward at the initial parameters) within 1e-5;
-* the final logits (the forward after two Adam steps) within 1e-3 at the worst entry and
-  6e-5 on average (GPU observed: 3.3e-4 and 2.75e-5 for round 1 fold 1): Adam's first
+* the final logits (the forward after two Adam steps) within 1e-3 at the worst entry,
+  6e-5 on average, and at most FINAL_OVER_1E4 of the entries beyond 1e-4 (GPU round 3:
+  3.3e-4 and 2.75e-5 for round 1 fold 1; the counts are printed): Adam's first
   steps move every parameter by about lr = 5e-5 whatever the size of its gradient, so a
   parameter whose gradient is at rounding level moves by up to 2 lr in different
   directions on two devices, and the logits follow.
@@ -29,6 +30,8 @@ import numpy as np
 import pytest
 import torch
 
+# largest share of final-logit entries allowed beyond north_star's 1e-4
+FINAL_OVER_1E4 = 0.02
 FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "dropin_cli.npz")
 
 
@@ -89,10 +92,14 @@ def _check(dev):
     errs = {}
     for (rnd, fold), got in logits_at.items():
         d = np.abs(got - fx[f"logits_{rnd}_{fold}"])
-        errs[(rnd, fold)] = (float(d.max()), float(d.mean()))
-        print(f"  final logits round {rnd} fold {fold}: max abs err {d.max():.2e}, mean {d.mean():.2e}")
-    for key, (mx, mean) in errs.items():
-        assert mx <= 1e-3 and mean <= 6e-5, (key, mx, mean)
+        over = int((d > 1e-4).sum())
+        errs[(rnd, fold)] = (float(d.max()), float(d.mean()), over / d.size)
+        print(f"  final logits round {rnd} fold {fold}: max abs err {d.max():.2e}, mean {d.mean():.2e}, "
+              f"{over} of {d.size} entries beyond 1e-4")
+    for key, (mx, mean, frac_over) in errs.items():
+        # north_star's 1e-4 holds for all but a bounded share of the entries (those whose
+        # parameters' rounding-level gradients Adam moved by +-lr in another direction)
+        assert mx <= 1e-3 and mean <= 6e-5 and frac_over <= FINAL_OVER_1E4, (key, mx, mean, frac_over)
 
 
 def test_cpu_replay_reproduces_reference_cli():
