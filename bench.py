@@ -284,7 +284,7 @@ def _traffic(config, group, engine):
     PMC passes (profiles/pmc_traffic.json, scripts/pmc_traffic.sh: 2 FETCH_SIZE + WRITE_SIZE
     per KERNEL dispatch), or None. A GEMM call is one kernel; a max-aggregation call is the
     max kernel (+ the merge kernel when the graph has split rows), a max-backward call the
-    count, scan, place and stream kernels (+ the merge)."""
+    pack and pull kernels (+ the merge)."""
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(tfile):
         return None
@@ -292,7 +292,7 @@ def _traffic(config, group, engine):
         b = json.load(f).get(config, {}).get(group)
     if b is None:
         return None
-    per_call = {"spmm_max_fwd": 1 + (engine.dg.fwd.n_merges > 0), "spmm_max_bwd": 4 + (engine.dg.bwd_stream.n_merges > 0)}
+    per_call = {"spmm_max_fwd": 1 + (engine.dg.fwd.n_merges > 0), "spmm_max_bwd": 2 + (engine.dg.bwd.n_merges > 0)}
     return round(b * per_call.get(group, 1))
 
 

@@ -128,9 +128,6 @@ typedef struct pg_csr {
   int64_t n_slots;
   int32_t max_deg;
   int32_t chunk;
-  const int32_t* einv;   /* [nnz] in-CSR only: the transposed index of in-CSR slot k
-                            (einv[tslot[t]] = t); required by pg_spmm_max_bwd[_bf16] (its
-                            place pass finds each edge's list there, ABI 8), else unread */
 } pg_csr_t;
 
 /* ---------------- host: graph construction (code/utils.py:44-45) ---------------- */
@@ -175,7 +172,7 @@ int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, f
  * output, X >= 0): every entry left has X[u,f] * w != 0, hence X[u,f] > 0, so the mask is
  * implied and mask_src is not read (an element no entry reaches is +0 either way). With
  * X < 0 somewhere the result is undefined.
- * The u16 / F <= 1024 path needs g->einv. Every dx element is written (no zero-fill). */
+ * Every dx element is written (no zero-fill needed). */
 size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F);
 int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
                     int arg_kind, const float* dout, int64_t ldd, int64_t F,
@@ -432,9 +429,9 @@ int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-
                          (epilogue without splitk_cnt), no grouped SpMM pair; 6: with fwd_out,
                          pg_spmm_max_bwd[_bf16] takes mask_src >= 0 and does not read it;
                          PG_ARG_DEAD_NONE; 7: pg_spmm_max_bwd reads no einv, smaller
-                         workspace; 8: source-ordered max backward (reads g->einv);
-                         with fwd_out alone the relu' mask is applied, only
-                         PG_ARG_DEAD_NONE implies it */
+                         workspace; 8: pg_csr_t without einv; max backward lists as 8-B
+                         records with the edge weight folded in, dense pull; with fwd_out
+                         alone the relu' mask is applied, only PG_ARG_DEAD_NONE implies it */
 
 #ifdef __cplusplus
 }

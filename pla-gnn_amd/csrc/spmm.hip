@@ -403,79 +403,53 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
   }
 }
 
-// ---- max backward, source-ordered lists (default for u16 records and F <= 1024) -------
-// dX[u,f] = sum over u's out-edges (u -> v), ascending v, of [winner(v,f) is that edge] *
-// w * dout[v,f]: DGL's GSpMM.backward, a sequential scatter_add_ through argX.
-// The live entries (v, f) are regrouped so that every source's terms form ONE contiguous
-// run, in the order its sums need: source-major, ascending destination (the transposed
-// CSR order). Four passes:
-//   1. count  (per destination row v): cnt[s] = live features won by the edge at in-CSR
-//             slot s = ptr[v] + p (a wave per row with an LDS histogram; rows longer than
-//             kPackWaveMax: a workgroup);
-//   2. scan   (transposed order t, one pass with decoupled look-back): off_t[t] = the sum
-//             of cnt over the transposed entries before t;
-//   3. place  (per destination row v): each live (v, f) goes to rec[off_t[einv[s]] + rank]
-//             = {w * dout[v,f], f}; rank comes from an LDS integer atomic on the list's
-//             running offset (the order inside a list is free: a list never repeats a
-//             feature);
-//   4. stream (persistent waves over the transposed items {u, t0, t1}): rec[off_t[t0] ..
-//             off_t[t1]) is read as contiguous 64-record groups and added into an LDS row
-//             in order: each lane reads its word, adds, and swaps the sum in with
-//             ds_cmpst (compare-and-swap); lanes of one instruction that hit the same word
-//             are applied in ascending lane order, so of two records of one feature the
-//             earlier one's swap succeeds and the later one retries on its result. Every
-//             feature's terms are thus summed in ascending v, the order of the sequential
-//             scatter_add_: bit-exact on rows that are not split across items. (LDS float
-//             atomics, ds_add_f32, keep the same order but run at 1/16 of the integer
-//             atomics' rate on gfx950: scripts/probes/lds_rmw_probe.hip.)
-// The scatter that round 3's pull did with reads (one random descriptor line and two
-// random list lines per edge, 292 MB fetched per F = 256 launch for ~60 MB of lists) is
-// done by the place pass's writes instead; the stream pass reads sequential lines only.
-constexpr int kHistMax = 4096;  // longest row whose lists a workgroup counts in LDS
+// ---- max backward, grouped form (default for u16 records and F <= 1024) ---------------
+// Pass 1 (pack), per destination row v: group v's features by their winning in-row
+// position p, giving
+//   gfeat[v F + i]  the features, grouped by p (any order inside a group),
+//   dpack[v F + i]  = dout[v][gfeat[v F + i]]   (the upstream gradient in list order),
+//   glist[s]        = {v F + start_p, count_p} for the edge at in-CSR slot s = ptr[v] + p
+//                     (a row's descriptors are contiguous: coalesced stores).
+// Rows of in-degree <= kPackWaveMax: one wave per row (wave-private LDS histogram, wave
+// scan, LDS-atomic placement); longer rows: one workgroup per row (block histogram, or a
+// bitonic sort of (p << 16 | f) keys past kHistMax entries).
+// Pass 2 (pull), one wave per source row u: for each out-edge of u, ascending destination
+// v (the transposed CSR order), read its descriptor glist[tslot[t]] (the transposed
+// entry's in-CSR slot; loaded a window ahead) and add dpack[list] (* w) into an LDS row accumulator at gfeat[list]. A list never
+// repeats a feature, so one instruction's lanes hit distinct LDS words and every
+// feature's terms are summed in ascending v, the order of the sequential scatter_add_:
+// the order inside a list does not matter. Traffic per edge: its 4-B slot, one 8-B
+// descriptor and two short contiguous runs (~F/deg entries). (Descriptors stored at the
+// transposed index instead, read coalesced but written scattered by the pack: the cfg2
+// backward 259 vs 256 us per step.)
+constexpr int kHistMax = 4096;
 constexpr int kGroupMaxF = 1024;
 #ifndef PG_BWD_DIRECT
 #define PG_BWD_DIRECT 0
 #endif
-#ifndef PG_STREAM_PROBE
-#define PG_STREAM_PROBE 0  // timing-only probes (wrong results): 1 no atomics, 2 no record loads, 3 no stores
-#endif
-#ifndef PG_SCAN_PROBE
-#define PG_SCAN_PROBE 0    // timing-only probe: 1 = no look-back (every tile's prefix 0)
-#endif
-#ifndef PG_STREAM_U
-#define PG_STREAM_U 4  // 64-entry groups in flight per wave in the stream pass
-#endif
 
-// one record per entry: {value f32, feature} in 8 B; for bf16 storage without edge weights
-// the value is a bf16 upstream gradient taken as is, so {value bf16, feature u16} in 4 B
-struct BRecs {
+// one 8-B record {value f32, feature u32} per list entry (one contiguous run per list:
+// one line for the pull to fetch where two arrays cost two); the value carries the edge
+// weight already (w * dout[v,f], the product the pull formed before)
+struct GPack {
   uint2* __restrict__ r;
-  static constexpr int kBytes = 8;
-  __device__ __forceinline__ void put(int pos, int f, float d) const {
+  __device__ __forceinline__ void put(int64_t pos, int f, float d) const {
     r[pos] = make_uint2(__float_as_uint(d), (uint32_t)f);
   }
-  __device__ __forceinline__ void get(int pos, int& f, float& d) const {
+  __device__ __forceinline__ void get(int64_t pos, int& f, float& d) const {
     const uint2 x = r[pos];
     d = __uint_as_float(x.x);
     f = (int)x.y;
   }
 };
-struct BRecs4 {
-  uint32_t* __restrict__ r;
 
-  __device__ __forceinline__ void put(int pos, int f, float d) const {
-    r[pos] = (__float_as_uint(d) & 0xFFFF0000u) | (uint32_t)f;  // d is a bf16 value: exact
-  }
-  __device__ __forceinline__ void get(int pos, int& f, float& d) const {
-    const uint32_t x = r[pos];
-    d = __uint_as_float(x & 0xFFFF0000u);
-    f = (int)(x & 0xFFFFu);
-  }
-};
-
+#ifndef PG_SCAN_DPP
+#define PG_SCAN_DPP 1
+#endif
 // inclusive prefix sum over the 64 lanes: DPP row shifts, then row broadcasts 15 and 31
 // (six VALU ops; the __shfl_up form is six dependent ds_bpermute round trips)
 __device__ __forceinline__ int wave_incl_add(int x) {
+#if PG_SCAN_DPP
   x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
   x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
   x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
@@ -483,406 +457,518 @@ __device__ __forceinline__ int wave_incl_add(int x) {
   x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
   x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return x;
+#else
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  return x;
+#endif
 }
 
-// A destination row's entries as the lanes hold them. NV > 0 (F % 4 == 0, F <= 256 NV):
-// lane l owns features 256 c + 4 l + i, loaded 4 at a time at clamped columns (no branch
-// between the record and gradient loads, so both are in flight before the first wait).
-// NV == 0: lane l owns features l + 64 k (k < 16).
-template <int NV>
-struct RowLanes {
-  static constexpr int K = NV > 0 ? NV * 4 : kGroupMaxF / kWave;
-  __device__ static __forceinline__ int feat(int k, int lane) {
-    return NV > 0 ? ((k >> 2) * kWave + lane) * 4 + (k & 3) : lane + k * kWave;
-  }
-};
+__device__ int block_exclusive_scan(int* s, int n, int* wsum) {
+  const int per = (n + kBlock - 1) / kBlock;
+  const int b = threadIdx.x * per;
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  int local = 0;
+  for (int i = 0; i < per; ++i)
+    if (b + i < n) local += s[b + i];
+  int x = local;
+  x = wave_incl_add(x);
+  if (lane == kWave - 1) wsum[wave] = x;
+  __syncthreads();
+  int pre = 0;
+  for (int w = 0; w < wave; ++w) pre += wsum[w];
+  int run = pre + x - local;
+  for (int i = 0; i < per; ++i)
+    if (b + i < n) {
+      const int t = s[b + i];
+      s[b + i] = run;
+      run += t;
+    }
+  const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return total;
+}
 
-// a[k] = winning in-row position of the lane's k-th feature, or -1 if it has no live
-// winner (none, a zero forward maximum when fout is given, or an out-of-row position);
-// d[k] = its upstream gradient (LOAD_D)
-template <int NV, bool LOAD_D, typename A, typename T>
-__device__ __forceinline__ void load_row(int v, int lane, int deg, const A* __restrict__ arg,
-                                         int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-                                         const T* __restrict__ fout, int64_t ldf,
-                                         int (&a)[RowLanes<NV>::K], float (&d)[RowLanes<NV>::K]) {
-  constexpr int K = RowLanes<NV>::K;
+template <typename A, typename T>
+__device__ __forceinline__ void pack_short_row(
+    int v, int wave, const int32_t* __restrict__ ptr,
+    const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, GPack gp, int2* __restrict__ glist,
+    int* __restrict__ lds) {
+  constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
+  const int lane = lane_id();
+  // every independent load first: the row bounds, the argmax record and the upstream
+  // gradient (each lane its own features, coalesced), then the list descriptors' slots
+  const int rs = ptr[v];
+  const int re = ptr[v + 1];
   const A* ar = arg + (int64_t)v * lda;
-  if constexpr (NV > 0) {
+  const T* dr = dout + (int64_t)v * ldd;
+  int a[MAXW];
+  float d[MAXW];
 #pragma unroll
-    for (int c = 0; c < NV; ++c) {
-      const int f = (c * kWave + lane) * 4;
-      const int fc = min(f, F - 4);
-      int ac[4];
-      float dc[4] = {0.f, 0.f, 0.f, 0.f};
-      load_arg<4, A>(ar, fc, F, ac);
-      if constexpr (LOAD_D) load_tile<4, T>(dout + (int64_t)v * ldd, fc, F, dc, 0.f);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[c * 4 + i] = f < F ? ac[i] : arg_none<A>();
-        d[c * 4 + i] = dc[i];
-      }
-    }
-    if (fout) {
-#pragma unroll
-      for (int c = 0; c < NV; ++c) {
-        float m[4];
-        load_tile<4, T>(fout + (int64_t)v * ldf, (c * kWave + lane) * 4, F, m, 1.f);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (m[i] == 0.f) a[c * 4 + i] = arg_none<A>();
-      }
-    }
-  } else {
-    const T* dr = dout + (int64_t)v * ldd;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int f = lane + k * kWave;
-      const int fc = min(f, F - 1);
-      const int ak = (int)ar[fc];
-      a[k] = f < F ? ak : arg_none<A>();
-      d[k] = LOAD_D ? to_f(dr[fc]) : 0.f;
-    }
-    if (fout) {
-      const T* fr = fout + (int64_t)v * ldf;
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        if (to_f(fr[min(lane + k * kWave, F - 1)]) == 0.f) a[k] = arg_none<A>();
-    }
+  for (int i = 0; i < MAXW; ++i) {
+    const int f = lane + i * kWave;
+    a[i] = f < F ? (int)ar[f] : arg_none<A>();
+    d[i] = f < F ? to_f(dr[f]) : 0.f;
   }
+  if (fout) {  // a zero maximum: its winner's relu mask is 0, the entry contributes nothing
+    const T* fr = fout + (int64_t)v * ldf;
+    float m[MAXW];
 #pragma unroll
-  for (int k = 0; k < K; ++k)
-    if (a[k] == arg_none<A>() || a[k] >= deg) a[k] = -1;
-}
-
-// Passes 1 and 3 for a row of in-degree 1..kPackWaveMax, one wave. PLACE = false: count
-// into cnt[s]; PLACE = true: the list of slot s starts at off_t[einv[s]] (einv: in-CSR slot
-// -> transposed index), each live entry takes the next place of its list.
-template <int NV, bool PLACE, typename A, typename T, typename R>
-__device__ __forceinline__ void bwd_short_row(int v, int rs, int deg, int lane, int* __restrict__ hist,
-                                              const A* __restrict__ arg, int64_t lda, int F,
-                                              const T* __restrict__ dout, int64_t ldd,
-                                              const T* __restrict__ fout, int64_t ldf,
-                                              const float* __restrict__ ew,
-                                              int32_t* __restrict__ cnt,
-                                              const int32_t* __restrict__ einv,
-                                              const int32_t* __restrict__ off_t, R recs) {
-  constexpr int K = RowLanes<NV>::K;
+    for (int i = 0; i < MAXW; ++i) m[i] = to_f(fr[min(lane + i * kWave, F - 1)]);
+#pragma unroll
+    for (int i = 0; i < MAXW; ++i)
+      if (m[i] == 0.f) a[i] = arg_none<A>();
+  }
+  const int deg = re - rs;
   if (deg > kPackWaveMax || deg == 0) return;
-  int a[K];
-  float d[K];
-  load_row<NV, PLACE>(v, lane, deg, arg, lda, F, dout, ldd, fout, ldf, a, d);
-  for (int p = lane; p < deg; p += kWave) hist[p] = PLACE ? off_t[einv[rs + p]] : 0;
-  if constexpr (PLACE) {
-    if (ew) {  // the edge weight folded into the value: the product the pull formed, w * d
-      float w[K];
+  const int B = (deg + kWave - 1) / kWave;  // bins per lane, <= 4
+  int ei[4];
 #pragma unroll
-      for (int k = 0; k < K; ++k) w[k] = ew[rs + max(a[k], 0)];
+  for (int q = 0; q < 4; ++q) {
+    const int p = lane * B + q;
+    ei[q] = (q < B && p < deg) ? rs + p : 0;
+  }
+  int* hist = lds + wave * (kPackWaveMax + 4);
+  for (int p = lane; p < deg; p += kWave) hist[p] = 0;
+  wave_lds_sync();
 #pragma unroll
-      for (int k = 0; k < K; ++k) d[k] = w[k] * d[k];
+  for (int i = 0; i < MAXW; ++i)
+    if (a[i] != arg_none<A>()) atomicAdd(&hist[a[i]], 1);
+  wave_lds_sync();
+  // exclusive scan over the deg bins: lane owns bins [lane B, lane B + B)
+  int c[4], local = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = lane * B + q;
+    c[q] = (q < B && p < deg) ? hist[p] : 0;
+    local += c[q];
+  }
+  int x = local;
+  x = wave_incl_add(x);
+  int run = x - local;
+  const int vF = v * F;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = lane * B + q;
+    if (q < B && p < deg) {
+      hist[p] = run;
+      glist[ei[q]] = make_int2(vF + run, c[q]);
+      run += c[q];
     }
   }
   wave_lds_sync();
-  if constexpr (PLACE) {
+  // placement: every winner straight to its list slot (the order inside a list is free)
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-      if (a[k] >= 0) recs.put(atomicAdd(&hist[a[k]], 1), RowLanes<NV>::feat(k, lane), d[k]);
-  } else {
+  for (int i = 0; i < MAXW; ++i)
+    if (a[i] != arg_none<A>()) {
+      const int pos = vF + atomicAdd(&hist[a[i]], 1);
+      gp.put(pos, lane + i * kWave, ew ? ew[rs + a[i]] * d[i] : d[i]);
+    }
+}
+
+// The same for F <= 256 NV with rows of 4-aligned features: lane l owns the features
+// 256 c + 4 l + i (c < NV, i < 4), loaded 4 at a time (argmax records 8 B, upstream
+// gradient and forward output 16 B or 8 B), and one LDS atomic per live feature both
+// counts its winning position and ranks it inside that position's list (the order inside
+// a list is free); the list offsets come from one wave scan over the positions. The lists
+// are assembled in LDS and copied out with coalesced stores (scattered 2-B global stores
+// are read-modify-writes of partial lines): -6 % for the whole backward on cfg2.
+template <int NV>
+constexpr int pack_wave_ints() { return kPackWaveMax + 4 + NV * 512; }  // hist | records (8 B)
+
+template <int NV, typename A, typename T>
+__device__ __forceinline__ void pack_short_row_v(
+    int v, int wave, const int32_t* __restrict__ ptr,
+    const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, GPack gp, int2* __restrict__ glist,
+    int* __restrict__ lds) {
+  const int lane = lane_id();
+  const int rs = ptr[v];
+  const int deg = ptr[v + 1] - rs;
+  if (deg > kPackWaveMax || deg == 0) return;
+  int a[NV][4];
+  float d[NV][4];
+  // straight-line loads at clamped columns (F % 4 == 0 here), masked afterwards: no branch
+  // between the record and gradient loads, so both are in flight before the first wait
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-      if (a[k] >= 0) atomicAdd(&hist[a[k]], 1);
-    wave_lds_sync();
-    for (int p = lane; p < deg; p += kWave) cnt[rs + p] = hist[p];
+  for (int c = 0; c < NV; ++c) {
+    const int f = (c * kWave + lane) * 4;
+    const int fc = min(f, F - 4);
+    int ac[4];
+    float dc[4];
+    load_arg<4, A>(arg + (int64_t)v * lda, fc, F, ac);
+    load_tile<4, T>(dout + (int64_t)v * ldd, fc, F, dc, 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[c][i] = f < F ? ac[i] : arg_none<A>();
+      d[c][i] = f < F ? dc[i] : 0.f;
+    }
+  }
+  if (fout) {  // a zero maximum: its winner's relu mask is 0, the entry contributes nothing
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      float m[4];
+      load_tile<4, T>(fout + (int64_t)v * ldf, (c * kWave + lane) * 4, F, m, 1.f);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (m[i] == 0.f) a[c][i] = arg_none<A>();
+    }
+  }
+  const int B = (deg + kWave - 1) / kWave;  // bins per lane, <= 4
+  int ei[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = lane * B + q;
+    ei[q] = (q < B && p < deg) ? rs + p : 0;
+  }
+  int* hist = lds + wave * pack_wave_ints<NV>();
+  uint2* lr = reinterpret_cast<uint2*>(hist + kPackWaveMax + 4);  // 16-B aligned: kPackWaveMax + 4 = 260 ints
+  for (int p = lane; p < deg; p += kWave) hist[p] = 0;
+  wave_lds_sync();
+  int rank[NV][4];
+#pragma unroll
+  for (int c = 0; c < NV; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      rank[c][i] = a[c][i] != arg_none<A>() ? atomicAdd(&hist[a[c][i]], 1) : 0;
+  wave_lds_sync();
+  int cq[4], local = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = lane * B + q;
+    cq[q] = (q < B && p < deg) ? hist[p] : 0;
+    local += cq[q];
+  }
+  int x = local;
+  x = wave_incl_add(x);
+  int run = x - local;
+  const int vF = v * F;
+  wave_lds_sync();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = lane * B + q;
+    if (q < B && p < deg) {
+      hist[p] = run;
+      glist[ei[q]] = make_int2(vF + run, cq[q]);
+      run += cq[q];
+    }
+  }
+  wave_lds_sync();
+  if (ew) {  // the edge weight folded into the value: w * d, the product the pull formed
+#pragma unroll
+    for (int c = 0; c < NV; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[c][i] = ew[rs + (a[c][i] != arg_none<A>() ? a[c][i] : 0)] * d[c][i];
+  }
+#pragma unroll
+  for (int c = 0; c < NV; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (a[c][i] != arg_none<A>()) {
+        const int pos = hist[a[c][i]] + rank[c][i];
+        lr[pos] = make_uint2(__float_as_uint(d[c][i]), (uint32_t)((c * kWave + lane) * 4 + i));
+      }
+  wave_lds_sync();
+  const int total = __builtin_amdgcn_readlane(x, kWave - 1);
+  // 2 records per lane and store (16 B; vF and the LDS image are 16-B aligned: F % 4 == 0)
+  for (int i = lane * 2; i < total; i += 2 * kWave) {
+    if (i + 2 <= total) *reinterpret_cast<uint4*>(gp.r + vF + i) = *reinterpret_cast<const uint4*>(lr + i);
+    else gp.r[vF + i] = lr[i];
   }
 }
 
-// The same for a row longer than kPackWaveMax, one workgroup (thread t owns features
-// t + 256 i). Past kHistMax entries the counters are global integer atomics (order-free).
-template <bool PLACE, typename A, typename T, typename R>
-__device__ __forceinline__ void bwd_long_row(int v, int* __restrict__ hist,
-                                             const int32_t* __restrict__ ptr,
-                                             const A* __restrict__ arg, int64_t lda, int F,
-                                             const T* __restrict__ dout, int64_t ldd,
-                                             const T* __restrict__ fout, int64_t ldf,
-                                             const float* __restrict__ ew,
-                                             int32_t* __restrict__ cnt,
-                                             const int32_t* __restrict__ einv,
-                                             const int32_t* __restrict__ off_t, R recs) {
-  constexpr int FPT = kGroupMaxF / kBlock;
+template <typename A, typename T>
+__device__ __forceinline__ void pack_long_row(
+    int v, const int32_t* __restrict__ ptr,
+    const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, GPack gp, int2* __restrict__ glist,
+    int* __restrict__ lds) {
+  int* hist = lds;
+  uint16_t* feats = reinterpret_cast<uint16_t*>(lds + kHistMax + 8);
+  int* wsum = lds + kHistMax + 8 + kGroupMaxF / 2;
   const int rs = ptr[v];
   const int deg = ptr[v + 1] - rs;
   if (deg <= kPackWaveMax) return;
   const A* ar = arg + (int64_t)v * lda;
-  int a[FPT];
-  float d[FPT];
-#pragma unroll
-  for (int i = 0; i < FPT; ++i) {
-    const int f = threadIdx.x + i * kBlock;
-    a[i] = f < F ? (int)ar[f] : arg_none<A>();
-    d[i] = PLACE && f < F ? to_f(dout[(int64_t)v * ldd + f]) : 0.f;
-    if (f < F && fout && to_f(fout[(int64_t)v * ldf + f]) == 0.f) a[i] = arg_none<A>();
-    if (a[i] == arg_none<A>() || a[i] >= deg) a[i] = -1;
-    if (PLACE && ew && a[i] >= 0) d[i] = ew[rs + a[i]] * d[i];
-  }
+  const int64_t vF = (int64_t)v * F;
+  int total;
   if (deg <= kHistMax) {
-    for (int p = threadIdx.x; p < deg; p += kBlock) hist[p] = PLACE ? off_t[einv[rs + p]] : 0;
-    __syncthreads();
+    // independent loads first (each thread its own features), placement straight to the
+    // list slots as in the wave form
+    constexpr int FPT = kGroupMaxF / kBlock;
+    const T* dr = dout + (int64_t)v * ldd;
+    int a[FPT];
+    float d[FPT];
 #pragma unroll
-    for (int i = 0; i < FPT; ++i)
-      if (a[i] >= 0) {
-        const int pos = atomicAdd(&hist[a[i]], 1);
-        if (PLACE) recs.put(pos, threadIdx.x + i * kBlock, d[i]);
-      }
-    if (!PLACE) {
-      __syncthreads();
-      for (int p = threadIdx.x; p < deg; p += kBlock) cnt[rs + p] = hist[p];
+    for (int i = 0; i < FPT; ++i) {
+      const int f = threadIdx.x + i * kBlock;
+      a[i] = f < F ? (int)ar[f] : arg_none<A>();
+      d[i] = f < F ? to_f(dr[f]) : 0.f;
     }
-  } else {
-    // the row's counters in cnt (the scan has read it by the place pass), cleared first
-    for (int p = threadIdx.x; p < deg; p += kBlock) cnt[rs + p] = 0;
-    __threadfence();
+    if (fout) {  // zero maxima contribute nothing (their winner's relu mask is 0)
+      const T* fr = fout + (int64_t)v * ldf;
+      float m[FPT];
+#pragma unroll
+      for (int i = 0; i < FPT; ++i) m[i] = to_f(fr[min((int)threadIdx.x + i * kBlock, F - 1)]);
+#pragma unroll
+      for (int i = 0; i < FPT; ++i)
+        if (m[i] == 0.f) a[i] = arg_none<A>();
+    }
+    for (int p = threadIdx.x; p < deg; p += kBlock) hist[p] = 0;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < FPT; ++i)
-      if (a[i] >= 0) {
-        const int rank = atomicAdd(&cnt[rs + a[i]], 1);
-        if (PLACE) recs.put(off_t[einv[rs + a[i]]] + rank, threadIdx.x + i * kBlock, d[i]);
+      if (a[i] != arg_none<A>()) atomicAdd(&hist[a[i]], 1);
+    __syncthreads();
+    total = block_exclusive_scan(hist, deg, wsum);
+    for (int p0 = threadIdx.x; p0 < deg; p0 += 4 * kBlock) {
+      int e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = p0 + j * kBlock;
+        e[j] = p < deg ? rs + p : 0;
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = p0 + j * kBlock;
+        if (p < deg) {
+          const int st = hist[p];
+          const int en = p + 1 < deg ? hist[p + 1] : total;
+          glist[e[j]] = make_int2((int)(vF + st), en - st);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FPT; ++i)
+      if (a[i] != arg_none<A>()) {
+        const int64_t pos = vF + atomicAdd(&hist[a[i]], 1);
+        gp.put(pos, threadIdx.x + i * kBlock, ew ? ew[rs + a[i]] * d[i] : d[i]);
+      }
+    return;
+  } else {
+    // hub row: bitonic sort of (p << 16 | f) keys; "none" sorts last
+    uint32_t* keys = reinterpret_cast<uint32_t*>(hist);
+    int np = 1;
+    while (np < F) np <<= 1;
+    for (int i = threadIdx.x; i < np; i += kBlock) {
+      uint32_t key = 0xFFFFFFFFu;
+      if (i < F) {
+        const int a = (int)ar[i];
+        const bool live = !fout || to_f(fout[(int64_t)v * ldf + i]) != 0.f;
+        if (a != arg_none<A>() && live) key = ((uint32_t)a << 16) | (uint32_t)i;
+      }
+      keys[i] = key;
+    }
+    __syncthreads();
+    for (int k = 2; k <= np; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < np; i += kBlock) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const uint32_t a = keys[i], b = keys[ixj];
+            if ((a > b) == ((i & k) == 0)) {
+              keys[i] = b;
+              keys[ixj] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    auto lower = [&](uint32_t key) {
+      int lo = 0, hi = np;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < key) lo = mid + 1; else hi = mid;
+      }
+      return lo;
+    };
+    for (int p = threadIdx.x; p < deg; p += kBlock) {
+      const int st = lower((uint32_t)p << 16);
+      const int en = lower((uint32_t)(p + 1) << 16);
+      glist[rs + p] = make_int2((int)(vF + st), en - st);
+    }
+    if (threadIdx.x == 0) wsum[0] = lower(0xFFFFFFFFu);
+    __syncthreads();
+    total = wsum[0];
+    for (int i = threadIdx.x; i < total; i += kBlock) feats[i] = (uint16_t)(keys[i] & 0xFFFFu);
+    __syncthreads();
+  }
+  const T* dr = dout + (int64_t)v * ldd;
+  for (int i = threadIdx.x; i < total; i += kBlock) {
+    const int f = feats[i];
+    const float dv = to_f(dr[f]);
+    gp.put(vF + i, f, ew ? ew[rs + (int)(reinterpret_cast<const uint32_t*>(hist)[i] >> 16)] * dv : dv);
   }
 }
 
-// Passes 1 / 3, one launch each: blocks [0, n_long) take the rows past kPackWaveMax (`rows`
-// lists them as {row, ...} int4 = the split-row merges of a forward schedule whose chunk is
-// <= kPackWaveMax; NULL = every row, short ones exit at once) so the long rows start first;
-// the remaining blocks take 4 rows each, one wave per row. The count pass also clears the
-// scan's look-back words (lb, n_lb of them) for this call.
-template <int NV, bool PLACE, typename A, typename T, typename R>
-__global__ __launch_bounds__(kBlock) void bwd_rows_kernel(
+// One launch for both: blocks [0, n_long) take the rows past kPackWaveMax (`rows` lists
+// them, as {row, ...} int4 = the split-row merges of a schedule whose chunk is <=
+// kPackWaveMax; NULL = every row, short ones exit at once) so the long rows start first;
+// the remaining blocks take 4 rows each, one wave per row.
+constexpr int kPackLds = kHistMax + 8 + kGroupMaxF / 2 + 4;
+static_assert(kPackLds >= kWavesPerBlock * (kPackWaveMax + 4), "pack LDS");
+
+template <typename A, typename T = float, int NV = 0>
+__global__ __launch_bounds__(kBlock) void group_pack_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
-    const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew,
-    int32_t* __restrict__ cnt, const int32_t* __restrict__ einv, const int32_t* __restrict__ off_t,
-    R recs, unsigned long long* __restrict__ lb, int n_lb) {
-  __shared__ __attribute__((aligned(16))) int lds[kHistMax];
-  static_assert(kHistMax >= kWavesPerBlock * kPackWaveMax, "short-row histograms");
-  if (!PLACE)
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n_lb; i += gridDim.x * kBlock) lb[i] = 0ull;
+    const A* __restrict__ arg, int64_t lda, int F,
+    const T* __restrict__ dout, int64_t ldd, const T* __restrict__ fout, int64_t ldf,
+    const float* __restrict__ ew, GPack gp, int2* __restrict__ glist) {
+  constexpr int kLds = NV > 0 && kWavesPerBlock * pack_wave_ints<NV>() > kPackLds
+                           ? kWavesPerBlock * pack_wave_ints<NV>() : kPackLds;
+  __shared__ __attribute__((aligned(16))) int lds[kLds];
   const int b = blockIdx.x;
   if (b < n_long) {
-    bwd_long_row<PLACE, A, T, R>(rows ? rows[b].x : b, lds, ptr, arg, lda, F, dout, ldd, fout, ldf, ew,
-                              cnt, einv, off_t, recs);
+    pack_long_row<A, T>(rows ? rows[b].x : b, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
   } else {
-    // persistent waves over the short rows: wave w takes rows w, w + W, ...; its 64 lanes
-    // fetch 64 rows' bounds at once (one round trip per 64 rows instead of one in front of
-    // every row)
     const int wave = wave_id_uniform();
-    const int lane = lane_id();
-    const int W = ((int)gridDim.x - n_long) * kWavesPerBlock;
-    for (int base = (b - n_long) * kWavesPerBlock + wave; base < n_rows; base += kWave * W) {
-      const int my = base + lane * W;
-      int rs_l = 0, re_l = 0;
-      if (my < n_rows) {
-        rs_l = ptr[my];
-        re_l = ptr[my + 1];
-      }
-      const int nb = min(kWave, (n_rows - base + W - 1) / W);
-      for (int j = 0; j < nb; ++j) {
-        const int rs = bcast(rs_l, j);
-        bwd_short_row<NV, PLACE, A, T, R>(base + j * W, rs, bcast(re_l, j) - rs, lane, lds + wave * kPackWaveMax,
-                                          arg, lda, F, dout, ldd, fout, ldf, ew, cnt, einv, off_t, recs);
-      }
+    const int v = (b - n_long) * kWavesPerBlock + wave;
+    if (v < n_rows)
+    {
+      if constexpr (NV > 0)
+        pack_short_row_v<NV, A, T>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
+      else
+        pack_short_row<A, T>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
     }
   }
 }
 
-// Pass 2: exclusive scan of cnt in the transposed order, one pass (off_t only: the place
-// pass gathers its lists' offsets through einv; scattering them to in-CSR slots here
-// instead was slower). Tiles of kScanTile
-// entries are taken in ticket order (an atomic counter, so every tile's predecessors are
-// already running); each publishes its sum, then its inclusive prefix, in one 64-bit word
-// {status:2 | value:62} (a single atomic store carries both, no fence needed). Wave 0
-// looks back over 64 predecessors at a time. The spin is bounded, so a broken invariant
-// gives wrong offsets (caught by the tests), never a hung GPU.
-constexpr int kScanIpt = 4;
-constexpr int kScanTile = kBlock * kScanIpt;
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62;
-constexpr unsigned long long kLbVal = (1ull << 62) - 1;
-
-__device__ __forceinline__ unsigned long long lb_load(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// inclusive max-scan over the 64 lanes (values >= -1), the DPP pattern of wave_incl_add
+__device__ __forceinline__ int wave_incl_max(int x) {
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return x;
 }
 
-__global__ __launch_bounds__(kBlock) void bwd_scan_kernel(
-    const int32_t* __restrict__ tslot, int nnz, const int32_t* __restrict__ cnt,
-    int32_t* __restrict__ off_t, unsigned long long* __restrict__ lb, int ntiles) {
-  __shared__ int s_tile, s_prefix;
-  __shared__ int wsum[kWavesPerBlock];
-  if (threadIdx.x == 0)
-    s_tile = (int)atomicAdd(reinterpret_cast<unsigned int*>(lb + ntiles), 1u);
-  __syncthreads();
-  const int tile = s_tile;
-  const int lane = lane_id(), wave = (int)(threadIdx.x >> 6);
-  const int t0 = tile * kScanTile + (int)threadIdx.x * kScanIpt;
-  int ts[kScanIpt], c[kScanIpt];
-#pragma unroll
-  for (int j = 0; j < kScanIpt; ++j) ts[j] = tslot[min(t0 + j, nnz - 1)];
-#pragma unroll
-  for (int j = 0; j < kScanIpt; ++j) c[j] = cnt[ts[j]];
-  int local = 0;
-#pragma unroll
-  for (int j = 0; j < kScanIpt; ++j) {
-    if (t0 + j >= nnz) c[j] = 0;
-    local += c[j];
-  }
-  const int incl = wave_incl_add(local);
-  if (lane == kWave - 1) wsum[wave] = incl;
-  __syncthreads();
-  int wave_pre = 0, agg = 0;
-#pragma unroll
-  for (int w = 0; w < kWavesPerBlock; ++w) {
-    wave_pre += w < wave ? wsum[w] : 0;
-    agg += wsum[w];
-  }
-  if (wave == 0) {
-    int prefix = 0;
-    if (PG_SCAN_PROBE == 1 || tile == 0) {
-      if (lane == 0) lb_store(lb, kLbInc | (unsigned long long)agg);
-    } else {
-      if (lane == 0) lb_store(lb + tile, kLbAgg | (unsigned long long)agg);
-      int j = tile - 1;
-      for (;;) {
-        const int idx = j - lane;
-        unsigned long long s = idx >= 0 ? lb_load(lb + idx) : kLbInc;
-        for (int spin = 0; __ballot((s >> 62) == 0) != 0; ++spin) {
-          if (spin > (1 << 22)) {  // never reached when every tile publishes
-            s = kLbInc;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          if ((s >> 62) == 0) s = lb_load(lb + idx);
-        }
-        const unsigned long long inc = __ballot((s >> 62) == 2);
-        const int first = inc ? __ffsll((long long)inc) - 1 : kWave - 1;
-        const int val = wave_incl_add(lane <= first ? (int)(s & kLbVal) : 0);
-        prefix += __builtin_amdgcn_readlane(val, kWave - 1);
-        if (inc) break;
-        j -= kWave;
-      }
-      if (lane == 0) lb_store(lb + tile, kLbInc | (unsigned long long)(prefix + agg));
-    }
-    if (lane == 0) s_prefix = prefix;
-  }
-  __syncthreads();
-  int run = s_prefix + wave_pre + incl - local;
-#pragma unroll
-  for (int j = 0; j < kScanIpt; ++j) {
-    if (t0 + j < nnz) off_t[t0 + j] = run;
-    run += c[j];
-  }
-  if (tile == ntiles - 1 && threadIdx.x == 0) off_t[nnz] = s_prefix + agg;
-}
+#ifndef PG_PULL_U
+#define PG_PULL_U 4  // 64-entry segments in flight per wave
+#endif
+#ifndef PG_PULL_PROBE
+#define PG_PULL_PROBE 0  // timing-only probes (wrong results): 1 plain LDS adds, 2 no record loads
+#endif
 
-// Pass 4: persistent waves over the transposed items (each item's records are one
-// contiguous run). A wave takes items it, it + W, it + 2W, ... (W = waves in the grid); the
-// 64 lanes first fetch 64 of its items and their record ranges at once (two round trips per
-// 64 items instead of two dependent ones in front of every item), then the wave walks them.
-template <typename T, typename R>
-__global__ __launch_bounds__(kBlock) void bwd_stream_kernel(
-    const int4* __restrict__ items, int n_items, const int32_t* __restrict__ off_t, R recs,
-    int F, const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx,
-    float* __restrict__ ws, int64_t ldw) {
-  constexpr int U = PG_STREAM_U;
-  // the row, then 64 words that lanes past the run add their +0 into (distinct words: no
-  // serialised same-address atomics; the adds stay unconditional, so the compiler keeps the
-  // loads in flight together instead of sinking each behind its lane mask)
-  __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF + kWave];
+// Pass 2 (pull), dense: one wave per source-row item {u, t0, t1, slot}, its out-edges in
+// windows of 64 (ascending destination). Lane j holds window edge j's descriptor
+// {off, cnt} (loaded through its in-CSR slot tslot[t]). The window's lists, concatenated in
+// edge order, are cut into 64-entry segments, U at a time, so every load instruction
+// carries up to 64 entries of several lists (round 3's pull issued one instruction per
+// list of ~F/deg entries): lane L of segment k takes entry e = 64 k + L, whose edge is the
+// last one whose list starts at or before e (a start marker per list in LDS, an inclusive
+// max-scan across the lanes, carried from segment to segment), and loads record
+// off_j + e - excl_j. Records are added into the LDS row in entry order by
+// compare-and-swap: each lane reads its word, adds, and swaps the sum in; lanes of one
+// instruction that hit the same word are applied in ascending lane order, so the later
+// entry's swap fails and it retries on the earlier one's sum. Every feature's terms are
+// thus summed in ascending v, the sequential scatter_add_'s order (bit-exact on rows that
+// are not split across items). (LDS float atomics, ds_add_f32, keep the same order but run
+// at 1/16 of the integer atomics' rate on gfx950: scripts/probes/lds_rmw_probe.hip; they
+// are what made round 3's dense variant lose.)
+template <typename T = float>
+__global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
+    const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
+    const int2* __restrict__ glist, GPack gp, int F, const T* __restrict__ mask, int64_t ldm,
+    T* __restrict__ dx, int64_t ldx, float* __restrict__ ws, int64_t ldw) {
+  constexpr int U = PG_PULL_U;
+  __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
+  __shared__ int marks[kWavesPerBlock][U * kWave];
   const int wave = wave_id_uniform();
-  const int lane = lane_id();
-  const int W = (int)gridDim.x * kWavesPerBlock;
+  const int it = blockIdx.x * kWavesPerBlock + wave;
+  if (it >= n_items) return;
   float* acc = accs[wave];
-  const bool vec = (F & 3) == 0;
-  for (int base = (int)blockIdx.x * kWavesPerBlock + wave; base < n_items; base += kWave * W) {
-    const int my = base + lane * W;
-    int4 mi = make_int4(0, 0, 0, -1);
-    if (my < n_items) mi = items[my];
-    int me0 = 0, me1 = 0;
-    if (mi.z > mi.y) {  // an item with no out-edges reads nothing (off_t may hold no entry)
-      me0 = off_t[mi.y];
-      me1 = off_t[mi.z];
+  int* mark = marks[wave];
+  const int4 item = items[it];
+  const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
+  const int lane = lane_id();
+  for (int f = lane; f < F; f += kWave) acc[f] = 0.f;
+  // descriptors one window ahead, their in-CSR slots two windows ahead (an item with no
+  // out-edges reads nothing)
+  auto tl_of = [&](int tw) { return tw + min(lane, t1 - tw - 1); };
+  int2 dsc_next = make_int2(0, 0);
+  int ts_next = 0;
+  if (t1 > t0) {
+    dsc_next = glist[tslot[tl_of(t0)]];
+    if (t0 + kWave < t1) ts_next = tslot[tl_of(t0 + kWave)];
+  }
+  for (int tw = t0; tw < t1; tw += kWave) {
+    const int nw = min(kWave, t1 - tw);
+    const int2 dsc = dsc_next;
+    if (tw + kWave < t1) {
+      dsc_next = glist[ts_next];
+      if (tw + 2 * kWave < t1) ts_next = tslot[tl_of(tw + 2 * kWave)];
     }
-    const int nb = min(kWave, (n_items - base + W - 1) / W);
-    for (int j = 0; j < nb; ++j) {
-      const int row = bcast(mi.x, j), slot = bcast(mi.w, j);
-      const int e0 = bcast(me0, j), e1 = bcast(me1, j);
-      if (vec) {
-        for (int f = lane * 4; f < F; f += 4 * kWave) *reinterpret_cast<float4*>(acc + f) = make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        for (int f = lane; f < F; f += kWave) acc[f] = 0.f;
-      }
-      wave_lds_sync();
-      for (int e = e0; e < e1; e += U * kWave) {
-        int fe[U];
-        float de[U];
-        // straight-line loads (lanes past the run load its last record), masked at the add
+    const int cnt = lane < nw ? dsc.y : 0;
+    const int incl = wave_incl_add(cnt);
+    const int excl = incl - cnt;
+    const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+    int carry = -1;
+    for (int b = 0; b < total; b += U * kWave) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-#if PG_STREAM_PROBE == 2
-          fe[u] = (lane * 4 + u) & 255; de[u] = 1.f;
+      for (int u = 0; u < U; ++u) mark[u * kWave + lane] = -1;
+      wave_lds_sync();
+      if (cnt > 0 && excl >= b && excl < b + U * kWave) mark[excl - b] = lane;
+      wave_lds_sync();
+      int fe[U];
+      float de[U];
+      bool in[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = b + u * kWave + lane;
+        in[u] = e < total;
+        int m = max(wave_incl_max(mark[u * kWave + lane]), carry);
+        carry = __builtin_amdgcn_readlane(m, kWave - 1);
+        const int ec = min(e, total - 1);  // lanes past the end load a valid entry, unused
+        m = in[u] ? m : carry;
+        const int off = __builtin_amdgcn_ds_bpermute(m << 2, dsc.x);
+        const int ex = __builtin_amdgcn_ds_bpermute(m << 2, excl);
+#if PG_PULL_PROBE == 2
+        fe[u] = (lane * 4 + u + (off - ex + ec) * 0) & 255;
+        de[u] = 1.f;
 #else
-          recs.get(min(e + u * kWave + lane, e1 - 1), fe[u], de[u]);
+        gp.get(off + (ec - ex), fe[u], de[u]);
 #endif
-        }
+      }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          bool pend = e + u * kWave + lane < e1;
-          unsigned* w = reinterpret_cast<unsigned*>(acc + (pend ? fe[u] : kGroupMaxF + lane));
-          float cur = *reinterpret_cast<const float*>(w);
-          // in-order add: same-word lanes retry on the earlier lane's sum (see the header)
-          while (__ballot(pend)) {
-            if (pend) {
-              const unsigned want = __float_as_uint(cur);
-              const unsigned got = atomicCAS(w, want, __float_as_uint(cur + de[u]));
-              pend = got != want;
-              cur = __uint_as_float(got);
-            }
+      for (int u = 0; u < U; ++u) {
+        bool pend = in[u];
+        unsigned* w = reinterpret_cast<unsigned*>(acc + fe[u]);
+#if PG_PULL_PROBE == 1
+        if (pend) *reinterpret_cast<float*>(w) += de[u];
+        pend = false;
+#endif
+        float cur = pend ? *reinterpret_cast<const float*>(w) : 0.f;
+        while (__ballot(pend)) {
+          if (pend) {
+            const unsigned want = __float_as_uint(cur);
+            const unsigned got = atomicCAS(w, want, __float_as_uint(cur + de[u]));
+            pend = got != want;
+            cur = __uint_as_float(got);
           }
         }
       }
-      wave_lds_sync();
-#if PG_STREAM_PROBE == 3
-      if (acc[lane] != 12345.f) continue;
-#endif
-      if (slot < 0) {
-        T* xr = dx + (int64_t)row * ldx;
-        const T* mr = mask ? mask + (int64_t)row * ldm : nullptr;
-        if (vec) {
-          for (int f = lane * 4; f < F; f += 4 * kWave) {
-            const float4 t = *reinterpret_cast<const float4*>(acc + f);
-            float a[4] = {t.x, t.y, t.z, t.w};
-            if (mr) {
-              float mk[4];
-              load_tile<4, T>(mr, f, F, mk, 0.f);
-#pragma unroll
-              for (int i = 0; i < 4; ++i)
-                if (!(mk[i] > 0.f)) a[i] = 0.f;
-            }
-            store_tile<4, T>(xr, f, F, a);
-          }
-        } else {
-          for (int f = lane; f < F; f += kWave) {
-            float a = acc[f];
-            if (mr && !(to_f(mr[f]) > 0.f)) a = 0.f;
-            xr[f] = from_f<T>(a);
-          }
-        }
-      } else {
-        float* wr = ws + (int64_t)slot * ldw;
-        for (int f = lane; f < F; f += kWave) wr[f] = acc[f];
-      }
-      wave_lds_sync();
     }
+  }
+  wave_lds_sync();
+  if (slot < 0) {
+    T* xr = dx + (int64_t)row * ldx;
+    const T* mr = mask ? mask + (int64_t)row * ldm : nullptr;
+    for (int f = lane; f < F; f += kWave) {
+      float a = acc[f];
+      if (mr && !(to_f(mr[f]) > 0.f)) a = 0.f;
+      xr[f] = from_f<T>(a);
+    }
+  } else {
+    float* wr = ws + (int64_t)slot * ldw;
+    for (int f = lane; f < F; f += kWave) wr[f] = acc[f];
   }
 }
 
@@ -1075,18 +1161,6 @@ inline int hip_status(const char* who) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pg::set_error((int)e, "%s: launch failed: %s", who, hipGetErrorString(e));
   return pg::ok();
-}
-
-// workgroups that fit the device at once, `per_cu` to a CU (persistent kernels)
-inline int resident_blocks(int per_cu) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    cus = n;
-  }
-  return cus * per_cu;
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -1315,21 +1389,17 @@ int pg_spmm_max_fwd_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t 
                                  arg_kind, ws, ws_bytes, stream);
 }
 
-// [split-row partials][source-ordered path: cnt nnz | off_t nnz + 1 |
-//  look-back words ntiles + 1 (u64) | records N x F]
+// [split-row partials][grouped path: list records N x F x 8 B | glist nnz x int2]
 static size_t bwd_partials_bytes(const pg_csr_t* gt, int64_t F) {
   return gt->n_slots > 0 ? round_up(gt->n_slots * ws_ld(F) * 4, 256) : 0;
 }
-static int64_t bwd_scan_tiles(int64_t nnz) { return (nnz + kScanTile - 1) / kScanTile; }
-static size_t bwd_rec_bytes(int64_t n) { return round_up(n * BRecs::kBytes, 256); }
 
 size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
   if (!gt || F <= 0) return 0;
   size_t b = bwd_partials_bytes(gt, F);
   if (F <= kGroupMaxF) {
-    const int64_t N = gt->n_cols, E = gt->nnz;
-    b += round_up(E * 4, 256) + round_up((E + 1) * 4, 256) +
-         round_up((bwd_scan_tiles(E) + 1) * 8, 256) + bwd_rec_bytes(N * F);
+    const int64_t N = gt->n_cols;
+    b += round_up(N * F * 8, 256) + round_up(gt->nnz * 8, 256);
   }
   return b;
 }
@@ -1369,74 +1439,46 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
   const int64_t N = g->n_rows;
   // PG_BWD_DIRECT (variant builds): always the argmax-record gather over the transposed CSR
   if (arg_kind == PG_ARG_U16 && F <= kGroupMaxF && N * F < INT32_MAX && !PG_BWD_DIRECT) {
-    if (g->nnz > 0 && !g->einv)
-      return pg::set_error(PG_ERR_INVALID, "pg_spmm_max_bwd: g needs einv (in-CSR slot -> transposed index)");
     char* p = (char*)ws + pbytes;
-    const int64_t E = g->nnz;
-    const int ntiles = (int)bwd_scan_tiles(E);
-    int32_t* cnt = (int32_t*)p;
-    p += round_up(E * 4, 256);
-    int32_t* off_t = (int32_t*)p;
-    p += round_up((E + 1) * 4, 256);
-    auto* lb = (unsigned long long*)p;
-    p += round_up((ntiles + 1) * 8, 256);
-    // records: {f32 value, feature} (8 B); bf16 storage without edge weights: the bf16
-    // upstream gradient itself, {bf16 value, u16 feature} (4 B). The sums are f32 either way
-    // (one rounding of dx at the end, as the oracle's f32 sums).
-    auto run = [&](auto recs) {
-      using R = decltype(recs);
-      const auto* arg16 = (const uint16_t*)argpos;
-      // rows past kPackWaveMax: the schedule's split rows when its chunk guarantees they are
-      // a superset, else every row
-      const bool listed = g->merges != nullptr && g->chunk > 0 && g->chunk <= kPackWaveMax;
-      const int n_long = (int)(listed ? g->n_merges : N);
-      const int n_short_blocks = (int)((N + kWavesPerBlock - 1) / kWavesPerBlock);
-      // 4 features per lane (vector loads) when every row is 4-aligned
-      constexpr uintptr_t kTa = 4 * sizeof(T) - 1;
-      const bool vec = F % 4 == 0 && lda % 4 == 0 && ldd % 4 == 0 && (!fwd_out || ldf % 4 == 0) &&
-                       ((uintptr_t)argpos & 7) == 0 && ((uintptr_t)dout & kTa) == 0 && ((uintptr_t)fwd_out & kTa) == 0;
-      const dim3 pgrid((unsigned)(n_long + std::min<int64_t>(n_short_blocks, resident_blocks(8))));
-      const int4* prow = listed ? (const int4*)g->merges : nullptr;
-      if (E > 0) {
-        auto rows = [&](auto nv_c, auto place_c) {
-          constexpr int NV = decltype(nv_c)::value;
-          constexpr bool PL = decltype(place_c)::value;
-          hipLaunchKernelGGL((bwd_rows_kernel<NV, PL, uint16_t, T, R>), pgrid, dim3(kBlock), 0, st, prow, n_long,
-                             (int)N, g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, g->ew,
-                             cnt, g->einv, off_t, recs, lb, PL ? 0 : ntiles + 1);
-          return PG_OK;
-        };
-        auto pass = [&](auto place_c) {
-          if (vec) dispatch_nc_vec((int)((F + 255) / 256), [&](auto n) { return rows(n, place_c); });
-          else rows(std::integral_constant<int, 0>{}, place_c);
-        };
-        pass(std::false_type{});
-        hipLaunchKernelGGL(bwd_scan_kernel, dim3((unsigned)ntiles), dim3(kBlock), 0, st, gt->eslot, (int)E, cnt,
-                           off_t, lb, ntiles);
-        pass(std::true_type{});
-      }
-      // dead-none records imply the relu' mask (the contract: mask_src >= 0): every entry
-      // left has a maximum X[u,f] w != 0, so X[u,f] > 0; an element no entry reaches sums to
-      // +0, which the mask would leave +0. With fwd_out alone the mask is applied.
-      const T* mk = dead_none ? nullptr : mask_src;
-      const int sblocks = (int)std::min<int64_t>(grid_for(gt->n_items), (int64_t)resident_blocks(8));
-      hipLaunchKernelGGL((bwd_stream_kernel<T, R>), dim3(sblocks), dim3(kBlock), 0, st,
-                         (const int4*)gt->items, (int)gt->n_items, off_t, recs, (int)F, mk, ldm, dx,
-                         ldx, w, ws_ld(F));
-      if (gt->n_merges > 0)
-        hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
-                           (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
-                           mk, ldm, dx, ldx);
+    // the records carry the upstream gradient as f32 even for bf16 storage (one rounding of
+    // dx at the end, as the oracle's f32 sums)
+    GPack gp;
+    gp.r = (uint2*)p;
+    p += round_up(N * F * 8, 256);
+    int2* glist = (int2*)p;
+    p += round_up(g->nnz * 8, 256);
+    const auto* arg16 = (const uint16_t*)argpos;
+    // rows past kPackWaveMax: the schedule's split rows when its chunk guarantees they are
+    // a superset, else every row
+    const bool listed = g->merges != nullptr && g->chunk > 0 && g->chunk <= kPackWaveMax;
+    const int n_long = (int)(listed ? g->n_merges : N);
+    const int n_short_blocks = (int)((N + kWavesPerBlock - 1) / kWavesPerBlock);
+    // 4 features per lane (vector loads) when every row is 4-aligned
+    constexpr uintptr_t kTa = 4 * sizeof(T) - 1;
+    const bool vec = F % 4 == 0 && lda % 4 == 0 && ldd % 4 == 0 && (!fwd_out || ldf % 4 == 0) &&
+                     ((uintptr_t)argpos & 7) == 0 && ((uintptr_t)dout & kTa) == 0 && ((uintptr_t)fwd_out & kTa) == 0;
+    const dim3 pgrid((unsigned)(n_long + n_short_blocks));
+    const int4* prow = listed ? (const int4*)g->merges : nullptr;
+    auto pack = [&](auto nv_c) {
+      constexpr int NV = decltype(nv_c)::value;
+      hipLaunchKernelGGL((group_pack_kernel<uint16_t, T, NV>), pgrid, dim3(kBlock), 0, st, prow, n_long, (int)N,
+                         g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, g->ew, gp, glist);
+      return PG_OK;
     };
-    if (sizeof(T) == 2 && !g->ew) {
-      BRecs4 r4;
-      r4.r = (uint32_t*)p;
-      run(r4);
-    } else {
-      BRecs r8;
-      r8.r = (uint2*)p;
-      run(r8);
-    }
+    if (vec) dispatch_nc_vec((int)((F + 255) / 256), pack);
+    else pack(std::integral_constant<int, 0>{});
+    const int blocks = grid_for(gt->n_items);
+    // dead-none records imply the relu' mask (the contract: mask_src >= 0): every entry left
+    // in the lists has a maximum X[u,f] w != 0, so X[u,f] > 0; an element with no entries
+    // sums to +0, which the mask would leave +0. With fwd_out alone the mask is applied.
+    if (dead_none) mask_src = nullptr;
+    hipLaunchKernelGGL((max_bwd_pull_kernel<T>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
+                       (const int4*)gt->items, (int)gt->n_items, glist, gp, (int)F, mask_src, ldm, dx, ldx,
+                       w, ws_ld(F));
+    if (gt->n_merges > 0)
+      hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
+                         (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
+                         mask_src, ldm, dx, ldx);
     return hip_status("pg_spmm_max_bwd");
   }
   if constexpr (sizeof(T) == 4) {

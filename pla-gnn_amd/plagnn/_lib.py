@@ -44,7 +44,6 @@ class PgCsr(ctypes.Structure):
         ("n_slots", ctypes.c_int64),
         ("max_deg", ctypes.c_int32),
         ("chunk", ctypes.c_int32),
-        ("einv", ctypes.c_void_p),
     ]
 
 

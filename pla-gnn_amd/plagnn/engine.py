@@ -214,7 +214,7 @@ class TrainEngine:
         for l in range(self.L):
             Fi = pd[l]
             need = max(need, L.pg_spmm_max_fwd_workspace(self.dg.fwd.struct(self.ews), Fi, self.dg.arg_kind))
-            need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd_stream.struct(None), Fi))
+            need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd.struct(None), Fi))
         self._gemm_plans = {}
         # weight gradients' split-K combines deferred to one batched launch per step
         self._slabs: Dict[str, torch.Tensor] = {}
@@ -505,7 +505,7 @@ class TrainEngine:
         st = self._s()
         G, P, pd = self.G, self.P, self.pd
         g = self.dg.fwd.struct(self.ews)
-        gt = self.dg.bwd_stream.struct(None)
+        gt = self.dg.bwd.struct(None)
         # liner2: dW2 = dZ^T A4 (+ db2 = row sums of dZ^T); dA4 came from the fused head
         self._gemm(self.dZ, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
         # liner1

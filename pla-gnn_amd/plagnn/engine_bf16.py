@@ -122,7 +122,7 @@ class TrainEngineBF16(TrainEngine):
         for l in range(self.L):
             Fi = pd[l]
             need = max(need, L.pg_spmm_max_fwd_workspace(self.dg.fwd.struct(self.ews), Fi, self.dg.arg_kind))
-            need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd_stream.struct(None), Fi))
+            need = max(need, L.pg_spmm_max_bwd_workspace(self.dg.bwd.struct(None), Fi))
         self._gemm_plans = {}
         for (M_, N_, K_) in self._wgrad_shapes():
             sk = int(L.pg_gemm_bf16_split_k(M_, N_, K_))
@@ -176,7 +176,7 @@ class TrainEngineBF16(TrainEngine):
         st = self._s()
         G, P, W, pd = self.G, self.P, self.Wb, self.pd
         g = self.dg.fwd.struct(self.ews)
-        gt = self.dg.bwd_stream.struct(None)
+        gt = self.dg.bwd.struct(None)
         # liner2 / liner1 (weights W[out][in] as k images for the input gradients)
         self._gemm(self.dZb, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
         self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")

@@ -24,21 +24,16 @@ from ._lib import PgCsr, call
 # in-CSR entries per forward work item before a row is split (CSRGraph(chunk=...))
 DEFAULT_CHUNK = 256
 # out-CSR entries per backward work item, its work is data-dependent (CSRGraph(chunk_bwd=...);
-# None = by graph size). Measured whole steps: S0 (24 041 nodes) 64-96 best (1.97 ms), 128
-# 1.99, 32 2.01, 256 2.11 (round 2); again in round 3 with the cheaper pull: the cfg2
-# step's backward 0.259 ms at 64 vs 0.285 at 128, although the isolated kernel on random
-# relu inputs (scripts/bwd_chunk_sweep.py) prefers 128. RMAT x16 (384 656 nodes): 128
-# 24.3 ms per step vs 64 25.2 ms: finer items pay off only while the graph alone does not
-# fill the chip.
+# None = by graph size). Measured with the dense pull (scripts/bwd_bench.py, per call): S0
+# (24 041 nodes) F = 256: 68.0 / 66.0 / 72.1 / 101.6 us at 64 / 128 / 256 / 512 (hub
+# sources serialise on one wave past 128); RMAT x16 (384 656 nodes) F = 512 bf16: 1504 /
+# 1375 / 1308 / 1275 us: finer items pay off only while the graph alone does not fill the
+# chip.
 DEFAULT_CHUNK_BWD = None
-# out-CSR entries per item of the max backward's stream pass (pg_spmm_max_bwd's gt): it
-# streams each source's records at full rate, so only rows this long are split (their
-# partial rows merged in order by sum_merge)
-DEFAULT_CHUNK_STREAM = 4096
 
 
 def default_chunk_bwd(num_nodes: int) -> int:
-    return 64 if num_nodes <= 65536 else 128
+    return 128 if num_nodes <= 65536 else 512
 
 
 def _np_ptr(a: np.ndarray) -> int:
@@ -62,8 +57,8 @@ def _schedule(ptr: np.ndarray, chunk: int):
 class HostCsr:
     """One CSR direction with its schedule, in host memory (numpy int32)."""
 
-    def __init__(self, ptr, col, eslot, n_cols: int, chunk: int, epos=None, einv=None):
-        self.ptr, self.col, self.eslot, self.epos, self.einv = ptr, col, eslot, epos, einv
+    def __init__(self, ptr, col, eslot, n_cols: int, chunk: int, epos=None):
+        self.ptr, self.col, self.eslot, self.epos = ptr, col, eslot, epos
         self.n_rows = len(ptr) - 1
         self.n_cols = int(n_cols)
         self.nnz = int(len(col))
@@ -71,30 +66,17 @@ class HostCsr:
         (self.items, self.n_items, self.merges, self.n_merges, self.n_slots,
          self.max_deg) = _schedule(ptr, chunk)
 
-    def rescheduled(self, chunk: int) -> "HostCsr":
-        """The same arrays with a schedule split at `chunk` entries."""
-        return HostCsr(self.ptr, self.col, self.eslot, self.n_cols, chunk, epos=self.epos, einv=self.einv)
-
 
 class DeviceCsr:
     """A HostCsr uploaded to one device; ``struct()`` gives the pg_csr_t view."""
 
-    def __init__(self, h: HostCsr, device: torch.device, share: Optional["DeviceCsr"] = None):
-        """`share`: a DeviceCsr of the same arrays (another schedule): its tensors are reused."""
+    def __init__(self, h: HostCsr, device: torch.device):
         def up(a):
-            if a is None:
-                return None
-            if share is not None:
-                for ha, da in share._host_dev:
-                    if ha is a:
-                        return da
-            return torch.from_numpy(a).to(device)
+            return None if a is None else torch.from_numpy(a).to(device)
 
         self.device = device
         self.ptr, self.col, self.eslot, self.epos = up(h.ptr), up(h.col), up(h.eslot), up(h.epos)
-        self.einv = up(h.einv)
-        self._host_dev = [(h.ptr, self.ptr), (h.col, self.col), (h.eslot, self.eslot), (h.epos, self.epos),
-                          (h.einv, self.einv)]
+
         self.items, self.merges = up(h.items), up(h.merges)
         self.n_rows, self.n_cols, self.nnz = h.n_rows, h.n_cols, h.nnz
         self.n_items, self.n_merges, self.n_slots = h.n_items, h.n_merges, h.n_slots
@@ -124,7 +106,6 @@ class DeviceCsr:
         s.n_slots = self.n_slots
         s.max_deg = self.max_deg
         s.chunk = self.chunk
-        s.einv = _lib.ptr(self.einv)
         return s
 
 
@@ -132,7 +113,7 @@ class CSRGraph:
     """In-CSR + out-CSR of a directed graph given as COO (src -> dst), host resident."""
 
     def __init__(self, src, dst, num_nodes: int, chunk: int = DEFAULT_CHUNK,
-                 chunk_bwd: Optional[int] = DEFAULT_CHUNK_BWD, chunk_stream: int = DEFAULT_CHUNK_STREAM):
+                 chunk_bwd: Optional[int] = DEFAULT_CHUNK_BWD):
         src = np.ascontiguousarray(np.asarray(src, dtype=np.int64))
         dst = np.ascontiguousarray(np.asarray(dst, dtype=np.int64))
         if src.shape != dst.shape or src.ndim != 1:
@@ -154,16 +135,10 @@ class CSRGraph:
         self.num_nodes = n
         self.num_edges = E
         self.eid = eid  # in-CSR slot -> edge id
-        # in-CSR slot -> transposed index (the max backward's place pass finds each edge's
-        # list offset through it)
-        einv = np.empty(E, np.int32)
-        einv[tslot[:E]] = np.arange(E, dtype=np.int32)
-        self.fwd = HostCsr(ptr, col, None, n, chunk, einv=einv)
+        self.fwd = HostCsr(ptr, col, None, n, chunk)
         if chunk_bwd is None:
             chunk_bwd = default_chunk_bwd(n)
-        self.bwd = HostCsr(tptr, tcol[:E], tslot[:E], n, min(chunk, chunk_bwd), epos=tpos[:E])
-        # the max backward's transposed schedule (its stream pass)
-        self.bwd_stream = self.bwd.rescheduled(chunk_stream)
+        self.bwd = HostCsr(tptr, tcol[:E], tslot[:E], n, chunk_bwd, epos=tpos[:E])
         # argmax records hold positions inside in-CSR rows: u16 while every row is shorter
         # than 0xFFFF entries (0xFFFF = no winner)
         self.arg_kind = _lib.PG_ARG_U16 if self.fwd.max_deg < 0xFFFF else _lib.PG_ARG_I32
@@ -194,7 +169,6 @@ class DeviceGraph:
         self.arg_dtype = torch.int16 if g.arg_kind == _lib.PG_ARG_U16 else torch.int32
         self.fwd = DeviceCsr(g.fwd, device)
         self.bwd = DeviceCsr(g.bwd, device)
-        self.bwd_stream = DeviceCsr(g.bwd_stream, device, share=self.bwd)
         self.eid = torch.from_numpy(g.eid.astype(np.int64)).to(device)
 
     @property

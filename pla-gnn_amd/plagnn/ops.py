@@ -115,7 +115,7 @@ def spmm_max_backward(dg: DeviceGraph, argpos: torch.Tensor, dout: torch.Tensor,
     if dx is None:
         dx = torch.empty(n, F, dtype=dout.dtype, device=dout.device)
     g = dg.fwd.struct(ew_slots)
-    gt = (dg.bwd_stream if dg.is_cuda else dg.bwd).struct(None)
+    gt = dg.bwd.struct(None)
     ldm = _ld(mask) if mask is not None else 0
     if dg.is_cuda:
         ws_n = _lib.lib().pg_spmm_max_bwd_workspace(gt, F)

@@ -1,8 +1,7 @@
 """Max-backward micro-benchmark (the engine's call: dead-none records, implied relu' mask):
 S0 at F = 256 / 512 (f32) and RMAT x16 at F = 512 (bf16), HIP-event timed per call, with
 the algorithmic bytes of SURVEY.md §8d (4(N+1) + 8E' + (2+4+4+4) F N for f32). Run under
-`rocprofv3 --kernel-trace --stats` for the per-pass split (count, scan, place, stream,
-merge).  python scripts/bwd_bench.py [s0|rmat|all] [reps] [stream chunks, comma list]"""
+`rocprofv3 --kernel-trace --stats` for the per-pass split (pack, pull, merge).  python scripts/bwd_bench.py [s0|rmat|all] [reps] [backward chunks, comma list]"""
 import os
 import sys
 
@@ -27,14 +26,14 @@ def timeit(fn, reps):
     return a.elapsed_time(b) / reps
 
 
-def run(kind, widths, bf16, reps, chunk_stream):
+def run(kind, widths, bf16, reps, chunk_bwd):
     ds = data.make_dataset(kind)
     src, dst = ds.edges_with_self_loops()
-    g = plagnn.CSRGraph(src, dst, ds.n, chunk_stream=chunk_stream)
+    g = plagnn.CSRGraph(src, dst, ds.n, chunk_bwd=chunk_bwd)
     dg = g.on("cuda")
     N, E = ds.n, g.num_edges
     print(f"graph {kind}: N={N} E'={E} max_in={g.fwd.max_deg} max_out={g.bwd.max_deg} "
-          f"stream items={g.bwd_stream.n_items} split={g.bwd_stream.n_merges} (chunk {chunk_stream})", flush=True)
+          f"bwd items={g.bwd.n_items} split={g.bwd.n_merges} (chunk {chunk_bwd})", flush=True)
     gen = torch.Generator(device="cuda").manual_seed(1)
     for F in widths:
         dt = torch.bfloat16 if bf16 else torch.float32
@@ -43,7 +42,7 @@ def run(kind, widths, bf16, reps, chunk_stream):
         _, arg = ops.spmm_max(dg, P, dead_none=True)
         dZ = torch.randn(N, F, device="cuda", generator=gen).to(dt)
         dX = torch.empty_like(P)
-        gs, gts = dg.fwd.struct(None), dg.bwd_stream.struct(None)
+        gs, gts = dg.fwd.struct(None), dg.bwd.struct(None)
         ws = torch.empty(plagnn.lib().pg_spmm_max_bwd_workspace(gts, F), dtype=torch.uint8, device="cuda")
         fn = "pg_spmm_max_bwd_bf16" if bf16 else "pg_spmm_max_bwd"
         kind_flag = dg.arg_kind | plagnn._lib.PG_ARG_DEAD_NONE
@@ -65,7 +64,7 @@ def run(kind, widths, bf16, reps, chunk_stream):
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    chunks = [int(c) for c in (sys.argv[3] if len(sys.argv) > 3 else "4096").split(",")]
+    chunks = [int(c) for c in (sys.argv[3] if len(sys.argv) > 3 else "128").split(",")]
     for c in chunks:
         if which in ("s0", "all"):
             run("s0", (256, 512), False, reps, c)

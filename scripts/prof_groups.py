@@ -3,7 +3,7 @@ bench.py's roofline against the profiler. Groups (the engine's l
 groups, bench.py / TrainEngine.group_times):
   gemm          gemm_x3_kernel, gemm_dma_kernel, gemm_*_kernel, splitk_reduce*, gemm_bf16*
   spmm_max_fwd  max_fwd_kernel, max_merge_kernel
-  spmm_max_bwd  bwd_rows_kernel (count, place), bwd_scan_kernel, bwd_stream_kernel, sum_merge_kernel
+  spmm_max_bwd  group_pack_kernel, max_bwd_pull_kernel, sum_merge_kernel
   head          head_kernel, head_final_kernel;   adam  adam_*, cast_*
 Usage: python scripts/prof_groups.py <rocprof -d dir> [--bench bench.json] [--json out.json]
 The process whose pid bench.json names (its "pid") is the headline; the others are the
@@ -16,7 +16,7 @@ import os
 import re
 
 RULES = [("gemm", r"gemm_|splitk_reduce"), ("spmm_max_fwd", r"max_fwd_kernel|max_merge_kernel"),
-         ("spmm_max_bwd", r"bwd_rows_kernel|bwd_scan_kernel|bwd_stream_kernel|sum_merge_kernel"),
+         ("spmm_max_bwd", r"group_pack_kernel|max_bwd_pull_kernel|sum_merge_kernel"),
          ("head", r"head_kernel|head_final_kernel"), ("adam", r"adam_|cast_f32_bf16")]
 
 

@@ -42,11 +42,11 @@ def main():
         tf = timeit(lambda: ops.spmm_max(dg, P, out=out, argpos=arg))
         dZ = torch.randn(N, F, device="cuda")
         dX = torch.empty_like(P)
-        ws = torch.empty(plagnn.lib().pg_spmm_max_bwd_workspace(dg.bwd_stream.struct(None), F),
+        ws = torch.empty(plagnn.lib().pg_spmm_max_bwd_workspace(dg.bwd.struct(None), F),
                          dtype=torch.uint8, device="cuda")
 
         def bwd():
-            plagnn._lib.call("pg_spmm_max_bwd", dg.fwd.struct(None), dg.bwd_stream.struct(None), arg.data_ptr(), F,
+            plagnn._lib.call("pg_spmm_max_bwd", dg.fwd.struct(None), dg.bwd.struct(None), arg.data_ptr(), F,
                              dg.arg_kind, dZ.data_ptr(), F, F, P.data_ptr(), F,
                              out.data_ptr() if skip_zero else None, F, dX.data_ptr(), F,
                              ws.data_ptr(), ws.numel(), plagnn._lib.stream_handle(P.device))

@@ -87,8 +87,6 @@ static void run_case(int64_t n, int64_t e, int64_t hub, int64_t F, int chunk, bo
   std::vector<int32_t> tptr(n + 1), tcol(E), tslot(E), tpos(E);
   CHECK(pg_csr_transpose(ptr.data(), col.data(), n, n, E, tptr.data(), tcol.data(), tslot.data(), tpos.data()) == 0,
         "transpose");
-  std::vector<int32_t> einv(E);
-  for (int64_t t = 0; t < E; ++t) einv[tslot[t]] = (int32_t)t;
   auto sched = [&](const std::vector<int32_t>& p, std::vector<int32_t>& items, std::vector<int32_t>& merges,
                    int64_t& ni, int64_t& nm, int64_t& ns, int32_t& md) {
     CHECK(pg_schedule_count(p.data(), n, chunk, &ni, &nm, &ns, &md) == 0, "schedule count");
@@ -110,9 +108,9 @@ static void run_case(int64_t n, int64_t e, int64_t hub, int64_t F, int chunk, bo
   for (int64_t k = 0; k < E; ++k) w_eid[k] = ud(rng);
   for (int64_t k = 0; k < E; ++k) w_slot[k] = w_eid[eid[k]];
   pg_csr_t fwd{n, n, E, ptr.data(), col.data(), nullptr, nullptr, weighted ? w_slot.data() : nullptr,
-               fi.data(), fni, fnm ? fm.data() : nullptr, fnm, fns, fmd, chunk, einv.data()};
+               fi.data(), fni, fnm ? fm.data() : nullptr, fnm, fns, fmd, chunk};
   pg_csr_t bwd{n, n, E, tptr.data(), tcol.data(), tslot.data(), tpos.data(), nullptr,
-               bi.data(), bni, bnm ? bm.data() : nullptr, bnm, bns, bmd, chunk, nullptr};
+               bi.data(), bni, bnm ? bm.data() : nullptr, bnm, bns, bmd, chunk};
   std::vector<float> out(n * F), dx(n * F), sum(n * F);
   std::vector<int32_t> arg(n * F);
   std::vector<int64_t> argx(n * F), argx_o(n * F), arge_o(n * F);

@@ -92,7 +92,7 @@ def test_spmm_max_bwd(oracle_mod, F, weighted):
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
     dX_ref = oracle_mod.spmm_max_bwd(og, argx, arge, dZ, use_weight=weighted)
     dX = ops.spmm_max_backward(dg, argpos, torch.from_numpy(dZ).to(DEV), ews).cpu().numpy()
-    split_rows = set(g.bwd_stream.merges.reshape(-1, 4)[: g.bwd_stream.n_merges, 0].tolist())
+    split_rows = set(g.bwd.merges.reshape(-1, 4)[: g.bwd.n_merges, 0].tolist())
     exact = np.array([u not in split_rows for u in range(n)])
     np.testing.assert_array_equal(dX[exact], dX_ref[exact])
     # split rows: a different summation grouping, bounded by the error scale sum |terms|
@@ -203,7 +203,7 @@ def test_spmm_max_bwd_hub_past_lds_histogram(oracle_mod, F):
     Xd = torch.from_numpy(X).to(DEV)
     _, argx, arge = oracle_mod.spmm_max(og, X)
     dX_ref = oracle_mod.spmm_max_bwd(og, argx, arge, dZ)
-    split_rows = set(g.bwd_stream.merges.reshape(-1, 4)[: g.bwd_stream.n_merges, 0].tolist())
+    split_rows = set(g.bwd.merges.reshape(-1, 4)[: g.bwd.n_merges, 0].tolist())
     exact = np.array([u not in split_rows for u in range(n)])
     mag = np.abs(oracle_mod.spmm_max_bwd(og, argx, arge, np.abs(dZ)))
     for dead in (False, True):
