@@ -404,42 +404,55 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
 }
 
 // ---- max backward, grouped form (default for u16 records and F <= 1024) ---------------
-// Pass 1 (pack), per destination row v: group v's features by their winning in-row
-// position p, giving
-//   gfeat[v F + i]  the features, grouped by p (any order inside a group),
-//   dpack[v F + i]  = dout[v][gfeat[v F + i]]   (the upstream gradient in list order),
+// Pass 1 (pack), per destination row v: group v's live entries (v, f) by their winning
+// in-row position p, giving
+//   rec[v F + i]    = {w * dout[v,f], f}, grouped by p (any order inside a group; 8-B
+//                     records, or 4-B {bf16 dout, f} for bf16 storage without weights),
 //   glist[s]        = {v F + start_p, count_p} for the edge at in-CSR slot s = ptr[v] + p
 //                     (a row's descriptors are contiguous: coalesced stores).
 // Rows of in-degree <= kPackWaveMax: one wave per row (wave-private LDS histogram, wave
 // scan, LDS-atomic placement); longer rows: one workgroup per row (block histogram, or a
 // bitonic sort of (p << 16 | f) keys past kHistMax entries).
-// Pass 2 (pull), one wave per source row u: for each out-edge of u, ascending destination
-// v (the transposed CSR order), read its descriptor glist[tslot[t]] (the transposed
-// entry's in-CSR slot; loaded a window ahead) and add dpack[list] (* w) into an LDS row accumulator at gfeat[list]. A list never
-// repeats a feature, so one instruction's lanes hit distinct LDS words and every
-// feature's terms are summed in ascending v, the order of the sequential scatter_add_:
-// the order inside a list does not matter. Traffic per edge: its 4-B slot, one 8-B
-// descriptor and two short contiguous runs (~F/deg entries). (Descriptors stored at the
-// transposed index instead, read coalesced but written scattered by the pack: the cfg2
-// backward 259 vs 256 us per step.)
+// Pass 2 (pull), one wave per source row item: for each out-edge of u, ascending
+// destination v (the transposed CSR order), read its descriptor glist[tslot[t]] and add
+// its records into an LDS row accumulator (max_bwd_pull_kernel). Traffic per edge: its
+// 4-B slot, one 8-B descriptor and one short contiguous run of records (~F/deg entries).
+// (Descriptors stored at the transposed index instead, read coalesced but written
+// scattered by the pack: pull 35.6 vs 43.5 us, pack 28.3 vs 15.9 us at F = 256, no gain.
+// A source-ordered record layout, DESIGN.md §7, measured slower still.)
 constexpr int kHistMax = 4096;
 constexpr int kGroupMaxF = 1024;
 #ifndef PG_BWD_DIRECT
 #define PG_BWD_DIRECT 0
 #endif
 
-// one 8-B record {value f32, feature u32} per list entry (one contiguous run per list:
-// one line for the pull to fetch where two arrays cost two); the value carries the edge
-// weight already (w * dout[v,f], the product the pull formed before)
+// one record per list entry, one contiguous run per list (one line for the pull to fetch
+// where two arrays cost two). GPack: {value f32, feature u32} (8 B); the value carries the
+// edge weight already (w * dout[v,f], the product the pull formed before). GPack4 (bf16
+// storage without edge weights): the bf16 upstream gradient itself and the feature,
+// {value bf16, feature u16} (4 B); exact, since the value is a bf16 number.
 struct GPack {
-  uint2* __restrict__ r;
-  __device__ __forceinline__ void put(int64_t pos, int f, float d) const {
-    r[pos] = make_uint2(__float_as_uint(d), (uint32_t)f);
-  }
+  using W = uint2;
+  W* __restrict__ r;
+  __device__ static __forceinline__ W make(int f, float d) { return make_uint2(__float_as_uint(d), (uint32_t)f); }
+  __device__ __forceinline__ void put(int64_t pos, int f, float d) const { r[pos] = make(f, d); }
   __device__ __forceinline__ void get(int64_t pos, int& f, float& d) const {
-    const uint2 x = r[pos];
+    const W x = r[pos];
     d = __uint_as_float(x.x);
     f = (int)x.y;
+  }
+};
+struct GPack4 {
+  using W = uint32_t;
+  W* __restrict__ r;
+  __device__ static __forceinline__ W make(int f, float d) {
+    return (__float_as_uint(d) & 0xFFFF0000u) | (uint32_t)f;
+  }
+  __device__ __forceinline__ void put(int64_t pos, int f, float d) const { r[pos] = make(f, d); }
+  __device__ __forceinline__ void get(int64_t pos, int& f, float& d) const {
+    const W x = r[pos];
+    d = __uint_as_float(x & 0xFFFF0000u);
+    f = (int)(x & 0xFFFFu);
   }
 };
 
@@ -493,11 +506,11 @@ __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   return total;
 }
 
-template <typename A, typename T>
+template <typename A, typename T, typename R>
 __device__ __forceinline__ void pack_short_row(
     int v, int wave, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, GPack gp, int2* __restrict__ glist,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, int2* __restrict__ glist,
     int* __restrict__ lds) {
   constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
   const int lane = lane_id();
@@ -581,11 +594,11 @@ __device__ __forceinline__ void pack_short_row(
 template <int NV>
 constexpr int pack_wave_ints() { return kPackWaveMax + 4 + NV * 512; }  // hist | records (8 B)
 
-template <int NV, typename A, typename T>
+template <int NV, typename A, typename T, typename R>
 __device__ __forceinline__ void pack_short_row_v(
     int v, int wave, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, GPack gp, int2* __restrict__ glist,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, int2* __restrict__ glist,
     int* __restrict__ lds) {
   const int lane = lane_id();
   const int rs = ptr[v];
@@ -627,7 +640,7 @@ __device__ __forceinline__ void pack_short_row_v(
     ei[q] = (q < B && p < deg) ? rs + p : 0;
   }
   int* hist = lds + wave * pack_wave_ints<NV>();
-  uint2* lr = reinterpret_cast<uint2*>(hist + kPackWaveMax + 4);  // 16-B aligned: kPackWaveMax + 4 = 260 ints
+  typename R::W* lr = reinterpret_cast<typename R::W*>(hist + kPackWaveMax + 4);  // 16-B aligned: 260 ints
   for (int p = lane; p < deg; p += kWave) hist[p] = 0;
   wave_lds_sync();
   int rank[NV][4];
@@ -671,22 +684,27 @@ __device__ __forceinline__ void pack_short_row_v(
     for (int i = 0; i < 4; ++i)
       if (a[c][i] != arg_none<A>()) {
         const int pos = hist[a[c][i]] + rank[c][i];
-        lr[pos] = make_uint2(__float_as_uint(d[c][i]), (uint32_t)((c * kWave + lane) * 4 + i));
+        lr[pos] = R::make((c * kWave + lane) * 4 + i, d[c][i]);
       }
   wave_lds_sync();
   const int total = __builtin_amdgcn_readlane(x, kWave - 1);
-  // 2 records per lane and store (16 B; vF and the LDS image are 16-B aligned: F % 4 == 0)
-  for (int i = lane * 2; i < total; i += 2 * kWave) {
-    if (i + 2 <= total) *reinterpret_cast<uint4*>(gp.r + vF + i) = *reinterpret_cast<const uint4*>(lr + i);
-    else gp.r[vF + i] = lr[i];
+  // 16-B stores of 2 (8-B) or 4 (4-B) records per lane (vF and the LDS image are 16-B
+  // aligned: F % 4 == 0)
+  constexpr int RP = 16 / sizeof(typename R::W);
+  for (int i = lane * RP; i < total; i += RP * kWave) {
+    if (i + RP <= total) {
+      *reinterpret_cast<uint4*>(gp.r + vF + i) = *reinterpret_cast<const uint4*>(lr + i);
+    } else {
+      for (int k = i; k < total; ++k) gp.r[vF + k] = lr[k];
+    }
   }
 }
 
-template <typename A, typename T>
+template <typename A, typename T, typename R>
 __device__ __forceinline__ void pack_long_row(
     int v, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, GPack gp, int2* __restrict__ glist,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, int2* __restrict__ glist,
     int* __restrict__ lds) {
   int* hist = lds;
   uint16_t* feats = reinterpret_cast<uint16_t*>(lds + kHistMax + 8);
@@ -814,78 +832,57 @@ __device__ __forceinline__ void pack_long_row(
 constexpr int kPackLds = kHistMax + 8 + kGroupMaxF / 2 + 4;
 static_assert(kPackLds >= kWavesPerBlock * (kPackWaveMax + 4), "pack LDS");
 
-template <typename A, typename T = float, int NV = 0>
+template <typename A, typename T, int NV, typename R>
 __global__ __launch_bounds__(kBlock) void group_pack_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F,
     const T* __restrict__ dout, int64_t ldd, const T* __restrict__ fout, int64_t ldf,
-    const float* __restrict__ ew, GPack gp, int2* __restrict__ glist) {
+    const float* __restrict__ ew, R gp, int2* __restrict__ glist) {
   constexpr int kLds = NV > 0 && kWavesPerBlock * pack_wave_ints<NV>() > kPackLds
                            ? kWavesPerBlock * pack_wave_ints<NV>() : kPackLds;
   __shared__ __attribute__((aligned(16))) int lds[kLds];
   const int b = blockIdx.x;
   if (b < n_long) {
-    pack_long_row<A, T>(rows ? rows[b].x : b, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
+    pack_long_row<A, T, R>(rows ? rows[b].x : b, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
   } else {
     const int wave = wave_id_uniform();
     const int v = (b - n_long) * kWavesPerBlock + wave;
     if (v < n_rows)
     {
       if constexpr (NV > 0)
-        pack_short_row_v<NV, A, T>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
+        pack_short_row_v<NV, A, T, R>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
       else
-        pack_short_row<A, T>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
+        pack_short_row<A, T, R>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
     }
   }
 }
 
-// inclusive max-scan over the 64 lanes (values >= -1), the DPP pattern of wave_incl_add
-__device__ __forceinline__ int wave_incl_max(int x) {
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));  // row_shr:1
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));  // row_shr:2
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));  // row_shr:4
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));  // row_shr:8
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return x;
-}
-
 #ifndef PG_PULL_U
-#define PG_PULL_U 4  // 64-entry segments in flight per wave
-#endif
-#ifndef PG_PULL_PROBE
-#define PG_PULL_PROBE 0  // timing-only probes (wrong results): 1 plain LDS adds, 2 no record loads
+#define PG_PULL_U 8  // list segments in flight per wave (4-8 best on S0, 16 +6 %, 32 +25 %)
 #endif
 
-// Pass 2 (pull), dense: one wave per source-row item {u, t0, t1, slot}, its out-edges in
-// windows of 64 (ascending destination). Lane j holds window edge j's descriptor
-// {off, cnt} (loaded through its in-CSR slot tslot[t]). The window's lists, concatenated in
-// edge order, are cut into 64-entry segments, U at a time, so every load instruction
-// carries up to 64 entries of several lists (round 3's pull issued one instruction per
-// list of ~F/deg entries): lane L of segment k takes entry e = 64 k + L, whose edge is the
-// last one whose list starts at or before e (a start marker per list in LDS, an inclusive
-// max-scan across the lanes, carried from segment to segment), and loads record
-// off_j + e - excl_j. Records are added into the LDS row in entry order by
-// compare-and-swap: each lane reads its word, adds, and swaps the sum in; lanes of one
-// instruction that hit the same word are applied in ascending lane order, so the later
-// entry's swap fails and it retries on the earlier one's sum. Every feature's terms are
-// thus summed in ascending v, the sequential scatter_add_'s order (bit-exact on rows that
-// are not split across items). (LDS float atomics, ds_add_f32, keep the same order but run
-// at 1/16 of the integer atomics' rate on gfx950: scripts/probes/lds_rmw_probe.hip; they
-// are what made round 3's dense variant lose.)
-template <typename T = float>
+// Pass 2 (pull): one wave per source-row item {u, t0, t1, slot}, its out-edges in windows
+// of 64 (ascending destination); lane j holds window edge j's descriptor (loaded through its
+// in-CSR slot tslot[t]: the descriptors one window ahead, the slots two). The records of
+// each list are added into an LDS row accumulator. A list never repeats a feature, so the
+// lanes of one segment add into distinct words, and every feature's terms are summed in
+// ascending v, the order of the sequential scatter_add_ (bit-exact on rows that are not
+// split across items). Dense segments across several lists, added in order by LDS
+// compare-and-swap (the float LDS atomic, ds_add_f32, runs at 1/16 of the integer atomics'
+// rate on gfx950: scripts/probes/lds_rmw_probe.hip), measured slower on the engine's data:
+// a source that wins a feature at many destinations puts it many times into one segment,
+// and the swaps serialise.
+template <typename T, typename R>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
-    const int2* __restrict__ glist, GPack gp, int F, const T* __restrict__ mask, int64_t ldm,
+    const int2* __restrict__ glist, R gp, int F, const T* __restrict__ mask, int64_t ldm,
     T* __restrict__ dx, int64_t ldx, float* __restrict__ ws, int64_t ldw) {
   constexpr int U = PG_PULL_U;
   __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
-  __shared__ int marks[kWavesPerBlock][U * kWave];
   const int wave = wave_id_uniform();
   const int it = blockIdx.x * kWavesPerBlock + wave;
   if (it >= n_items) return;
   float* acc = accs[wave];
-  int* mark = marks[wave];
   const int4 item = items[it];
   const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
   const int lane = lane_id();
@@ -906,54 +903,33 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
       dsc_next = glist[ts_next];
       if (tw + 2 * kWave < t1) ts_next = tslot[tl_of(tw + 2 * kWave)];
     }
-    const int cnt = lane < nw ? dsc.y : 0;
-    const int incl = wave_incl_add(cnt);
-    const int excl = incl - cnt;
-    const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
-    int carry = -1;
-    for (int b = 0; b < total; b += U * kWave) {
+    // segments: 64-entry pieces of single lists, U segments' loads in flight. Segment t
+    // belongs to the edge i with excl_i <= t < excl_i + nseg_i, i.e.
+    // i = popcount(ballot(excl <= t)) - 1.
+    {
+      const int nseg = lane < nw ? (dsc.y + kWave - 1) / kWave : 0;
+      const int incl = wave_incl_add(nseg);
+      const int excl = incl - nseg;
+      const int nseg_all = bcast(incl, kWave - 1);
+      for (int s0 = 0; s0 < nseg_all; s0 += U) {
+        const int nv = min(U, nseg_all - s0);
+        int fe[U], ne[U];
+        float de[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) mark[u * kWave + lane] = -1;
-      wave_lds_sync();
-      if (cnt > 0 && excl >= b && excl < b + U * kWave) mark[excl - b] = lane;
-      wave_lds_sync();
-      int fe[U];
-      float de[U];
-      bool in[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = b + u * kWave + lane;
-        in[u] = e < total;
-        int m = max(wave_incl_max(mark[u * kWave + lane]), carry);
-        carry = __builtin_amdgcn_readlane(m, kWave - 1);
-        const int ec = min(e, total - 1);  // lanes past the end load a valid entry, unused
-        m = in[u] ? m : carry;
-        const int off = __builtin_amdgcn_ds_bpermute(m << 2, dsc.x);
-        const int ex = __builtin_amdgcn_ds_bpermute(m << 2, excl);
-#if PG_PULL_PROBE == 2
-        fe[u] = (lane * 4 + u + (off - ex + ec) * 0) & 255;
-        de[u] = 1.f;
-#else
-        gp.get(off + (ec - ex), fe[u], de[u]);
-#endif
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        bool pend = in[u];
-        unsigned* w = reinterpret_cast<unsigned*>(acc + fe[u]);
-#if PG_PULL_PROBE == 1
-        if (pend) *reinterpret_cast<float*>(w) += de[u];
-        pend = false;
-#endif
-        float cur = pend ? *reinterpret_cast<const float*>(w) : 0.f;
-        while (__ballot(pend)) {
-          if (pend) {
-            const unsigned want = __float_as_uint(cur);
-            const unsigned got = atomicCAS(w, want, __float_as_uint(cur + de[u]));
-            pend = got != want;
-            cur = __uint_as_float(got);
-          }
+        for (int u = 0; u < U; ++u) {
+          const int t = s0 + min(u, nv - 1);
+          const int i = __popcll(__ballot(excl <= t)) - 1;
+          const int seg = t - bcast(excl, i);
+          const int base = bcast(dsc.x, i) + seg * kWave;
+          const int n = min(kWave, bcast(dsc.y, i) - seg * kWave);
+          ne[u] = n;
+          // straight-line loads (lanes past n load a valid entry of the same segment), so
+          // the waits are counted instead of a vmcnt(0) behind each branch
+          gp.get(base + min(lane, n - 1), fe[u], de[u]);
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (u < nv && lane < ne[u]) acc[fe[u]] += de[u];
       }
     }
   }
@@ -1440,10 +1416,10 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
   // PG_BWD_DIRECT (variant builds): always the argmax-record gather over the transposed CSR
   if (arg_kind == PG_ARG_U16 && F <= kGroupMaxF && N * F < INT32_MAX && !PG_BWD_DIRECT) {
     char* p = (char*)ws + pbytes;
-    // the records carry the upstream gradient as f32 even for bf16 storage (one rounding of
-    // dx at the end, as the oracle's f32 sums)
-    GPack gp;
-    gp.r = (uint2*)p;
+    // the records carry the upstream gradient as f32 (8 B), or for bf16 storage without edge
+    // weights as its bf16 value (4 B); the sums are f32 either way (one rounding of dx at the
+    // end, as the oracle's f32 sums)
+    void* recs = p;
     p += round_up(N * F * 8, 256);
     int2* glist = (int2*)p;
     p += round_up(g->nnz * 8, 256);
@@ -1459,9 +1435,11 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
                      ((uintptr_t)argpos & 7) == 0 && ((uintptr_t)dout & kTa) == 0 && ((uintptr_t)fwd_out & kTa) == 0;
     const dim3 pgrid((unsigned)(n_long + n_short_blocks));
     const int4* prow = listed ? (const int4*)g->merges : nullptr;
+    auto run = [&](auto gp) {
+    using R = decltype(gp);
     auto pack = [&](auto nv_c) {
       constexpr int NV = decltype(nv_c)::value;
-      hipLaunchKernelGGL((group_pack_kernel<uint16_t, T, NV>), pgrid, dim3(kBlock), 0, st, prow, n_long, (int)N,
+      hipLaunchKernelGGL((group_pack_kernel<uint16_t, T, NV, R>), pgrid, dim3(kBlock), 0, st, prow, n_long, (int)N,
                          g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, g->ew, gp, glist);
       return PG_OK;
     };
@@ -1472,13 +1450,23 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     // in the lists has a maximum X[u,f] w != 0, so X[u,f] > 0; an element with no entries
     // sums to +0, which the mask would leave +0. With fwd_out alone the mask is applied.
     if (dead_none) mask_src = nullptr;
-    hipLaunchKernelGGL((max_bwd_pull_kernel<T>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
+    hipLaunchKernelGGL((max_bwd_pull_kernel<T, R>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
                        (const int4*)gt->items, (int)gt->n_items, glist, gp, (int)F, mask_src, ldm, dx, ldx,
                        w, ws_ld(F));
     if (gt->n_merges > 0)
       hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
                          (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
                          mask_src, ldm, dx, ldx);
+    };
+    if (sizeof(T) == 2 && !g->ew) {
+      GPack4 gp;
+      gp.r = (uint32_t*)recs;
+      run(gp);
+    } else {
+      GPack gp;
+      gp.r = (uint2*)recs;
+      run(gp);
+    }
     return hip_status("pg_spmm_max_bwd");
   }
   if constexpr (sizeof(T) == 4) {

@@ -33,7 +33,7 @@ DEFAULT_CHUNK_BWD = None
 
 
 def default_chunk_bwd(num_nodes: int) -> int:
-    return 128 if num_nodes <= 65536 else 512
+    return 64 if num_nodes <= 65536 else 512
 
 
 def _np_ptr(a: np.ndarray) -> int:
