@@ -417,7 +417,8 @@ def run(args, rank, world, dev, dist, mode, breakdown=True):
                 "step_distribution": step_dist,
                 "scaling": "strong" if not summed else "weak",
                 "what": ("one shared model; every rank runs the full-graph step on its shard of the train rows, "
-                         "one RCCL all-reduce of the gradients per step; value = ONE model's edges/s"
+                         f"one {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} all-reduce of the "
+                         "gradients per step; value = ONE model's edges/s"
                          if not summed else "a different graph per rank; value sums the ranks"),
                 "allreduce": ar_info, "loss": {"train": loss_tr, "val": loss_va}}
 
