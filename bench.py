@@ -519,7 +519,12 @@ def main():
     ap.add_argument("--breakdown-reps", type=int, default=5, help="replays of each launch-group timing graph")
     ap.add_argument("--dump-breakdown", default="", help="write the per-launch-site breakdown (JSON)")
     ap.add_argument("--dropin-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--chunk-bwd", type=int, default=0, help=argparse.SUPPRESS)  # tuning experiments
     args = ap.parse_args()
+    if args.chunk_bwd:
+        import plagnn.graph
+
+        plagnn.graph.CHUNK_BWD_OVERRIDE = args.chunk_bwd
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

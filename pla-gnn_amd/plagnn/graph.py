@@ -32,7 +32,12 @@ DEFAULT_CHUNK = 256
 DEFAULT_CHUNK_BWD = None
 
 
+CHUNK_BWD_OVERRIDE: Optional[int] = None  # tuning experiments (bench.py --chunk-bwd)
+
+
 def default_chunk_bwd(num_nodes: int) -> int:
+    if CHUNK_BWD_OVERRIDE:
+        return CHUNK_BWD_OVERRIDE
     return 64 if num_nodes <= 65536 else 512
 
 
