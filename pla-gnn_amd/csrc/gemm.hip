@@ -69,6 +69,9 @@ constexpr int kSplitBM = PG_SPLIT_TILE / 1000, kSplitBN = PG_SPLIT_TILE % 1000;
 #ifndef PG_X3_TILE_FORCE
 #define PG_X3_TILE_FORCE 0
 #endif
+#ifndef PG_X3_MIN_SLICE
+#define PG_X3_MIN_SLICE 128  // shortest K slice of a split product of the three-piece kernel
+#endif
 #ifndef PG_X3_SPLIT_TARGET
 #define PG_X3_SPLIT_TARGET 512
 #endif
@@ -767,7 +770,7 @@ int pg_gemm_f32_split_k(int64_t M, int64_t N, int64_t K) {
     pick_tile_x3(M, N, K, 2, bm, bn);
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
     const int64_t target = (PG_X3_SPLIT_TARGET + tiles - 1) / tiles;
-    return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, K / 128), 256));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(target, K / PG_X3_MIN_SLICE), 256));
   }
   int bm, bn;
   pick_tile(M, N, K, 1, bm, bn);
