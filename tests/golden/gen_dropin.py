@@ -14,9 +14,9 @@ reference dims (train.py:179), Adam lr 5e-5 (main_normal.py:26), multi_loss (tra
 89-108). Only outputs are stored: every epoch's train / val loss of every (round, fold)
 from its fig_data_<round>.json (train.py:351-357) and the final logits of three
 (round, fold) pairs ({round}_{fold}_loc_logits.npy, train.py:289); and, from a second run
-with -e 1 (the same models: -e does not change what the torch RNG draws), the same
-pairs' logits of the first epoch, i.e. the forward at the initial parameters. No source
-is stored.
+with -e 1 and -e 2 (the same models: -e does not change what the torch RNG draws), the
+same pairs' logits of the first and second epoch, i.e. the forward at the initial
+parameters and after one Adam step. No source is stored.
 tests/test_gpu_dropin_cli.py replays the same seeds and folds through the shim on cuda.
 """
 from __future__ import annotations
@@ -63,6 +63,8 @@ def main():
 
         cli(1)
         first = {p: np.load(os.path.join(log, f"{p[0]}_{p[1]}_loc_logits.npy")).astype(np.float32) for p in LOGITS}
+        cli(2)  # the forward after ONE Adam step
+        second = {p: np.load(os.path.join(log, f"{p[0]}_{p[1]}_loc_logits.npy")).astype(np.float32) for p in LOGITS}
         cli(EPOCHS)
         tl = np.zeros((10, FOLDS, EPOCHS), np.float64)
         vl = np.zeros((10, FOLDS, EPOCHS), np.float64)
@@ -78,6 +80,7 @@ def main():
         for rnd, fold in LOGITS:
             out[f"logits_{rnd}_{fold}"] = np.load(os.path.join(log, f"{rnd}_{fold}_loc_logits.npy")).astype(np.float32)
             out[f"logits0_{rnd}_{fold}"] = first[(rnd, fold)]
+            out[f"logits1_{rnd}_{fold}"] = second[(rnd, fold)]
     np.savez_compressed(os.path.join(HERE, "dropin_cli.npz"), **out)
     print("wrote dropin_cli.npz:", {k: getattr(v, "shape", v) for k, v in out.items()})
 
