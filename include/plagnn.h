@@ -301,6 +301,31 @@ int pg_gemm_f32_partials(int transa, int transb, int64_t M, int64_t N, int64_t K
                          int64_t lda, const float* B, int64_t ldb, const pg_gemm_epilogue_t* ep,
                          int split_k, void* ws, size_t ws_bytes, int* split_used, pg_stream_t stream);
 int pg_gemm_splitk_reduce_batch(const pg_splitk_job_t* jobs, int n_jobs, pg_stream_t stream);
+/* Grouped split-K products (a training step's weight gradients, code/model.py:13-17
+ * backward: they feed only the optimizer, so all of them can run at the end of the
+ * backward): part p computes C_p = op(A_p) op(B_p) (+ C_p when beta_p = 1; beta 0 or 1)
+ * and, if rowsum_p, rowsum_p = the row sums of op(A_p), as pg_gemm_f32 with no other
+ * epilogue. The parts' tiles times one K-slice count for the whole group run as ONE
+ * three-piece launch sized for the chip (so the partial slabs scale with the group's
+ * workgroups, not with each product's), then one combine launch; deterministic. Parts
+ * that are not all of one (transa, transb), or whose operands the three-piece kernel does
+ * not take (16-B alignment, extents multiple of 4), run one after another as pg_gemm_f32.
+ * Up to 16 parts. The workspace size depends on the shapes and flags only. */
+typedef struct pg_gemm_part {
+  int32_t transa, transb;
+  int64_t M, N, K;
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float beta;
+  float* C;
+  int64_t ldc;
+  float* rowsum; /* or NULL */
+} pg_gemm_part_t;
+size_t pg_gemm_f32_group_workspace(const pg_gemm_part_t* parts, int n_parts);
+int pg_gemm_f32_group(const pg_gemm_part_t* parts, int n_parts, void* ws, size_t ws_bytes,
+                      pg_stream_t stream);
 int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
                 int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
@@ -430,8 +455,9 @@ int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-
                          pg_spmm_max_bwd[_bf16] takes mask_src >= 0 and does not read it;
                          PG_ARG_DEAD_NONE; 7: pg_spmm_max_bwd reads no einv, smaller
                          workspace; 8: pg_csr_t without einv; max backward lists as 8-B
-                         records with the edge weight folded in, dense pull; with fwd_out
-                         alone the relu' mask is applied, only PG_ARG_DEAD_NONE implies it */
+                         records with the edge weight folded in; with fwd_out alone the
+                         relu' mask is applied, only PG_ARG_DEAD_NONE implies it;
+                         9: pg_gemm_f32_group */
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,9 @@ constexpr int kSplitBM = PG_SPLIT_TILE / 1000, kSplitBN = PG_SPLIT_TILE % 1000;
 #ifndef PG_X3_TILE_FORCE
 #define PG_X3_TILE_FORCE 0
 #endif
+#ifndef PG_X3_GROUP_TARGET
+#define PG_X3_GROUP_TARGET 768  // workgroups of a grouped split-K launch (three 128 x 128 per CU)
+#endif
 #ifndef PG_X3_MIN_SLICE
 #define PG_X3_MIN_SLICE 128  // shortest K slice of a split product of the three-piece kernel
 #endif
@@ -962,6 +965,123 @@ int pg_gemm_splitk_reduce_batch(const pg_splitk_job_t* jobs, int n_jobs, pg_stre
   if (e != hipSuccess)
     return pg::set_error((int)e, "pg_gemm_splitk_reduce_batch: launch failed: %s", hipGetErrorString(e));
   return pg::ok();
+}
+
+}  // extern "C"
+
+namespace {
+
+// The group's plan: one K-slice count for every part, chosen so that the union of the
+// parts' 128 x 128 tiles times the slices fills PG_X3_GROUP_TARGET workgroups (three per
+// CU), each slice >= PG_X3_MIN_SLICE entries of K; each part's slabs (+ row-sum slices) at
+// a 256-B aligned offset of ws.
+struct GroupPlan {
+  int split[kX3MaxParts];
+  int kps[kX3MaxParts];
+  size_t off[kX3MaxParts + 1];
+};
+
+inline void group_plan(const pg_gemm_part_t* parts, int n, GroupPlan& g) {
+  int64_t tiles = 0;
+  for (int p = 0; p < n; ++p) tiles += ((parts[p].M + 127) / 128) * ((parts[p].N + 127) / 128);
+  const int64_t s = std::max<int64_t>(1, PG_X3_GROUP_TARGET / std::max<int64_t>(1, tiles));
+  size_t off = 0;
+  for (int p = 0; p < n; ++p) {
+    const pg_gemm_part_t& q = parts[p];
+    int64_t sp = std::max<int64_t>(1, std::min<int64_t>(s, q.K / PG_X3_MIN_SLICE));
+    int64_t kps = (q.K + sp - 1) / sp;
+    kps = std::max<int64_t>(BK, (kps + BK - 1) / BK * BK);
+    sp = std::max<int64_t>(1, (q.K + kps - 1) / kps);
+    g.split[p] = (int)sp;
+    g.kps[p] = (int)kps;
+    g.off[p] = off;
+    off += ((size_t)sp * (size_t)std::max<int64_t>(q.M, 0) * (size_t)(std::max<int64_t>(q.N, 0) + 1) * 4 + 255) /
+           256 * 256;
+  }
+  g.off[n] = off;
+}
+
+inline bool part_ok(const pg_gemm_part_t& q) {
+  return q.M >= 0 && q.N >= 0 && q.K >= 0 && q.M <= INT32_MAX && q.N <= INT32_MAX && q.K <= INT32_MAX &&
+         q.ldc >= q.N && (q.transa ? q.lda >= q.M : q.lda >= q.K) && (q.transb ? q.ldb >= q.K : q.ldb >= q.N) &&
+         (q.beta == 0.f || q.beta == 1.f);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t pg_gemm_f32_group_workspace(const pg_gemm_part_t* parts, int n) {
+  if (n <= 0 || n > kX3MaxParts || !parts) return 0;
+  GroupPlan g;
+  group_plan(parts, n, g);
+  size_t need = g.off[n];
+  for (int p = 0; p < n; ++p) {  // the per-part path (operands the grouped kernel does not take)
+    const pg_gemm_part_t& q = parts[p];
+    need = std::max(need, pg_gemm_f32_workspace(q.M, q.N, q.K, pg_gemm_f32_split_k(q.M, q.N, q.K)));
+  }
+  return std::max<size_t>(need, 256);
+}
+
+int pg_gemm_f32_group(const pg_gemm_part_t* parts, int n, void* ws, size_t ws_bytes, pg_stream_t stream) {
+  if (n < 0 || n > kX3MaxParts || (n > 0 && !parts))
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32_group: 0..%d parts", kX3MaxParts);
+  if (n == 0) return pg::ok();
+  for (int p = 0; p < n; ++p)
+    if (!part_ok(parts[p])) return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32_group: bad part %d", p);
+  if (ws_bytes < pg_gemm_f32_group_workspace(parts, n) || !ws)
+    return pg::set_error(PG_ERR_WORKSPACE, "pg_gemm_f32_group: workspace too small");
+  GroupPlan g;
+  group_plan(parts, n, g);
+  const pg_gemm_epilogue_t none{nullptr, PG_ACT_NONE, 0.f, nullptr, 0, nullptr};
+  bool grouped = PG_GEMM_ALGO != 0;
+  for (int p = 0; p < n && grouped; ++p) {
+    const pg_gemm_part_t& q = parts[p];
+    grouped = q.transa == parts[0].transa && q.transb == parts[0].transb &&
+              x3_ok(q.transa, q.transb, q.M, q.N, q.K, q.A, q.lda, q.B, q.ldb, nullptr, 0, &none, true,
+                    (char*)ws + g.off[p]);
+  }
+  if (!grouped) {  // each part on its own (split-K product + combine)
+    for (int p = 0; p < n; ++p) {
+      const pg_gemm_part_t& q = parts[p];
+      const pg_gemm_epilogue_t ep{nullptr, PG_ACT_NONE, 0.f, nullptr, 0, q.rowsum};
+      const int rc = gemm_f32_impl(q.transa, q.transb, q.M, q.N, q.K, 1.f, q.A, q.lda, q.B, q.ldb, q.beta, q.C,
+                                   q.ldc, &ep, pg_gemm_f32_split_k(q.M, q.N, q.K), ws, ws_bytes, stream, false,
+                                   nullptr);
+      if (rc != PG_OK) return rc;
+    }
+    return pg::ok();
+  }
+  X3Group xg{};
+  pg_splitk_job_t jobs[kX3MaxParts];
+  int items = 0, nj = 0;
+  for (int p = 0; p < n; ++p) {
+    const pg_gemm_part_t& q = parts[p];
+    if (q.M == 0 || q.N == 0) continue;
+    float* w = (float*)((char*)ws + g.off[p]);
+    X3Part& x = xg.p[nj];
+    x.M = (int)q.M; x.N = (int)q.N; x.K = (int)q.K; x.kps = g.kps[p];
+    x.tiles_n = (int)((q.N + 127) / 128);
+    x.tiles = x.tiles_n * (int)((q.M + 127) / 128);
+    x.first_item = items;
+    x.A = q.A; x.lda = q.lda; x.B = q.B; x.ldb = q.ldb;
+    x.ws = w;
+    x.ws_rowsum = w + (int64_t)g.split[p] * q.M * q.N;
+    x.rowsum = q.rowsum;
+    items += x.tiles * g.split[p];
+    pg_splitk_job_t& j = jobs[nj];
+    j.ws = w; j.split_k = g.split[p]; j.M = q.M; j.N = q.N;
+    j.alpha = 1.f; j.beta = q.beta; j.C = q.C; j.ldc = q.ldc; j.rowsum = q.rowsum;
+    ++nj;
+  }
+  if (nj == 0) return pg::ok();
+  xg.n = nj;
+  xg.items = items;
+  const int rc = gemm_x3_group_launch(xg, parts[0].transa != 0, parts[0].transb != 0, (hipStream_t)stream);
+  const hipError_t e = hipGetLastError();
+  if (rc != PG_OK || e != hipSuccess)
+    return pg::set_error(rc != PG_OK ? rc : (int)e, "pg_gemm_f32_group: launch failed");
+  return pg_gemm_splitk_reduce_batch(jobs, nj, stream);
 }
 
 }  // extern "C"

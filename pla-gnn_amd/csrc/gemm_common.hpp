@@ -149,6 +149,24 @@ struct X3Args {
 };
 int gemm_x3_launch(const X3Args& a, hipStream_t st);
 
+// Grouped split-K partials (pg_gemm_f32_group): 128 x 128 tiles, one (ta, tb) for the group.
+struct X3Part {
+  int M, N, K, kps, tiles_n, tiles, first_item;
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float* ws;         // [n_split][M][N] slabs
+  float* ws_rowsum;  // [n_split][M] row-sum slices
+  float* rowsum;     // non-null: row sums wanted (the slices are written; the combine writes here)
+};
+constexpr int kX3MaxParts = 16;
+struct X3Group {
+  X3Part p[kX3MaxParts];
+  int n, items;
+};
+int gemm_x3_group_launch(const X3Group& g, bool ta, bool tb, hipStream_t st);
+
 // Threads per output of the split-K combine: enough slice groups that each thread sums
 // <= ~8 slices.
 inline int splitk_groups(int split_k) { return split_k <= 8 ? 1 : split_k <= 32 ? 4 : 16; }

@@ -239,14 +239,22 @@ __device__ unsigned long long pg_x3_stamp[64][66][4];
 template <int BM, int BN>
 constexpr int x3_depth() { return BM * BN <= 128 * 64 ? 2 : 1; }
 
+template <int BM, int BN>
+constexpr int x3_lds_u16() {
+  constexpr int STAGE_U16 = 2 * 3 * (BM * KS + BN * KS);  // two buffers of [A_h A_m A_l | B_h B_m B_l]
+  constexpr int PASSES = 2 * BM * BN > STAGE_U16 ? 2 : 1;
+  constexpr int EPI_U16 = 2 * BM * BN / PASSES;
+  return STAGE_U16 > EPI_U16 ? STAGE_U16 : EPI_U16;
+}
+
+// One output tile (tm, tn) over the K slice kz of the product: the whole workgroup's work.
 template <int BM, int BN, bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_depth<BM, BN>() == 2 ? 4 : 1)))
-void gemm_x3_kernel(
-    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
+__device__ __forceinline__ void x3_tile(
+    uint16_t* __restrict__ lds, int M, int N, int K, int k_per_split, int kz, int tm, int tn, float alpha,
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
     float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
     const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
-    float* __restrict__ ws, float* __restrict__ ws_rowsum, int n_split) {
+    float* __restrict__ ws, float* __restrict__ ws_rowsum) {
   constexpr bool AK = TA, BKM = !TB;
   constexpr bool SPLIT = EPI == EPI_SPLIT;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -254,18 +262,8 @@ void gemm_x3_kernel(
   constexpr int BUF = 3 * (IA + IB);         // one buffer: [A_h A_m A_l | B_h B_m B_l]
   constexpr int STAGE_U16 = 2 * BUF;
   constexpr int PASSES = 2 * BM * BN > STAGE_U16 ? 2 : 1;  // f32 epilogue image in row bands
-  constexpr int EPI_U16 = 2 * BM * BN / PASSES;
-  constexpr int LDS_U16 = STAGE_U16 > EPI_U16 ? STAGE_U16 : EPI_U16;
-  static_assert(LDS_U16 * 2 >= NT * 4 * 8, "row-sum scratch");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
+  static_assert(x3_lds_u16<BM, BN>() * 2 >= NT * 4 * 8, "row-sum scratch");
 
-  // XCD-aware order over the (slice, tile) items (as gemm.hip's DMA kernel)
-  const int b = blockIdx.x;
-  const int items = tiles * n_split;
-  const int q8 = items / 8, r8 = items % 8, x8 = b % 8;
-  const int item = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int kz = item / tiles, tile = item % tiles;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, l32 = lane & 31;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -420,6 +418,48 @@ void gemm_x3_kernel(
   X3_STAMP(65, 1);
 }
 
+// XCD-aware order over `items` (slice-major within a product): workgroup b runs on XCD
+// b % 8, which takes one contiguous range of the items, so the workgroups sharing a K
+// slice's operand rows share that XCD's L2 (as gemm.hip's DMA kernel)
+__device__ __forceinline__ int x3_item(int items) {
+  const int b = blockIdx.x;
+  const int q8 = items / 8, r8 = items % 8, x8 = b % 8;
+  return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+}
+
+template <int BM, int BN, bool TA, bool TB, int EPI>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_depth<BM, BN>() == 2 ? 4 : 1)))
+void gemm_x3_kernel(
+    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
+    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
+    const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
+    float* __restrict__ ws, float* __restrict__ ws_rowsum, int n_split) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[x3_lds_u16<BM, BN>()];
+  const int item = x3_item(tiles * n_split);
+  const int kz = item / tiles, tile = item % tiles;
+  x3_tile<BM, BN, TA, TB, EPI>(lds, M, N, K, k_per_split, kz, tile / tiles_n, tile % tiles_n, alpha, A, lda, B,
+                               ldb, beta, C, ldc, bias, slope, dact, lddact, rowsum, ws, ws_rowsum);
+}
+
+// Grouped split-K partials: the items of every part (its tiles x its K slices, slice-major)
+// laid end to end, one launch for all of them (the step's weight gradients: the slab bytes
+// then scale with the group's workgroups, not with each product's).
+template <int BM, int BN, bool TA, bool TB>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_depth<BM, BN>() == 2 ? 4 : 1)))
+void gemm_x3_group_kernel(X3Group g) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[x3_lds_u16<BM, BN>()];
+  const int item = x3_item(g.items);
+  int k = 0;
+  while (k + 1 < g.n && item >= g.p[k + 1].first_item) ++k;
+  const X3Part& p = g.p[k];
+  const int local = item - p.first_item;
+  const int kz = local / p.tiles, tile = local % p.tiles;
+  x3_tile<BM, BN, TA, TB, EPI_SPLIT>(lds, p.M, p.N, p.K, p.kps, kz, tile / p.tiles_n, tile % p.tiles_n, 1.f, p.A,
+                                     p.lda, p.B, p.ldb, 0.f, nullptr, 0, nullptr, 0.f, nullptr, 0, p.rowsum, p.ws,
+                                     p.ws_rowsum);
+}
+
 
 
 template <int BM, int BN, bool TA, bool TB>
@@ -453,6 +493,17 @@ int launch_trans(const X3Args& a, hipStream_t st) {
 }  // namespace
 
 namespace pg_gemm {
+
+int gemm_x3_group_launch(const X3Group& g, bool ta, bool tb, hipStream_t st) {
+  const dim3 grid((unsigned)g.items), block(NT);
+#define PG_G(TA_, TB_) hipLaunchKernelGGL((gemm_x3_group_kernel<128, 128, TA_, TB_>), grid, block, 0, st, g)
+  if (ta && !tb) PG_G(true, false);
+  else if (!ta && !tb) PG_G(false, false);
+  else if (!ta && tb) PG_G(false, true);
+  else PG_G(true, true);
+#undef PG_G
+  return PG_OK;
+}
 
 int gemm_x3_launch(const X3Args& a, hipStream_t st) {
   if (a.bm == 128 && a.bn == 128) return launch_trans<128, 128>(a, st);

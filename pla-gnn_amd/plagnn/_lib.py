@@ -68,6 +68,26 @@ _d = ctypes.c_double
 _sz = ctypes.c_size_t
 _vp = ctypes.c_void_p
 _csr = ctypes.POINTER(PgCsr)
+class PgGemmPart(ctypes.Structure):
+    """pg_gemm_part_t (include/plagnn.h)."""
+
+    _fields_ = [
+        ("transa", ctypes.c_int32),
+        ("transb", ctypes.c_int32),
+        ("M", ctypes.c_int64),
+        ("N", ctypes.c_int64),
+        ("K", ctypes.c_int64),
+        ("A", ctypes.c_void_p),
+        ("lda", ctypes.c_int64),
+        ("B", ctypes.c_void_p),
+        ("ldb", ctypes.c_int64),
+        ("beta", ctypes.c_float),
+        ("C", ctypes.c_void_p),
+        ("ldc", ctypes.c_int64),
+        ("rowsum", ctypes.c_void_p),
+    ]
+
+
 class PgSplitkJob(ctypes.Structure):
     """pg_splitk_job_t (include/plagnn.h)."""
 
@@ -100,6 +120,8 @@ SIGNATURES = {
     "pg_gemm_f32_partials": (_i, [_i, _i, _i64, _i64, _i64, _vp, _i64, _vp, _i64, ctypes.POINTER(PgGemmEpilogue),
                                   _i, _vp, _sz, ctypes.POINTER(ctypes.c_int), _vp]),
     "pg_gemm_splitk_reduce_batch": (_i, [ctypes.POINTER(PgSplitkJob), _i, _vp]),
+    "pg_gemm_f32_group_workspace": (_sz, [ctypes.POINTER(PgGemmPart), _i]),
+    "pg_gemm_f32_group": (_i, [ctypes.POINTER(PgGemmPart), _i, _vp, _sz, _vp]),
     "pg_csr_spmm_f64": (_i, [_i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),
     "pg_spmm_max_bwd_scatter": (_i, [_csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "pg_spmm_sum_workspace": (_sz, [_csr, _i64]),

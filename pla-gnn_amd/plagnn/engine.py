@@ -76,6 +76,9 @@ class _Flat:
 
 class TrainEngine:
     REDUCE_INLINE = False  # True: each split-K combine right after its partials (A/B knob)
+    # True: every weight gradient of the step in one grouped split-K launch at the end of the
+    # backward (pg_gemm_f32_group); False: one split-K launch per product (A/B knob)
+    GROUP_WGRAD = True
     WIDTH_ALIGN = 4  # every padded width is a multiple of this
     _cur = ""                      # launch site being issued (_t)
     _filter: Optional[str] = None  # group_times: issue only this launch group
@@ -219,10 +222,19 @@ class TrainEngine:
         # weight gradients' split-K combines deferred to one batched launch per step
         self._slabs: Dict[str, torch.Tensor] = {}
         self._jobs: list = []
+        self._parts: list = []
         for (M_, N_, K_) in self._wgrad_shapes():
             sk = ops._split_k(M_, N_, K_)
             self._gemm_plans[(M_, N_, K_)] = sk
             need = max(need, L.pg_gemm_f32_workspace(M_, N_, K_, sk))
+        if self.GROUP_WGRAD:
+            # the grouped launch's slabs: sized from the shapes alone (transposed A, plain B)
+            shapes = self._wgrad_shapes()
+            parts = (_lib.PgGemmPart * len(shapes))()
+            for i, (M_, N_, K_) in enumerate(shapes):
+                parts[i].transa, parts[i].transb, parts[i].M, parts[i].N, parts[i].K = 1, 0, M_, N_, K_
+            self.gws = torch.empty(int(L.pg_gemm_f32_group_workspace(parts, len(shapes))), dtype=torch.uint8,
+                                   device=dev)
         need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
         self.ws_bytes = self.ws.numel()
@@ -427,6 +439,13 @@ class TrainEngine:
         N = B.shape[0] if transb else B.shape[1]
         self._rec_gemm(A, B, C, M, N, K, beta, dact)
         sk = self._gemm_plans.get((M, N, K), 1) if (bias is None and act == NONE and dact is None) else 1
+        if self.GROUP_WGRAD and (M, N, K) in self._gemm_plans and bias is None and act == NONE and dact is None:
+            q = _lib.PgGemmPart()
+            q.transa, q.transb, q.M, q.N, q.K = int(transa), int(transb), M, N, K
+            q.A, q.lda, q.B, q.ldb = ptr(A), A.stride(0), ptr(B), B.stride(0)
+            q.beta, q.C, q.ldc, q.rowsum = beta, ptr(C), C.stride(0), ptr(rowsum)
+            self._parts.append((q, 2.0 * M * N * K))
+            return
         if sk > 1:
             self._gemm_partials(A, B, C, transa, transb, beta, rowsum, tag, M, N, K, sk)
             return
@@ -458,6 +477,11 @@ class TrainEngine:
             self._reduce_deferred()
 
     def _reduce_deferred(self) -> None:
+        parts, self._parts = self._parts, []
+        if parts:
+            arr = (_lib.PgGemmPart * len(parts))(*[q for q, _ in parts])
+            with self._t("gemm.wgrad.group", sum(w for _, w in parts)):
+                self._call("pg_gemm_f32_group", arr, len(parts), ptr(self.gws), self.gws.numel(), self._s())
         jobs, self._jobs = self._jobs, []
         for i in range(0, len(jobs), 16):
             part = jobs[i:i + 16]

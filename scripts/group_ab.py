@@ -24,6 +24,9 @@ def main():
     if os.environ.get("PG_REDUCE_INLINE") is not None:  # A/B of the split-K combine placement
         plagnn.TrainEngine.REDUCE_INLINE = os.environ["PG_REDUCE_INLINE"] == "1"
         label += f"+inline{os.environ['PG_REDUCE_INLINE']}"
+    if os.environ.get("PG_GROUP_WGRAD") is not None:  # A/B of the grouped weight gradients
+        plagnn.TrainEngine.GROUP_WGRAD = os.environ["PG_GROUP_WGRAD"] == "1"
+        label += f"+group{os.environ['PG_GROUP_WGRAD']}"
     if wl.bf16 and os.environ.get("PG_STACK_T") is not None:  # A/B of the stacked-weight layout
         plagnn.TrainEngineBF16.STACK_T = os.environ["PG_STACK_T"] == "1"
         label += f"+stackT{os.environ['PG_STACK_T']}"

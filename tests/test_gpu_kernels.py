@@ -552,6 +552,87 @@ def test_gemm_split_k_deferred_batch_reduce_is_bitwise():
         assert torch.equal(rs, rs_ref)
 
 
+def _group_parts(specs, gen):
+    """pg_gemm_part_t array + the tensors behind it; spec = (ta, tb, M, N, K, beta, rowsum,
+    misalign): misalign offsets A by one float (the grouped kernel does not take it)."""
+    from plagnn import _lib
+    from plagnn._lib import ptr
+
+    parts = (_lib.PgGemmPart * len(specs))()
+    keep = []
+    for q, (ta, tb, M, N, K, beta, want_rs, mis) in zip(parts, specs):
+        a = torch.randn(K * M + 1, generator=gen).to(DEV)
+        A = (a[1:] if mis else a[:-1]).view(*((K, M) if ta else (M, K)))
+        B = torch.randn(*((N, K) if tb else (K, N)), generator=gen).to(DEV)
+        C = torch.randn(M, N, generator=gen).to(DEV)
+        rs = torch.full((M,), float("nan"), device=DEV) if want_rs else None
+        q.transa, q.transb, q.M, q.N, q.K = int(ta), int(tb), M, N, K
+        q.A, q.lda, q.B, q.ldb = ptr(A), A.stride(0), ptr(B), B.stride(0)
+        q.beta, q.C, q.ldc, q.rowsum = beta, ptr(C), C.stride(0), ptr(rs)
+        keep.append((ta, tb, A, B, C, C.clone(), rs, beta))
+    return parts, keep
+
+
+# the cfg2 step's weight gradients (TrainEngine groups them), one with beta = 1, and ragged
+_CFG2_WGRADS = [(True, False, 256, 1008, 24041, 0.0, True, False), (True, False, 504, 504, 24041, 0.0, True, False),
+                (True, False, 256, 512, 24041, 1.0, True, False), (True, False, 256, 256, 24041, 0.0, True, False),
+                (True, False, 100, 256, 24041, 0.0, True, False), (True, False, 12, 100, 24041, 0.0, True, False),
+                (True, False, 0, 64, 24041, 0.0, False, False), (True, False, 132, 20, 999, 1.0, False, False)]
+
+
+@pytest.mark.parametrize("case", ["grouped", "misaligned", "mixed"])
+def test_gemm_f32_group(case):
+    """pg_gemm_f32_group against float64: every part's product within float32 bounds, beta
+    = 1 accumulating, row sums, an empty part, a ragged short-K part; deterministic (two
+    calls bitwise equal). `misaligned` / `mixed` (a part on another transposition) take the
+    one-by-one path, which must give the same contract."""
+    from plagnn import _lib
+    from plagnn._lib import call, ptr
+
+    specs = list(_CFG2_WGRADS)
+    if case == "misaligned":
+        specs[3] = specs[3][:7] + (True,)
+    elif case == "mixed":
+        specs[-1] = (False, True, 132, 20, 999, 1.0, False, False)
+    gen = torch.Generator().manual_seed(5)
+    parts, keep = _group_parts(specs, gen)
+    n = len(specs)
+    ws = torch.empty(int(_lib.lib().pg_gemm_f32_group_workspace(parts, n)), dtype=torch.uint8, device=DEV)
+    st = _lib.stream_handle(torch.device(DEV))
+    call("pg_gemm_f32_group", parts, n, ptr(ws), ws.numel(), st)
+    first = [(C.clone(), None if rs is None else rs.clone()) for (_, _, _, _, C, _, rs, _) in keep]
+    for (_, _, _, _, C, C0, _, _) in keep:
+        C.copy_(C0)
+    call("pg_gemm_f32_group", parts, n, ptr(ws), ws.numel(), st)
+    torch.cuda.synchronize()
+    for (ta, tb, A, B, C, C0, rs, beta), (c1, r1) in zip(keep, first):
+        assert torch.equal(C, c1) and (rs is None or torch.equal(rs, r1))
+        a64 = (A.t() if ta else A).double()
+        b64 = (B.t() if tb else B).double()
+        if a64.shape[0] == 0:
+            continue
+        ref = a64 @ b64 + beta * C0.double()
+        scale = (a64.abs() @ b64.abs()).max().item() + beta * C0.abs().max().item()
+        assert (C.double() - ref).abs().max().item() <= 2e-6 * scale
+        if rs is not None:
+            rs64 = a64.sum(1)
+            bound = 2e-7 * 256 ** 0.5 * a64.pow(2).sum(1).sqrt() + 2e-7 * rs64.abs()
+            assert torch.all((rs.double() - rs64).abs() <= bound)
+
+
+def test_gemm_f32_group_bad_args():
+    from plagnn import _lib
+
+    gen = torch.Generator().manual_seed(6)
+    parts, keep = _group_parts(_CFG2_WGRADS[:2], gen)
+    L = _lib.lib()
+    ws = torch.empty(int(L.pg_gemm_f32_group_workspace(parts, 2)), dtype=torch.uint8, device=DEV)
+    assert L.pg_gemm_f32_group(parts, 2, ws.data_ptr(), ws.numel() - 256, None) == -3
+    parts[1].beta = 0.5
+    assert L.pg_gemm_f32_group(parts, 2, ws.data_ptr(), ws.numel(), None) == -1
+    assert L.pg_gemm_f32_group(parts, 17, ws.data_ptr(), ws.numel(), None) == -1
+
+
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(1, 4, 4), (33, 12, 20), (129, 132, 100), (64, 4, 1000), (4, 260, 36)])
 def test_gemm_f32_edge_shapes_with_epilogue(ta, tb, M, N, K):
