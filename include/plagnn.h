@@ -314,9 +314,9 @@ int pg_gemm_splitk_reduce_batch(const pg_splitk_job_t* jobs, int n_jobs, pg_stre
 typedef struct pg_gemm_part {
   int32_t transa, transb;
   int64_t M, N, K;
-  const float* A;
+  const void* A; /* f32 (pg_gemm_f32_group) or bf16 bits (pg_gemm_bf16_group); C is f32 */
   int64_t lda;
-  const float* B;
+  const void* B;
   int64_t ldb;
   float beta;
   float* C;
@@ -343,6 +343,15 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
  * 4; split_k > 1 only with an f32 C. Else PG_ERR_UNSUPPORTED. */
 int pg_gemm_bf16_split_k(int64_t M, int64_t N, int64_t K);
 size_t pg_gemm_bf16_workspace(int64_t M, int64_t N, int64_t K, int split_k);
+/* pg_gemm_f32_group's contract with bf16 operands and f32 C (bf16 weight gradients): parts
+ * of one (transa, transb) whose 256 x 256 tiles waste at most 4x their area run as one
+ * split-K launch of the two-phase kernel (one K-slice count for the group, chosen so the
+ * items fill whole rounds of one workgroup per CU) and one combine; the others (and all of
+ * them when the operands break pg_gemm_bf16's layout rules) one after another as
+ * pg_gemm_bf16. Up to 16 parts. */
+size_t pg_gemm_bf16_group_workspace(const pg_gemm_part_t* parts, int n_parts);
+int pg_gemm_bf16_group(const pg_gemm_part_t* parts, int n_parts, void* ws, size_t ws_bytes,
+                       pg_stream_t stream);
 int pg_gemm_bf16(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
                  const void* A, int64_t lda, const void* B, int64_t ldb, float beta, void* C,
                  int64_t ldc, int c_dtype, const pg_gemm_epilogue_t* ep, int split_k, void* ws,

@@ -1038,14 +1038,14 @@ int pg_gemm_f32_group(const pg_gemm_part_t* parts, int n, void* ws, size_t ws_by
   for (int p = 0; p < n && grouped; ++p) {
     const pg_gemm_part_t& q = parts[p];
     grouped = q.transa == parts[0].transa && q.transb == parts[0].transb &&
-              x3_ok(q.transa, q.transb, q.M, q.N, q.K, q.A, q.lda, q.B, q.ldb, nullptr, 0, &none, true,
+              x3_ok(q.transa, q.transb, q.M, q.N, q.K, (const float*)q.A, q.lda, (const float*)q.B, q.ldb, nullptr, 0, &none, true,
                     (char*)ws + g.off[p]);
   }
   if (!grouped) {  // each part on its own (split-K product + combine)
     for (int p = 0; p < n; ++p) {
       const pg_gemm_part_t& q = parts[p];
       const pg_gemm_epilogue_t ep{nullptr, PG_ACT_NONE, 0.f, nullptr, 0, q.rowsum};
-      const int rc = gemm_f32_impl(q.transa, q.transb, q.M, q.N, q.K, 1.f, q.A, q.lda, q.B, q.ldb, q.beta, q.C,
+      const int rc = gemm_f32_impl(q.transa, q.transb, q.M, q.N, q.K, 1.f, (const float*)q.A, q.lda, (const float*)q.B, q.ldb, q.beta, q.C,
                                    q.ldc, &ep, pg_gemm_f32_split_k(q.M, q.N, q.K), ws, ws_bytes, stream, false,
                                    nullptr);
       if (rc != PG_OK) return rc;
@@ -1064,7 +1064,7 @@ int pg_gemm_f32_group(const pg_gemm_part_t* parts, int n, void* ws, size_t ws_by
     x.tiles_n = (int)((q.N + 127) / 128);
     x.tiles = x.tiles_n * (int)((q.M + 127) / 128);
     x.first_item = items;
-    x.A = q.A; x.lda = q.lda; x.B = q.B; x.ldb = q.ldb;
+    x.A = (const float*)q.A; x.lda = q.lda; x.B = (const float*)q.B; x.ldb = q.ldb;
     x.ws = w;
     x.ws_rowsum = w + (int64_t)g.split[p] * q.M * q.N;
     x.rowsum = q.rowsum;

@@ -133,6 +133,8 @@ __device__ __forceinline__ bf16x8 frag(const uint16_t* __restrict__ S, int rc, i
   }
 }
 
+__device__ __attribute__((aligned(16))) float g_zero4f[4] = {0.f, 0.f, 0.f, 0.f};  // never written; read as a float4
+
 __device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
 __device__ __forceinline__ uint16_t f2bf(float x) {
   return __builtin_bit_cast(uint16_t, static_cast<__bf16>(x));
@@ -149,6 +151,24 @@ __device__ __forceinline__ float img_rowsum(const uint16_t* __restrict__ As, int
   return s;
 }
 
+// row sums of a k-image A tile ([KB k][BM rows], 8-row chunks swizzled per k-row): thread t
+// adds chunk t % (BM / 8)'s 8 rows over the k-rows t / (BM / 8) + G i with one
+// ds_read_b128 each (8x fewer LDS reads than one u16 per row and k)
+template <int BM, int NT, int KB = BK>
+__device__ __forceinline__ void img_rowsum8(const uint16_t* __restrict__ As, int tid, float (&rs)[8]) {
+  constexpr int CPR = BM / 8, G = NT / CPR;
+  static_assert(NT % CPR == 0 && KB % G == 0, "k-groups");
+  const int c = tid % CPR, g = tid / CPR;
+#pragma unroll
+  for (int i = 0; i < KB / G; ++i) {
+    const int k = g + i * G;
+    const int f = BM == 64 ? ((k >> 1) & 1) * 4 : (k & 3) * 4;
+    const uint4 v = *reinterpret_cast<const uint4*>(As + k * BM + ((c ^ f) << 3));
+    rs[0] += bf2f(v.x & 0xFFFF); rs[1] += bf2f(v.x >> 16); rs[2] += bf2f(v.y & 0xFFFF); rs[3] += bf2f(v.y >> 16);
+    rs[4] += bf2f(v.z & 0xFFFF); rs[5] += bf2f(v.z >> 16); rs[6] += bf2f(v.w & 0xFFFF); rs[7] += bf2f(v.w >> 16);
+  }
+}
+
 // s_waitcnt vmcnt(N) alone (expcnt, lgkmcnt left at their no-wait maxima), gfx9 encoding
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -157,20 +177,21 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // one output quad (row gr, columns gc .. gc + 3) with the fused epilogue, or its split-K
-// partial (slab blockIdx.z)
+// partial (slab kz)
+// (d2: the activation operand's quad at (gr, gc), b4: the bias quad at gc, both loaded by
+// the caller ahead of the store loop)
 template <int EPI, bool OBF>
 __device__ __forceinline__ void store4(const float4 v, int gr, int gc, int M, int N, float alpha, float beta,
                                        void* __restrict__ Cv, int64_t ldc, const float* __restrict__ bias,
-                                       float slope, const uint16_t* __restrict__ dact, int64_t lddact,
-                                       float* __restrict__ ws) {
+                                       const float4 b4, float slope, const uint2 d2, float* __restrict__ ws,
+                                       int kz) {
   if constexpr (EPI == EPI_SPLIT) {
-    *reinterpret_cast<float4*>(ws + ((int64_t)blockIdx.z * M + gr) * N + gc) = v;
+    *reinterpret_cast<float4*>(ws + ((int64_t)kz * M + gr) * N + gc) = v;
     return;
   } else {
     float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
     float y[4] = {0.f, 0.f, 0.f, 0.f};
     if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
-      const uint2 d2 = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gc);
       y[0] = bf2f(d2.x & 0xFFFF); y[1] = bf2f(d2.x >> 16); y[2] = bf2f(d2.y & 0xFFFF); y[3] = bf2f(d2.y >> 16);
     }
     if constexpr (OBF) {
@@ -181,7 +202,6 @@ __device__ __forceinline__ void store4(const float4 v, int gr, int gc, int M, in
         o[2] = o[2] + beta * bf2f(c2.y & 0xFFFF); o[3] = o[3] + beta * bf2f(c2.y >> 16);
       }
       if (bias) {
-        const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
         o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
       }
       uint2 w;
@@ -198,7 +218,6 @@ __device__ __forceinline__ void store4(const float4 v, int gr, int gc, int M, in
         o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
       }
       if (bias) {
-        const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
         o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
       }
       *reinterpret_cast<float4*>(cp) =
@@ -219,7 +238,7 @@ __device__ __forceinline__ void finish_tile(const f32x16 (&acc)[BM / WM / 32][BN
                                             int64_t ldc, const float* __restrict__ bias, float slope,
                                             const uint16_t* __restrict__ dact, int64_t lddact,
                                             float* __restrict__ rowsum, float* __restrict__ ws,
-                                            float* __restrict__ ws_rowsum) {
+                                            float* __restrict__ ws_rowsum, int kz) {
   constexpr bool SPLIT = EPI == EPI_SPLIT;
   constexpr int NT = 64 * WM * WN;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -233,13 +252,39 @@ __device__ __forceinline__ void finish_tile(const f32x16 (&acc)[BM / WM / 32][BN
     if (tid < BM && m0 + tid < M) {
       float t = 0.f;
       for (int g = 0; g < NT / BM; ++g) t += lds[g * BM + tid];
-      if constexpr (SPLIT) ws_rowsum[(int64_t)blockIdx.z * M + m0 + tid] = t;
+      if constexpr (SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = t;
       else rowsum[m0 + tid] = t;
     }
     __syncthreads();
   }
+  // this thread's column quad is the same in every iteration: its bias is loaded once, and
+  // the activation operand's quads CH at a time ahead of their use (clamped addresses, no
+  // branch: inside the store loop's bounds test each load would wait out its own latency)
+  constexpr int IT = BAND * BN / 4 / NT;  // output quads per thread and pass
+  constexpr int CH = IT < 8 ? IT : 8;
+  constexpr bool DACT = EPI == EPI_DRELU || EPI == EPI_DLEAKY;
+  static_assert(NT % (BN / 4) == 0 && IT % CH == 0, "one column quad per thread");
+  const int cq = (tid % (BN / 4)) * 4;
+  const int gcl = min(n0 + cq, N - 4);
+  float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (!SPLIT) b4 = *reinterpret_cast<const float4*>(bias ? bias + gcl : g_zero4f);
+  uint2 d2[CH];
+  auto prefetch = [&](int pass, int c0) {
+    if constexpr (DACT) {
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        const int row = ((c0 + q) * NT + tid) / (BN / 4);
+        const int gr = min(m0 + pass * BAND + row, M - 1);
+        d2[q] = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gcl);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < CH; ++q) d2[q] = make_uint2(0u, 0u);
+    }
+  };
 #pragma unroll
   for (int pass = 0; pass < PASSES; ++pass) {
+    prefetch(pass, 0);
     if (PASSES == 1 || wm == pass) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -253,13 +298,17 @@ __device__ __forceinline__ void finish_tile(const f32x16 (&acc)[BM / WM / 32][BN
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < BAND * BN / 4 / NT; ++it) {
-      const int u = it * NT + tid;
-      const int row = u / (BN / 4), c = (u % (BN / 4)) * 4;
-      const int gr = m0 + pass * BAND + row, gc = n0 + c;
-      if (gr >= M || gc >= N) continue;
-      const float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
-      store4<EPI, OBF>(v, gr, gc, M, N, alpha, beta, Cv, ldc, bias, slope, dact, lddact, ws);
+    for (int c0 = 0; c0 < IT; c0 += CH) {
+      if (c0 > 0) prefetch(pass, c0);
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        const int u = (c0 + q) * NT + tid;
+        const int row = u / (BN / 4), c = cq;
+        const int gr = m0 + pass * BAND + row, gc = n0 + c;
+        if (gr >= M || gc >= N) continue;
+        const float4 v = *reinterpret_cast<const float4*>(lds + row * BN + c);
+        store4<EPI, OBF>(v, gr, gc, M, N, alpha, beta, Cv, ldc, bias, b4, slope, d2[q], ws, kz);
+      }
     }
     if (PASSES > 1) __syncthreads();
   }
@@ -271,9 +320,18 @@ __device__ __forceinline__ void finish_tile(const f32x16 (&acc)[BM / WM / 32][BN
 // the next tile only with a counted s_waitcnt vmcnt (the later tiles stay in flight) and a
 // raw s_barrier (cdna_hip_programming.md "Pipelining across barriers"); a partial last K
 // tile (fewer DMAs) switches the count to 0.
+template <int BM, int BN, int WM, int WN, int KB, int NS>
+constexpr int bf16_lds_u16() {
+  constexpr int STAGE = NS * (BM * KB + BN * KB);
+  constexpr int PASSES = 2 * BM * BN > STAGE ? WM : 1;
+  constexpr int EPI_U16 = 2 * BM * BN / PASSES;
+  return STAGE > EPI_U16 ? STAGE : EPI_U16;
+}
+
+// One output tile (tm, tn) over the K slice kz of the product: the whole workgroup's work.
 template <int BM, int BN, int WM, int WN, int KB, int NS, bool TA, bool TB, int EPI, bool OBF>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
-    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
+__device__ __forceinline__ void bf16_tile(
+    uint16_t* __restrict__ lds, int M, int N, int K, int k_per_split, int kz, int tm, int tn, float alpha,
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
     float beta, void* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
     const uint16_t* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
@@ -289,22 +347,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
   // image of the tile (in WM row bands when the whole tile does not fit)
   constexpr int STAGE = NS * (IA + IB);
   constexpr int PASSES = 2 * BM * BN > STAGE ? WM : 1;
-  constexpr int EPI_U16 = 2 * BM * BN / PASSES;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[STAGE > EPI_U16 ? STAGE : EPI_U16];
 
-  // XCD-aware tile order (as gemm.hip): blocks b, b + 8, ... share an XCD and get a
-  // contiguous run of row-major tile ids, so the tiles sharing A rows meet in one L2
-  const int b = blockIdx.x;
-  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
-  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN, l32 = lane & 31;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kz0 = blockIdx.z * k_per_split;
+  const int kz0 = kz * k_per_split;
   const int kz1 = min(K, kz0 + k_per_split);
   const bool do_rs = rowsum != nullptr && tn == 0;
   float rs = 0.f;
+  float rs8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // k-image A: 8 rows per thread
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -359,7 +410,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
       }
       const uint16_t* As = lds + cur * IA;
       const uint16_t* Bs = lds + NS * IA + cur * IB;
-      if (do_rs) rs += img_rowsum<BM, AK, NT, KB>(As, tid);
+      if (do_rs) {
+        if constexpr (AK) img_rowsum8<BM, NT, KB>(As, tid, rs8);
+        else rs += img_rowsum<BM, AK, NT, KB>(As, tid);
+      }
 #pragma unroll
       for (int s = 0; s < SS; ++s) {
         const int u = s & 1;
@@ -392,8 +446,79 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
     if constexpr (NS > 2) wait_vmcnt<0>();
     __syncthreads();  // the epilogue reuses the staging array
   }
-  finish_tile<BM, BN, WM, WN, EPI, OBF, PASSES>(acc, rs, do_rs, reinterpret_cast<float*>(lds), tid, m0, n0, M, N, alpha,
-                                beta, C, ldc, bias, slope, dact, lddact, rowsum, ws, ws_rowsum);
+  if constexpr (AK) {
+    // the k-groups' partial row sums combined in a fixed order
+    if (do_rs) {
+      constexpr int CPR = BM / 8, G = NT / CPR;
+      float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[(tid / CPR) * BM + 8 * (tid % CPR) + e] = rs8[e];
+      __syncthreads();
+      if (tid < BM && m0 + tid < M) {
+        float t = 0.f;
+        for (int g = 0; g < G; ++g) t += red[g * BM + tid];
+        if constexpr (EPI == EPI_SPLIT) ws_rowsum[(int64_t)kz * M + m0 + tid] = t;
+        else rowsum[m0 + tid] = t;
+      }
+      __syncthreads();
+    }
+  }
+  finish_tile<BM, BN, WM, WN, EPI, OBF, PASSES>(acc, rs, do_rs && !AK, reinterpret_cast<float*>(lds), tid, m0, n0,
+                                                M, N, alpha, beta, C, ldc, bias, slope, dact, lddact, rowsum, ws,
+                                                ws_rowsum, kz);
+}
+
+template <int BM, int BN, int WM, int WN, int KB, int NS, bool TA, bool TB, int EPI, bool OBF>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(
+    int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
+    const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+    float beta, void* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
+    const uint16_t* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
+    float* __restrict__ ws, float* __restrict__ ws_rowsum) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[bf16_lds_u16<BM, BN, WM, WN, KB, NS>()];
+  // XCD-aware tile order (as gemm.hip): blocks b, b + 8, ... share an XCD and get a
+  // contiguous run of row-major tile ids, so the tiles sharing A rows meet in one L2
+  const int b = blockIdx.x;
+  const int q8 = tiles / 8, r8 = tiles % 8, x8 = b % 8;
+  const int tile = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  bf16_tile<BM, BN, WM, WN, KB, NS, TA, TB, EPI, OBF>(lds, M, N, K, k_per_split, blockIdx.z, tile / tiles_n,
+                                                      tile % tiles_n, alpha, A, lda, B, ldb, beta, C, ldc, bias,
+                                                      slope, dact, lddact, rowsum, ws, ws_rowsum);
+}
+
+// Grouped split-K partials (pg_gemm_bf16_group): every part's items (tiles x K slices,
+// slice-major) end to end in one launch, XCD-aware over the items as gemm_x3's group.
+struct BPart {
+  int M, N, K, kps, tiles_n, tiles, first_item;
+  const uint16_t* A;
+  int64_t lda;
+  const uint16_t* B;
+  int64_t ldb;
+  float* ws;
+  float* ws_rowsum;
+  float* rowsum;
+};
+constexpr int kBMaxParts = 16;
+struct BGroup {
+  BPart p[kBMaxParts];
+  int n, items;
+};
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_group_kernel(BGroup g) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[bf16_lds_u16<BM, BN, WM, WN, BK, 2>()];
+  const int b = blockIdx.x;
+  const int q8 = g.items / 8, r8 = g.items % 8, x8 = b % 8;
+  const int item = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  int k = 0;
+  while (k + 1 < g.n && item >= g.p[k + 1].first_item) ++k;
+  const BPart& p = g.p[k];
+  const int local = item - p.first_item;
+  const int kz = local / p.tiles, tile = local % p.tiles;
+  bf16_tile<BM, BN, WM, WN, BK, 2, TA, TB, EPI_SPLIT, false>(lds, p.M, p.N, p.K, p.kps, kz, tile / p.tiles_n,
+                                                             tile % p.tiles_n, 1.f, p.A, p.lda, p.B, p.ldb, 0.f,
+                                                             nullptr, 0, nullptr, 0.f, nullptr, 0, p.rowsum, p.ws,
+                                                             p.ws_rowsum);
 }
 
 // ---- 256 x 256 ping-pong kernel for A[m][k] x B[n][k]^T (both operands row images) -----
@@ -558,10 +683,24 @@ __global__ __launch_bounds__(512) void gemm_bf16_pp_kernel(
   }
   __syncthreads();  // every wave past its last fragment read: the epilogue reuses the LDS
 
-  // epilogue in four 64-row bands (band p = wave row p / 2, A half p % 2)
+  // epilogue in four 64-row bands (band p = wave row p / 2, A half p % 2); this thread's
+  // column quad is the same in every iteration (bias loaded once, the activation operand's
+  // 8 quads of a band loaded before the band is staged)
   float* img = reinterpret_cast<float*>(lds);
+  constexpr bool DACT = EPI == EPI_DRELU || EPI == EPI_DLEAKY;
+  const int gcl = min(n0 + (tid & 63) * 4, N - 4);
+  const float4 b4 = *reinterpret_cast<const float4*>(bias ? bias + gcl : g_zero4f);
+  uint2 d2[64 * 64 / 512];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int it = 0; it < 64 * 64 / 512; ++it) {
+      d2[it] = make_uint2(0u, 0u);
+      if constexpr (DACT) {
+        const int gr = min(m0 + p * 64 + ((it * 512 + tid) >> 6), M - 1);
+        d2[it] = *reinterpret_cast<const uint2*>(dact + (int64_t)gr * lddact + gcl);
+      }
+    }
     if (wr == (p >> 1)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -579,7 +718,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_pp_kernel(
       const int gr = m0 + p * 64 + row, gc = n0 + c;
       if (gr < M && gc < N)
         store4<EPI, OBF>(*reinterpret_cast<const float4*>(img + row * EPS + c), gr, gc, M, N, alpha, beta, C,
-                         ldc, bias, slope, dact, lddact, nullptr);
+                         ldc, bias, b4, slope, d2[it], nullptr, 0);
     }
     __syncthreads();
   }
@@ -812,6 +951,165 @@ int pg_gemm_bf16(int transa, int transb, int64_t M, int64_t N, int64_t K, float 
   if (e != hipSuccess)
     return pg::set_error((int)e, "pg_gemm_bf16: launch failed: %s", hipGetErrorString(e));
   return pg::ok();
+}
+
+}  // extern "C"
+
+namespace {
+
+// The bf16 group (pg_gemm_bf16_group): 256 x 256 tiles, one workgroup per CU. A part joins
+// when its tiles waste at most 4x its area; one K-slice count for the members, the one
+// (<= 64, slices >= 3 BK) whose items fill whole rounds of 256 workgroups best (the
+// smallest such count within 1 %).
+struct BPlan {
+  bool in[kBMaxParts];
+  int split[kBMaxParts];
+  int kps[kBMaxParts];
+  size_t off[kBMaxParts + 1];
+};
+
+inline bool bgroup_member(const pg_gemm_part_t& q) {
+  const int64_t pm = (q.M + 255) / 256 * 256, pn = (q.N + 255) / 256 * 256;
+  return q.M > 0 && q.N > 0 && pm * pn <= 4 * q.M * q.N;
+}
+
+inline void bgroup_plan(const pg_gemm_part_t* parts, int n, BPlan& g) {
+  int64_t T = 0, kmin = INT64_MAX;
+  for (int p = 0; p < n; ++p) {
+    g.in[p] = bgroup_member(parts[p]);
+    if (!g.in[p]) continue;
+    T += ((parts[p].M + 255) / 256) * ((parts[p].N + 255) / 256);
+    kmin = std::min<int64_t>(kmin, parts[p].K);
+  }
+  int best = 1;
+  if (T > 0) {
+    double bf = -1.0;
+    const int smax = (int)std::max<int64_t>(1, std::min<int64_t>(64, kmin / (3 * BK)));
+    for (int sc = 1; sc <= smax; ++sc) {
+      const int64_t items = T * sc, rounds = (items + 255) / 256;
+      const double fill = (double)items / (double)(rounds * 256);
+      if (fill > bf + 0.01) bf = fill, best = sc;
+    }
+  }
+  size_t off = 0;
+  for (int p = 0; p < n; ++p) {
+    const pg_gemm_part_t& q = parts[p];
+    g.split[p] = 1;
+    g.kps[p] = BK;
+    g.off[p] = off;
+    if (!g.in[p]) continue;
+    int64_t sp = std::max<int64_t>(1, std::min<int64_t>(best, q.K / (3 * BK)));
+    int64_t kps = (q.K + sp - 1) / sp;
+    kps = std::max<int64_t>(BK, (kps + BK - 1) / BK * BK);
+    sp = std::max<int64_t>(1, (q.K + kps - 1) / kps);
+    g.split[p] = (int)sp;
+    g.kps[p] = (int)kps;
+    off += ((size_t)sp * (size_t)q.M * (size_t)(q.N + 1) * 4 + 255) / 256 * 256;
+  }
+  g.off[n] = off;
+}
+
+inline bool bpart_layout_ok(const pg_gemm_part_t& q) {
+  const int64_t ext_a = q.transa ? q.M : q.K, ext_b = q.transb ? q.K : q.N;
+  return al16(q.A) && al16(q.B) && q.lda % 8 == 0 && q.ldb % 8 == 0 && ext_a % 8 == 0 && ext_b % 8 == 0 &&
+         q.N % 4 == 0 && !(q.transa && q.M < 8) && !(!q.transb && q.N < 8);
+}
+
+int bpart_alone(const pg_gemm_part_t& q, void* ws, size_t ws_bytes, pg_stream_t stream) {
+  const pg_gemm_epilogue_t ep{nullptr, PG_ACT_NONE, 0.f, nullptr, 0, q.rowsum};
+  return pg_gemm_bf16(q.transa, q.transb, q.M, q.N, q.K, 1.f, q.A, q.lda, q.B, q.ldb, q.beta, q.C, q.ldc,
+                      PG_DTYPE_F32, &ep, pg_gemm_bf16_split_k(q.M, q.N, q.K), ws, ws_bytes, stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t pg_gemm_bf16_group_workspace(const pg_gemm_part_t* parts, int n) {
+  if (n <= 0 || n > kBMaxParts || !parts) return 0;
+  BPlan g;
+  bgroup_plan(parts, n, g);
+  size_t need = g.off[n];
+  for (int p = 0; p < n; ++p) {
+    const pg_gemm_part_t& q = parts[p];
+    need = std::max(need, pg_gemm_bf16_workspace(q.M, q.N, q.K, pg_gemm_bf16_split_k(q.M, q.N, q.K)));
+  }
+  return std::max<size_t>(need, 256);
+}
+
+int pg_gemm_bf16_group(const pg_gemm_part_t* parts, int n, void* ws, size_t ws_bytes, pg_stream_t stream) {
+  if (n < 0 || n > kBMaxParts || (n > 0 && !parts))
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_bf16_group: 0..%d parts", kBMaxParts);
+  if (n == 0) return pg::ok();
+  for (int p = 0; p < n; ++p) {
+    const pg_gemm_part_t& q = parts[p];
+    if (q.M < 0 || q.N < 0 || q.K < 0 || q.M > INT32_MAX || q.N > INT32_MAX || q.K > INT32_MAX || q.ldc < q.N ||
+        (q.transa ? q.lda < q.M : q.lda < q.K) || (q.transb ? q.ldb < q.K : q.ldb < q.N) ||
+        (q.beta != 0.f && q.beta != 1.f))
+      return pg::set_error(PG_ERR_INVALID, "pg_gemm_bf16_group: bad part %d", p);
+  }
+  if (ws_bytes < pg_gemm_bf16_group_workspace(parts, n) || !ws || !al16(ws))
+    return pg::set_error(PG_ERR_WORKSPACE, "pg_gemm_bf16_group: workspace too small or misaligned");
+  BPlan g;
+  bgroup_plan(parts, n, g);
+  int first = -1;
+  bool grouped = true;
+  for (int p = 0; p < n; ++p) {
+    if (!g.in[p]) continue;
+    if (first < 0) first = p;
+    grouped = grouped && bpart_layout_ok(parts[p]) && parts[p].transa == parts[first].transa &&
+              parts[p].transb == parts[first].transb;
+  }
+  if (first < 0 || !grouped) {
+    for (int p = 0; p < n; ++p) {
+      const int rc = bpart_alone(parts[p], ws, ws_bytes, stream);
+      if (rc != PG_OK) return rc;
+    }
+    return pg::ok();
+  }
+  BGroup bg{};
+  pg_splitk_job_t jobs[kBMaxParts];
+  int items = 0, nj = 0;
+  for (int p = 0; p < n; ++p) {
+    if (!g.in[p]) continue;
+    const pg_gemm_part_t& q = parts[p];
+    float* w = (float*)((char*)ws + g.off[p]);
+    BPart& x = bg.p[nj];
+    x.M = (int)q.M; x.N = (int)q.N; x.K = (int)q.K; x.kps = g.kps[p];
+    x.tiles_n = (int)((q.N + 255) / 256);
+    x.tiles = x.tiles_n * (int)((q.M + 255) / 256);
+    x.first_item = items;
+    x.A = (const uint16_t*)q.A; x.lda = q.lda; x.B = (const uint16_t*)q.B; x.ldb = q.ldb;
+    x.ws = w;
+    x.ws_rowsum = w + (int64_t)g.split[p] * q.M * q.N;
+    x.rowsum = q.rowsum;
+    items += x.tiles * g.split[p];
+    pg_splitk_job_t& j = jobs[nj];
+    j.ws = w; j.split_k = g.split[p]; j.M = q.M; j.N = q.N;
+    j.alpha = 1.f; j.beta = q.beta; j.C = q.C; j.ldc = q.ldc; j.rowsum = q.rowsum;
+    ++nj;
+  }
+  bg.n = nj;
+  bg.items = items;
+  const bool ta = parts[first].transa != 0, tb = parts[first].transb != 0;
+  const dim3 grid((unsigned)items), block(64 * PG_BF16_WM * PG_BF16_WN);
+  hipStream_t st = (hipStream_t)stream;
+#define PG_G(TA_, TB_) \
+  hipLaunchKernelGGL((gemm_bf16_group_kernel<256, 256, PG_BF16_WM, PG_BF16_WN, TA_, TB_>), grid, block, 0, st, bg)
+  if (ta && !tb) PG_G(true, false);
+  else if (!ta && !tb) PG_G(false, false);
+  else if (!ta && tb) PG_G(false, true);
+  else PG_G(true, true);
+#undef PG_G
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return pg::set_error((int)e, "pg_gemm_bf16_group: launch failed: %s", hipGetErrorString(e));
+  int rc = pg_gemm_splitk_reduce_batch(jobs, nj, stream);
+  // the parts a 256 x 256 tile would waste, after the combine on the same stream (so they
+  // may reuse the workspace)
+  for (int p = 0; p < n && rc == PG_OK; ++p)
+    if (!g.in[p]) rc = bpart_alone(parts[p], ws, ws_bytes, stream);
+  return rc;
 }
 
 }  // extern "C"

@@ -169,8 +169,32 @@ __device__ __forceinline__ void x3_store(const f32x16 (&acc)[BM / 64][BN / 64], 
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
   constexpr int BAND = BM / PASSES;
+  constexpr int IT = BAND * BN / 4 / NT;  // output quads per thread and pass
+  constexpr int CH = IT < 8 ? IT : 8;     // quads whose operand loads are in flight together
+  constexpr bool DACT = EPI == EPI_DRELU || EPI == EPI_DLEAKY;
+  static_assert(NT % (BN / 4) == 0 && IT % CH == 0, "one column quad per thread");
+  // this thread's column quad is the same in every iteration: its bias is loaded once, and
+  // the activation operand's quads are loaded CH at a time ahead of their use (clamped
+  // addresses, no branch: behind the store loop's bounds test the loads would run one at a
+  // time, each waiting out its latency)
+  const int cq = (tid % (BN / 4)) * 4;
+  const int gcl = min(n0 + cq, N - 4);
+  float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (!SPLIT) b4 = *reinterpret_cast<const float4*>(bias ? bias + gcl : g_zero4);
+  float4 y4[CH];
+  auto prefetch = [&](int pass, int c0) {
+    if constexpr (DACT) {
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        const int row = ((c0 + q) * NT + tid) / (BN / 4);
+        const int gr = min(m0 + pass * BAND + row, M - 1);
+        y4[q] = *reinterpret_cast<const float4*>(dact + (int64_t)gr * lddact + gcl);
+      }
+    }
+  };
 #pragma unroll
   for (int pass = 0; pass < PASSES; ++pass) {
+    prefetch(pass, 0);
     if (PASSES == 1 || wm == pass) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -184,34 +208,36 @@ __device__ __forceinline__ void x3_store(const f32x16 (&acc)[BM / 64][BN / 64], 
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < BAND * BN / 4 / NT; ++it) {
-      const int u = it * NT + tid;
-      const int row = u / (BN / 4), c = (u % (BN / 4)) * 4;
-      const int gr = m0 + pass * BAND + row, gc = n0 + c;
-      if (gr >= M || gc >= N) continue;
-      const float4 v = *reinterpret_cast<const float4*>(img + row * BN + c);
-      if constexpr (SPLIT) {
-        *reinterpret_cast<float4*>(ws + ((int64_t)kz * M + gr) * N + gc) = v;
-      } else {
-        float* cp = C + (int64_t)gr * ldc + gc;
-        float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
-        if (beta != 0.f) {
-          const float4 c4 = *reinterpret_cast<const float4*>(cp);
-          o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
-          o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
+    for (int c0 = 0; c0 < IT; c0 += CH) {
+      if (c0 > 0) prefetch(pass, c0);
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        const int u = (c0 + q) * NT + tid;
+        const int row = u / (BN / 4), c = cq;
+        const int gr = m0 + pass * BAND + row, gc = n0 + c;
+        if (gr >= M || gc >= N) continue;
+        const float4 v = *reinterpret_cast<const float4*>(img + row * BN + c);
+        if constexpr (SPLIT) {
+          *reinterpret_cast<float4*>(ws + ((int64_t)kz * M + gr) * N + gc) = v;
+        } else {
+          float* cp = C + (int64_t)gr * ldc + gc;
+          float o[4] = {alpha * v.x, alpha * v.y, alpha * v.z, alpha * v.w};
+          if (beta != 0.f) {
+            const float4 c4 = *reinterpret_cast<const float4*>(cp);
+            o[0] = o[0] + beta * c4.x; o[1] = o[1] + beta * c4.y;
+            o[2] = o[2] + beta * c4.z; o[3] = o[3] + beta * c4.w;
+          }
+          if (bias) {  // (no add without a bias: -0 stays -0)
+            o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
+          }
+          float y[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (DACT) {
+            y[0] = y4[q].x; y[1] = y4[q].y; y[2] = y4[q].z; y[3] = y4[q].w;
+          }
+          *reinterpret_cast<float4*>(cp) =
+              make_float4(epi_apply<EPI>(o[0], y[0], slope), epi_apply<EPI>(o[1], y[1], slope),
+                          epi_apply<EPI>(o[2], y[2], slope), epi_apply<EPI>(o[3], y[3], slope));
         }
-        if (bias) {
-          const float4 b4 = *reinterpret_cast<const float4*>(bias + gc);
-          o[0] = o[0] + b4.x; o[1] = o[1] + b4.y; o[2] = o[2] + b4.z; o[3] = o[3] + b4.w;
-        }
-        float y[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (EPI == EPI_DRELU || EPI == EPI_DLEAKY) {
-          const float4 d4 = *reinterpret_cast<const float4*>(dact + (int64_t)gr * lddact + gc);
-          y[0] = d4.x; y[1] = d4.y; y[2] = d4.z; y[3] = d4.w;
-        }
-        *reinterpret_cast<float4*>(cp) =
-            make_float4(epi_apply<EPI>(o[0], y[0], slope), epi_apply<EPI>(o[1], y[1], slope),
-                        epi_apply<EPI>(o[2], y[2], slope), epi_apply<EPI>(o[3], y[3], slope));
       }
     }
     if (PASSES > 1) __syncthreads();

@@ -69,7 +69,7 @@ _sz = ctypes.c_size_t
 _vp = ctypes.c_void_p
 _csr = ctypes.POINTER(PgCsr)
 class PgGemmPart(ctypes.Structure):
-    """pg_gemm_part_t (include/plagnn.h)."""
+    """pg_gemm_part_t (include/plagnn.h): A, B f32 or bf16 bits, C f32."""
 
     _fields_ = [
         ("transa", ctypes.c_int32),
@@ -122,6 +122,8 @@ SIGNATURES = {
     "pg_gemm_splitk_reduce_batch": (_i, [ctypes.POINTER(PgSplitkJob), _i, _vp]),
     "pg_gemm_f32_group_workspace": (_sz, [ctypes.POINTER(PgGemmPart), _i]),
     "pg_gemm_f32_group": (_i, [ctypes.POINTER(PgGemmPart), _i, _vp, _sz, _vp]),
+    "pg_gemm_bf16_group_workspace": (_sz, [ctypes.POINTER(PgGemmPart), _i]),
+    "pg_gemm_bf16_group": (_i, [ctypes.POINTER(PgGemmPart), _i, _vp, _sz, _vp]),
     "pg_csr_spmm_f64": (_i, [_i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp]),
     "pg_spmm_max_bwd_scatter": (_i, [_csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp]),
     "pg_spmm_sum_workspace": (_sz, [_csr, _i64]),
@@ -187,6 +189,8 @@ def lib():
                 "(make -C pla-gnn_amd, or __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("PLAGNN_LIB") and not hasattr(L, name):
+                continue  # an older A/B build (scripts/*_ab.sh) without this entry point
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -128,6 +128,15 @@ class TrainEngineBF16(TrainEngine):
             sk = int(L.pg_gemm_bf16_split_k(M_, N_, K_))
             self._gemm_plans[(M_, N_, K_)] = sk
             need = max(need, L.pg_gemm_bf16_workspace(M_, N_, K_, sk))
+        self._parts = []
+        if self.GROUP_WGRAD:
+            # the grouped weight gradients' slabs: sized from the shapes alone
+            shapes = self._wgrad_shapes()
+            parts = (_lib.PgGemmPart * len(shapes))()
+            for i, (M_, N_, K_) in enumerate(shapes):
+                parts[i].transa, parts[i].transb, parts[i].M, parts[i].N, parts[i].K = 1, 0, M_, N_, K_
+            self.gws = torch.empty(int(L.pg_gemm_bf16_group_workspace(parts, len(shapes))), dtype=torch.uint8,
+                                   device=dev)
         # the fused head (pg_mlp_head, run by forward()) and the standalone loss kernel
         need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
@@ -141,6 +150,14 @@ class TrainEngineBF16(TrainEngine):
         N = B.shape[0] if transb else B.shape[1]
         self._rec_gemm(A, B, C, M, N, K, beta, dact)
         obf = C.dtype == torch.bfloat16
+        if (self.GROUP_WGRAD and not obf and bias is None and act == NONE and dact is None
+                and (M, N, K) in self._gemm_plans):
+            q = _lib.PgGemmPart()
+            q.transa, q.transb, q.M, q.N, q.K = int(transa), int(transb), M, N, K
+            q.A, q.lda, q.B, q.ldb = ptr(A), A.stride(0), ptr(B), B.stride(0)
+            q.beta, q.C, q.ldc, q.rowsum = beta, ptr(C), C.stride(0), ptr(rowsum)
+            self._parts.append((q, 2.0 * M * N * K))
+            return
         sk = 1
         if not obf and bias is None and act == NONE and dact is None:
             sk = self._gemm_plans.get((M, N, K), 1)
@@ -205,6 +222,16 @@ class TrainEngineBF16(TrainEngine):
                 else:
                     self._gemm(DYP, W[p + "Wstack"], self.DYP[l - 1][:, :Fi], act=LEAKY, dact=HM[:, :Fi],
                                tag=f"gemm.dgrad.stack.l{l + 1}")
+        self._reduce_deferred()
+
+    def _reduce_deferred(self) -> None:
+        """Every weight gradient of the step as one grouped split-K launch + one combine
+        (pg_gemm_bf16_group): they only feed Adam, so they all wait for the backward's end."""
+        parts, self._parts = self._parts, []
+        if parts:
+            arr = (_lib.PgGemmPart * len(parts))(*[q for q, _ in parts])
+            with self._t("gemm.wgrad.group", sum(w for _, w in parts)):
+                self._call("pg_gemm_bf16_group", arr, len(parts), ptr(self.gws), self.gws.numel(), self._s())
 
     def adam(self) -> None:
         super().adam()

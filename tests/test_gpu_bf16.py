@@ -100,6 +100,50 @@ def test_gemm_bf16_rowsum_and_split_k():
     assert torch.equal(a, b)  # deterministic
 
 
+@pytest.mark.parametrize("case", ["grouped", "mixed"])
+def test_gemm_bf16_group(case):
+    """pg_gemm_bf16_group on the cfg5 step's weight-gradient shapes (K = nodes, both
+    operands k images, row sums; liner2's 16 x 104 product runs alone, a 256 x 256 tile
+    would waste 39x its area; one part with beta = 1): within the f32-accumulation bound
+    of a float64 product of the same bf16 values, deterministic. `mixed` (one part with B
+    stored [n][k]) runs every part one by one as pg_gemm_bf16."""
+    from plagnn import _lib
+    from plagnn._lib import call, ptr
+
+    Nn = 40000
+    shapes = [(512, 1024), (504, 504), (512, 1024), (512, 512), (104, 512), (16, 104)]
+    parts = (_lib.PgGemmPart * len(shapes))()
+    keep = []
+    for i, (M, N) in enumerate(shapes):
+        tb = case == "mixed" and i == 2
+        A = _bf((Nn, M), 40 + i)
+        B = _bf((N, Nn) if tb else (Nn, N), 60 + i)
+        C = torch.randn(M, N, device=DEV)
+        beta = 1.0 if i == 1 else 0.0
+        rs = torch.empty(M, device=DEV)
+        q = parts[i]
+        q.transa, q.transb, q.M, q.N, q.K = 1, int(tb), M, N, Nn
+        q.A, q.lda, q.B, q.ldb = ptr(A), A.stride(0), ptr(B), B.stride(0)
+        q.beta, q.C, q.ldc, q.rowsum = beta, ptr(C), C.stride(0), ptr(rs)
+        keep.append((A, B, tb, C, C.clone(), rs, beta))
+    n = len(shapes)
+    ws = torch.empty(int(_lib.lib().pg_gemm_bf16_group_workspace(parts, n)), dtype=torch.uint8, device=DEV)
+    st = _lib.stream_handle(torch.device(DEV))
+    call("pg_gemm_bf16_group", parts, n, ptr(ws), ws.numel(), st)
+    first = [(C.clone(), rs.clone()) for (_, _, _, C, _, rs, _) in keep]
+    for (_, _, _, C, C0, _, _) in keep:
+        C.copy_(C0)
+    call("pg_gemm_bf16_group", parts, n, ptr(ws), ws.numel(), st)
+    torch.cuda.synchronize()
+    for (A, B, tb, C, C0, rs, beta), (c1, r1) in zip(keep, first):
+        assert torch.equal(C, c1) and torch.equal(rs, r1)
+        ref, mag = _ref(A, B, True, tb)
+        assert bool(((C.double() - ref - beta * C0.double()).abs()
+                     <= 2e-6 * np.sqrt(Nn) * mag + 1e-6 * beta * C0.double().abs()).all())
+        a64 = A.double()
+        assert bool(((rs.double() - a64.sum(0)).abs() <= 2e-6 * np.sqrt(Nn) * a64.abs().sum(0)).all())
+
+
 @pytest.mark.parametrize("ta,tb", [(True, False), (False, False), (True, True)])
 def test_gemm_bf16_256_tiles_rowsum_unsplit(ta, tb):
     """256 x 256 tiles without split-K (>= 256 tiles) in the k-image transpositions (the
