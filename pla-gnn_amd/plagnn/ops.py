@@ -234,6 +234,30 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
     return out
 
 
+def gemm_group(parts) -> None:
+    """Several split-K products in one launch + one combine (pg_gemm_f32_group): each part
+    (A, B, C, transa, transb, beta, rowsum) computes C = op(A) op(B) (+ C when beta = 1) and
+    rowsum = the row sums of op(A) when given. The weight gradients of a layer's backward."""
+    if not parts:
+        return
+    dev = parts[0][0].device
+    if dev.type != "cuda":
+        for A, B, C, ta, tb, beta, rs in parts:
+            gemm(A, B, transa=ta, transb=tb, out=C, beta=beta, rowsum=rs)
+        return
+    arr = (_lib.PgGemmPart * len(parts))()
+    for q, (A, B, C, ta, tb, beta, rs) in zip(arr, parts):
+        q.transa, q.transb = int(ta), int(tb)
+        q.M = A.shape[1] if ta else A.shape[0]
+        q.K = A.shape[0] if ta else A.shape[1]
+        q.N = B.shape[0] if tb else B.shape[1]
+        q.A, q.lda, q.B, q.ldb = ptr(A), _ld(A), ptr(B), _ld(B)
+        q.beta, q.C, q.ldc, q.rowsum = beta, ptr(C), _ld(C), ptr(rs)
+    ws_n = _lib.lib().pg_gemm_f32_group_workspace(arr, len(parts))
+    ws = _workspace(ws_n, dev)
+    call("pg_gemm_f32_group", arr, len(parts), ptr(ws), ws_n, _stream(parts[0][0]))
+
+
 def gemm_bf16(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = False,
               out: Optional[torch.Tensor] = None, out_dtype=torch.float32, alpha: float = 1.0,
               beta: float = 0.0, bias: Optional[torch.Tensor] = None, act: int = _lib.PG_ACT_NONE,
@@ -495,8 +519,10 @@ class SagePool(torch.autograd.Function):
         dY = DYP[:, :Fo]
         d_b = torch.empty(Fo, dtype=torch.float32, device=dY.device) if (need_b and ctx.has_bias) else None
         d_ws = d_wn = None
+        wgrads = []  # the layer's weight gradients, one grouped launch after the max backward
         if need_ws or need_wn:
-            d_wcat = gemm(dY, HM, transa=True, rowsum=d_b)  # [d Wself | d Wneigh] in one product
+            d_wcat = torch.empty(Fo, 2 * Fp, dtype=torch.float32, device=dY.device)
+            wgrads.append((dY, HM, d_wcat, True, False, 0.0, d_b))  # [d Wself | d Wneigh]
             d_ws, d_wn = d_wcat[:, :Fin], d_wcat[:, Fp:Fp + Fin]
         elif d_b is not None:
             d_b = col_sum(dY)
@@ -507,9 +533,12 @@ class SagePool(torch.autograd.Function):
         d_bp_p = torch.empty(Fp, dtype=torch.float32, device=dY.device) if need_bp else None
         d_wp = d_bp = None
         if need_wp:
-            d_wp = gemm(dP, HM[:, :Fp], transa=True, rowsum=d_bp_p)[:Fin, :Fin]
+            d_wp_p = torch.empty(Fp, Fp, dtype=torch.float32, device=dY.device)
+            wgrads.append((dP, HM[:, :Fp], d_wp_p, True, False, 0.0, d_bp_p))
+            d_wp = d_wp_p[:Fin, :Fin]
         elif d_bp_p is not None:
             d_bp_p = col_sum(dP)
+        gemm_group(wgrads)
         if d_bp_p is not None:
             d_bp = d_bp_p[:Fin]
         d_h = None
