@@ -983,7 +983,8 @@ struct GroupPlan {
 
 inline void group_plan(const pg_gemm_part_t* parts, int n, GroupPlan& g) {
   int64_t tiles = 0;
-  for (int p = 0; p < n; ++p) tiles += ((parts[p].M + 127) / 128) * ((parts[p].N + 127) / 128);
+  for (int p = 0; p < n; ++p)
+    tiles += ((parts[p].M + kX3GroupBM - 1) / kX3GroupBM) * ((parts[p].N + kX3GroupBN - 1) / kX3GroupBN);
   const int64_t s = std::max<int64_t>(1, PG_X3_GROUP_TARGET / std::max<int64_t>(1, tiles));
   size_t off = 0;
   for (int p = 0; p < n; ++p) {
@@ -1061,8 +1062,8 @@ int pg_gemm_f32_group(const pg_gemm_part_t* parts, int n, void* ws, size_t ws_by
     float* w = (float*)((char*)ws + g.off[p]);
     X3Part& x = xg.p[nj];
     x.M = (int)q.M; x.N = (int)q.N; x.K = (int)q.K; x.kps = g.kps[p];
-    x.tiles_n = (int)((q.N + 127) / 128);
-    x.tiles = x.tiles_n * (int)((q.M + 127) / 128);
+    x.tiles_n = (int)((q.N + kX3GroupBN - 1) / kX3GroupBN);
+    x.tiles = x.tiles_n * (int)((q.M + kX3GroupBM - 1) / kX3GroupBM);
     x.first_item = items;
     x.A = (const float*)q.A; x.lda = q.lda; x.B = (const float*)q.B; x.ldb = q.ldb;
     x.ws = w;

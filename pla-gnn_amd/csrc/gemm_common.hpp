@@ -149,7 +149,12 @@ struct X3Args {
 };
 int gemm_x3_launch(const X3Args& a, hipStream_t st);
 
-// Grouped split-K partials (pg_gemm_f32_group): 128 x 128 tiles, one (ta, tb) for the group.
+// Grouped split-K partials (pg_gemm_f32_group): one tile shape (128 x 128 measured best) and
+// one (ta, tb) for the group.
+#ifndef PG_X3_GROUP_TILE
+#define PG_X3_GROUP_TILE 128128  // variant builds: BM * 1000 + BN
+#endif
+constexpr int kX3GroupBM = PG_X3_GROUP_TILE / 1000, kX3GroupBN = PG_X3_GROUP_TILE % 1000;
 struct X3Part {
   int M, N, K, kps, tiles_n, tiles, first_item;
   const float* A;

@@ -522,7 +522,8 @@ namespace pg_gemm {
 
 int gemm_x3_group_launch(const X3Group& g, bool ta, bool tb, hipStream_t st) {
   const dim3 grid((unsigned)g.items), block(NT);
-#define PG_G(TA_, TB_) hipLaunchKernelGGL((gemm_x3_group_kernel<128, 128, TA_, TB_>), grid, block, 0, st, g)
+#define PG_G(TA_, TB_) \
+  hipLaunchKernelGGL((gemm_x3_group_kernel<kX3GroupBM, kX3GroupBN, TA_, TB_>), grid, block, 0, st, g)
   if (ta && !tb) PG_G(true, false);
   else if (!ta && !tb) PG_G(false, false);
   else if (!ta && tb) PG_G(false, true);
