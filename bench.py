@@ -185,10 +185,12 @@ def dropin_leg(wl, dims, dev, steps: int, warmup: int):
 
 def dropin_device_time(wl, dims, dev, reps: int = 20) -> float:
     """The device time of the shim model's forward + backward alone (without the reference's
-    multi_loss host loop and Adam): model(g, features).backward(G) with a fixed upstream
-    gradient G, issued `reps` times back to back between two HIP events after a warm-up.
-    The host issues one iteration in well under the device time, so the queue stays full
-    and the events see device time."""
+    multi_loss host loop and Adam): zero_grad + model(g, features).backward(G) with a fixed
+    upstream gradient G, issued `reps` times back to back between two HIP events after a
+    warm-up. zero_grad as the reference's epoch does it (code/train.py:197, optimizer.
+    zero_grad() on the installed torch: gradients set to None, so backward writes them
+    instead of adding into the previous ones). The host issues one iteration in well under
+    the device time, so the queue stays full and the events see device time."""
     import dgl
     from plagnn.model import GNN
 
@@ -199,11 +201,13 @@ def dropin_device_time(wl, dims, dev, reps: int = 20) -> float:
     model = GNN(dims).to(dev)
     dlog = torch.randn(wl.n, dims[-1], device=dev) * 1e-3
     for _ in range(5):
+        model.zero_grad()
         model(g, features).backward(dlog)
     torch.cuda.synchronize(dev)
     ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ea.record()
     for _ in range(reps):
+        model.zero_grad()
         model(g, features).backward(dlog)
     eb.record()
     torch.cuda.synchronize(dev)
