@@ -408,20 +408,27 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
 // in-row position p, giving
 //   rec[v F + i]    = {w * dout[v,f], f}, grouped by p (any order inside a group; 8-B
 //                     records, or 4-B {bf16 dout, f} for bf16 storage without weights),
-//   glist[s]        = {v F + start_p, count_p} for the edge at in-CSR slot s = ptr[v] + p
-//                     (a row's descriptors are contiguous: coalesced stores).
+//   glist[s]        = start_p | count_p << 16 for the edge at in-CSR slot s = ptr[v] + p:
+//                     4 B, the start relative to the row's run v F (a row's descriptors are
+//                     contiguous: coalesced stores).
 // Rows of in-degree <= kPackWaveMax: one wave per row (wave-private LDS histogram, wave
 // scan, LDS-atomic placement); longer rows: one workgroup per row (block histogram, or a
 // bitonic sort of (p << 16 | f) keys past kHistMax entries).
 // Pass 2 (pull), one wave per source row item: for each out-edge of u, ascending
 // destination v (the transposed CSR order), read its descriptor glist[tslot[t]] and add
 // its records into an LDS row accumulator (max_bwd_pull_kernel). Traffic per edge: its
-// 4-B slot, one 8-B descriptor and one short contiguous run of records (~F/deg entries).
+// 4-B slot and destination (coalesced), one 4-B descriptor (random; 8 B {v F + start,
+// count} before: twice the footprint for the caches to hold) and one short contiguous run
+// of records (~F/deg entries).
 // (Descriptors stored at the transposed index instead, read coalesced but written
 // scattered by the pack: pull 35.6 vs 43.5 us, pack 28.3 vs 15.9 us at F = 256, no gain.
 // A source-ordered record layout, DESIGN.md §7, measured slower still.)
 constexpr int kHistMax = 4096;
-constexpr int kGroupMaxF = 1024;
+constexpr int kGroupMaxF = 1024;  // (starts and counts <= F fit the descriptor's 16-bit halves)
+
+__device__ __forceinline__ uint32_t desc_make(int start, int count) {
+  return (uint32_t)start | ((uint32_t)count << 16);
+}
 #ifndef PG_BWD_DIRECT
 #define PG_BWD_DIRECT 0
 #endif
@@ -510,7 +517,7 @@ template <typename A, typename T, typename R>
 __device__ __forceinline__ void pack_short_row(
     int v, int wave, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, int2* __restrict__ glist,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist,
     int* __restrict__ lds) {
   constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
   const int lane = lane_id();
@@ -570,7 +577,7 @@ __device__ __forceinline__ void pack_short_row(
     const int p = lane * B + q;
     if (q < B && p < deg) {
       hist[p] = run;
-      glist[ei[q]] = make_int2(vF + run, c[q]);
+      glist[ei[q]] = desc_make(run, c[q]);
       run += c[q];
     }
   }
@@ -598,7 +605,7 @@ template <int NV, typename A, typename T, typename R>
 __device__ __forceinline__ void pack_short_row_v(
     int v, int wave, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, int2* __restrict__ glist,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist,
     int* __restrict__ lds) {
   const int lane = lane_id();
   const int rs = ptr[v];
@@ -667,7 +674,7 @@ __device__ __forceinline__ void pack_short_row_v(
     const int p = lane * B + q;
     if (q < B && p < deg) {
       hist[p] = run;
-      glist[ei[q]] = make_int2(vF + run, cq[q]);
+      glist[ei[q]] = desc_make(run, cq[q]);
       run += cq[q];
     }
   }
@@ -704,7 +711,7 @@ template <typename A, typename T, typename R>
 __device__ __forceinline__ void pack_long_row(
     int v, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, int2* __restrict__ glist,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist,
     int* __restrict__ lds) {
   int* hist = lds;
   uint16_t* feats = reinterpret_cast<uint16_t*>(lds + kHistMax + 8);
@@ -757,7 +764,7 @@ __device__ __forceinline__ void pack_long_row(
         if (p < deg) {
           const int st = hist[p];
           const int en = p + 1 < deg ? hist[p + 1] : total;
-          glist[e[j]] = make_int2((int)(vF + st), en - st);
+          glist[e[j]] = desc_make(st, en - st);
         }
       }
     }
@@ -809,7 +816,7 @@ __device__ __forceinline__ void pack_long_row(
     for (int p = threadIdx.x; p < deg; p += kBlock) {
       const int st = lower((uint32_t)p << 16);
       const int en = lower((uint32_t)(p + 1) << 16);
-      glist[rs + p] = make_int2((int)(vF + st), en - st);
+      glist[rs + p] = desc_make(st, en - st);
     }
     if (threadIdx.x == 0) wsum[0] = lower(0xFFFFFFFFu);
     __syncthreads();
@@ -837,7 +844,7 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F,
     const T* __restrict__ dout, int64_t ldd, const T* __restrict__ fout, int64_t ldf,
-    const float* __restrict__ ew, R gp, int2* __restrict__ glist) {
+    const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist) {
   constexpr int kLds = NV > 0 && kWavesPerBlock * pack_wave_ints<NV>() > kPackLds
                            ? kWavesPerBlock * pack_wave_ints<NV>() : kPackLds;
   __shared__ __attribute__((aligned(16))) int lds[kLds];
@@ -875,8 +882,9 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
 template <typename T, typename R>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
-    const int2* __restrict__ glist, R gp, int F, const T* __restrict__ mask, int64_t ldm,
-    T* __restrict__ dx, int64_t ldx, float* __restrict__ ws, int64_t ldw) {
+    const int32_t* __restrict__ tdst, const uint32_t* __restrict__ glist, R gp, int F,
+    const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx, float* __restrict__ ws,
+    int64_t ldw) {
   constexpr int U = PG_PULL_U;
   __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
   const int wave = wave_id_uniform();
@@ -887,20 +895,23 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
   const int lane = lane_id();
   for (int f = lane; f < F; f += kWave) acc[f] = 0.f;
-  // descriptors one window ahead, their in-CSR slots two windows ahead (an item with no
-  // out-edges reads nothing)
+  // descriptors (and the destinations' record bases v F) one window ahead, their in-CSR
+  // slots two windows ahead (an item with no out-edges reads nothing)
   auto tl_of = [&](int tw) { return tw + min(lane, t1 - tw - 1); };
-  int2 dsc_next = make_int2(0, 0);
-  int ts_next = 0;
+  uint32_t dsc_next = 0;
+  int vf_next = 0, ts_next = 0;
   if (t1 > t0) {
     dsc_next = glist[tslot[tl_of(t0)]];
+    vf_next = tdst[tl_of(t0)] * F;
     if (t0 + kWave < t1) ts_next = tslot[tl_of(t0 + kWave)];
   }
   for (int tw = t0; tw < t1; tw += kWave) {
     const int nw = min(kWave, t1 - tw);
-    const int2 dsc = dsc_next;
+    // this window's edge (lane): its list's first record and its length
+    const int2 dsc = make_int2(vf_next + (int)(dsc_next & 0xFFFFu), (int)(dsc_next >> 16));
     if (tw + kWave < t1) {
       dsc_next = glist[ts_next];
+      vf_next = tdst[tl_of(tw + kWave)] * F;
       if (tw + 2 * kWave < t1) ts_next = tslot[tl_of(tw + 2 * kWave)];
     }
     // segments: 64-entry pieces of single lists, U segments' loads in flight. Segment t
@@ -1375,7 +1386,7 @@ size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
   size_t b = bwd_partials_bytes(gt, F);
   if (F <= kGroupMaxF) {
     const int64_t N = gt->n_cols;
-    b += round_up(N * F * 8, 256) + round_up(gt->nnz * 8, 256);
+    b += round_up(N * F * 8, 256) + round_up(gt->nnz * 4, 256);
   }
   return b;
 }
@@ -1421,8 +1432,8 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     // end, as the oracle's f32 sums)
     void* recs = p;
     p += round_up(N * F * 8, 256);
-    int2* glist = (int2*)p;
-    p += round_up(g->nnz * 8, 256);
+    uint32_t* glist = (uint32_t*)p;
+    p += round_up(g->nnz * 4, 256);
     const auto* arg16 = (const uint16_t*)argpos;
     // rows past kPackWaveMax: the schedule's split rows when its chunk guarantees they are
     // a superset, else every row
@@ -1451,8 +1462,8 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     // sums to +0, which the mask would leave +0. With fwd_out alone the mask is applied.
     if (dead_none) mask_src = nullptr;
     hipLaunchKernelGGL((max_bwd_pull_kernel<T, R>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
-                       (const int4*)gt->items, (int)gt->n_items, glist, gp, (int)F, mask_src, ldm, dx, ldx,
-                       w, ws_ld(F));
+                       (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
+                       dx, ldx, w, ws_ld(F));
     if (gt->n_merges > 0)
       hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
                          (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
