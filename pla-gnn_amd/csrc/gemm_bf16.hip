@@ -829,6 +829,16 @@ inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& 
     if (M >= 256 && N >= 256) bm = bn = 256;
     return;
   }
+#ifndef PG_BF16_SMALLK_TILE
+#define PG_BF16_SMALLK_TILE 0  // variant builds: BM * 1000 + BN for products with K <= 128
+#endif
+  if constexpr (PG_BF16_SMALLK_TILE != 0) {
+    if (K <= 128) {
+      bm = PG_BF16_SMALLK_TILE / 1000;
+      bn = PG_BF16_SMALLK_TILE % 1000;
+      return;
+    }
+  }
   // (a short K leaves a 256 x 256 workgroup, alone on its CU, mostly in its epilogue)
   if (N >= 256 && K >= 384 && tiles(256, 256) >= 256) {
     bm = bn = 256;
