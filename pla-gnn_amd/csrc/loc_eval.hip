@@ -107,22 +107,44 @@ __global__ __launch_bounds__(kBlock) void loc_perf_rows_kernel(const float* __re
   rows[3 * r + 2] = fa / (float)o;
 }
 
-// running float32 sums in row order (one lane per metric), then / n
-__global__ void loc_perf_sum_kernel(const float* __restrict__ rows, int64_t n,
-                                    double* __restrict__ out) {
-  const int m = threadIdx.x;
-  if (m >= 3) return;
+// running float32 sums in row order (one lane per metric), then / n. The per-row values
+// stream through LDS in chunks loaded by waves 1-3 (many loads in flight, the next chunk
+// while the current one is summed); wave 0's lanes 0-2 keep the three dependent add chains
+// (a chain fed straight from global memory waited out one load latency per 8 rows).
+constexpr int kSumChunk = 2048;  // rows per LDS chunk (2 x 24 KB)
+__global__ __launch_bounds__(256) void loc_perf_sum_kernel(const float* __restrict__ rows, int64_t n,
+                                                           double* __restrict__ out) {
+  __shared__ float buf[2][kSumChunk * 3];
+  const int t = threadIdx.x;
+  const int64_t nch = (n + kSumChunk - 1) / kSumChunk;
+  auto load = [&](int64_t c) {
+    if (t < 64) return;
+    const int64_t r0 = c * kSumChunk;
+    const int cnt = (int)min<int64_t>(kSumChunk, n - r0) * 3;
+    float* b = buf[c & 1];
+    for (int i = t - 64; i < cnt; i += 192) b[i] = rows[3 * r0 + i];
+  };
   float s = 0.f;
-  int64_t r = 0;
-  for (; r + 8 <= n; r += 8) {
-    float v[8];
+  load(0);
+  __syncthreads();
+  for (int64_t c = 0; c < nch; ++c) {
+    if (c + 1 < nch) load(c + 1);
+    if (t < 3) {
+      const float* b = buf[c & 1];
+      const int cnt = (int)min<int64_t>(kSumChunk, n - c * kSumChunk);
+      int i = 0;
+      for (; i + 8 <= cnt; i += 8) {
+        float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = rows[3 * (r + e) + m];
+        for (int e = 0; e < 8; ++e) v[e] = b[3 * (i + e) + t];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s = s + v[e];
+        for (int e = 0; e < 8; ++e) s = s + v[e];
+      }
+      for (; i < cnt; ++i) s = s + b[3 * i + t];
+    }
+    __syncthreads();
   }
-  for (; r < n; ++r) s = s + rows[3 * r + m];
-  out[m] = (double)(s / (float)n);
+  if (t < 3) out[t] = (double)(s / (float)n);
 }
 
 }  // namespace
@@ -167,7 +189,7 @@ int pg_loc_performance(const float* loc_true, int64_t ldt, const double* loc_pre
   float* rows = (float*)ws;
   hipLaunchKernelGGL(loc_perf_rows_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                      loc_true, ldt, loc_pred, ldp, n, (int)C, rows);
-  hipLaunchKernelGGL(loc_perf_sum_kernel, dim3(1), dim3(64), 0, st, (const float*)rows, n, out3);
+  hipLaunchKernelGGL(loc_perf_sum_kernel, dim3(1), dim3(256), 0, st, (const float*)rows, n, out3);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pg::set_error((int)e, "pg_loc_performance: %s", hipGetErrorString(e));
   return pg::ok();
