@@ -20,7 +20,7 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kRowsPerPart = 1024;
+constexpr int kRowsPerPart = 256;
 
 // per-column partial min / max over row chunks: part[b][c] = {min, max}
 __global__ __launch_bounds__(kBlock) void col_minmax_part_kernel(const float* __restrict__ p,
@@ -31,12 +31,25 @@ __global__ __launch_bounds__(kBlock) void col_minmax_part_kernel(const float* __
   const int64_t r0 = (int64_t)blockIdx.x * kRowsPerPart;
   const int64_t r1 = std::min<int64_t>(n, r0 + kRowsPerPart);
   float mn = INFINITY, mx = -INFINITY;
-  if (g < G)
-    for (int64_t r = r0 + g; r < r1; r += G) {
+  if (g < G) {
+    // four rows' loads in flight per iteration (min / max are order-free)
+    int64_t r = r0 + g;
+    for (; r + 3 * G < r1; r += 4 * G) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = p[(r + e * G) * ldp + c];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        mn = fminf(mn, v[e]);
+        mx = fmaxf(mx, v[e]);
+      }
+    }
+    for (; r < r1; r += G) {
       const float v = p[r * ldp + c];
       mn = fminf(mn, v);
       mx = fmaxf(mx, v);
     }
+  }
   smin[threadIdx.x] = mn;
   smax[threadIdx.x] = mx;
   __syncthreads();
@@ -49,9 +62,14 @@ __global__ __launch_bounds__(kBlock) void col_minmax_part_kernel(const float* __
   }
 }
 
+// CT: the class count at compile time (the per-row arrays then live in registers; with a
+// run-time count they went to scratch memory), or 0
+template <int CT>
 __global__ __launch_bounds__(kBlock) void loc_correction_kernel(
-    const float* __restrict__ p, int64_t ldp, int64_t n, int C, const float2* __restrict__ part,
+    const float* __restrict__ p, int64_t ldp, int64_t n, int Cr, const float2* __restrict__ part,
     int nparts, float alpha, double* __restrict__ pred, int64_t ldpred) {
+  const int C = CT > 0 ? CT : Cr;
+  constexpr int VN = CT > 0 ? CT : 64;
   __shared__ float cmin[64], cmax[64];
   if ((int)threadIdx.x < C) {
     float mn = INFINITY, mx = -INFINITY;
@@ -66,19 +84,22 @@ __global__ __launch_bounds__(kBlock) void loc_correction_kernel(
   __syncthreads();
   const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (r >= n) return;
-  float v[64];
+  float v[VN];
   float s = 0.f;
+#pragma unroll
   for (int c = 0; c < C; ++c) {
     v[c] = (p[r * ldp + c] - cmin[c]) / (cmax[c] - cmin[c]);
     s = s + v[c];
   }
   float rmax = -INFINITY, rmin = INFINITY;
+#pragma unroll
   for (int c = 0; c < C; ++c) {
     v[c] = v[c] / s;
     rmax = fmaxf(rmax, v[c]);
     rmin = fminf(rmin, v[c]);
   }
   const float th = rmax - (rmax - rmin) * alpha;
+#pragma unroll
   for (int c = 0; c < C; ++c) pred[r * ldpred + c] = v[c] > th ? 1.0 : 0.0;
 }
 
@@ -169,8 +190,13 @@ int pg_loc_correction(const float* proba, int64_t ldp, int64_t n, int32_t C, dou
   float2* part = (float2*)ws;
   hipLaunchKernelGGL(col_minmax_part_kernel, dim3(parts), dim3(kBlock), 0, st, proba, ldp, n, (int)C, part);
   // torch multiplies a float32 tensor by the Python float alpha in float32
-  hipLaunchKernelGGL(loc_correction_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                     st, proba, ldp, n, (int)C, (const float2*)part, parts, (float)alpha, pred, ldpred);
+  const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+  if (C == 12)  // the reference's 12 subcellular locations
+    hipLaunchKernelGGL(loc_correction_kernel<12>, grid, dim3(kBlock), 0, st, proba, ldp, n, (int)C,
+                       (const float2*)part, parts, (float)alpha, pred, ldpred);
+  else
+    hipLaunchKernelGGL(loc_correction_kernel<0>, grid, dim3(kBlock), 0, st, proba, ldp, n, (int)C,
+                       (const float2*)part, parts, (float)alpha, pred, ldpred);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pg::set_error((int)e, "pg_loc_correction: %s", hipGetErrorString(e));
   return pg::ok();
