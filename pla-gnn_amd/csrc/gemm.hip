@@ -1003,7 +1003,8 @@ inline void group_plan(const pg_gemm_part_t* parts, int n, GroupPlan& g) {
 }
 
 inline bool part_ok(const pg_gemm_part_t& q) {
-  return q.M >= 0 && q.N >= 0 && q.K >= 0 && q.M <= INT32_MAX && q.N <= INT32_MAX && q.K <= INT32_MAX &&
+  const bool bufs = (q.M == 0 || q.N == 0 || q.C) && (q.M == 0 || q.N == 0 || q.K == 0 || (q.A && q.B));
+  return bufs && q.M >= 0 && q.N >= 0 && q.K >= 0 && q.M <= INT32_MAX && q.N <= INT32_MAX && q.K <= INT32_MAX &&
          q.ldc >= q.N && (q.transa ? q.lda >= q.M : q.lda >= q.K) && (q.transb ? q.ldb >= q.K : q.ldb >= q.N) &&
          (q.beta == 0.f || q.beta == 1.f);
 }

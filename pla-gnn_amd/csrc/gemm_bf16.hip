@@ -1055,7 +1055,8 @@ int pg_gemm_bf16_group(const pg_gemm_part_t* parts, int n, void* ws, size_t ws_b
     const pg_gemm_part_t& q = parts[p];
     if (q.M < 0 || q.N < 0 || q.K < 0 || q.M > INT32_MAX || q.N > INT32_MAX || q.K > INT32_MAX || q.ldc < q.N ||
         (q.transa ? q.lda < q.M : q.lda < q.K) || (q.transb ? q.ldb < q.K : q.ldb < q.N) ||
-        (q.beta != 0.f && q.beta != 1.f))
+        (q.beta != 0.f && q.beta != 1.f) || (q.M > 0 && q.N > 0 && !q.C) ||
+        (q.M > 0 && q.N > 0 && q.K > 0 && (!q.A || !q.B)))
       return pg::set_error(PG_ERR_INVALID, "pg_gemm_bf16_group: bad part %d", p);
   }
   if (ws_bytes < pg_gemm_bf16_group_workspace(parts, n) || !ws || !al16(ws))

@@ -631,6 +631,9 @@ def test_gemm_f32_group_bad_args():
     parts[1].beta = 0.5
     assert L.pg_gemm_f32_group(parts, 2, ws.data_ptr(), ws.numel(), None) == -1
     assert L.pg_gemm_f32_group(parts, 17, ws.data_ptr(), ws.numel(), None) == -1
+    parts[1].beta = 0.0
+    parts[0].C = None  # a part with outputs needs C
+    assert L.pg_gemm_f32_group(parts, 2, ws.data_ptr(), ws.numel(), None) == -1
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
