@@ -284,21 +284,18 @@ def _roofline(engine, gt, bf16):
     return groups, roof
 
 
-def _traffic(config, group, engine):
-    """HBM bytes per launch (per library call, as `achieved`) of `group` from the committed
-    PMC passes (profiles/pmc_traffic.json, scripts/pmc_traffic.sh: 2 FETCH_SIZE + WRITE_SIZE
-    per KERNEL dispatch), or None. A GEMM call is one kernel; a max-aggregation call is the
-    max kernel (+ the merge kernel when the graph has split rows), a max-backward call the
-    pack and pull kernels (+ the merge)."""
+def _traffic(config, group, calls_per_step):
+    """HBM bytes per library call (as `achieved`: a call can be several kernel dispatches) of
+    `group` from the committed PMC passes (profiles/pmc_traffic.json, scripts/pmc_traffic.sh:
+    2 FETCH_SIZE + WRITE_SIZE of every dispatch of the group, per step), or None."""
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(tfile):
         return None
     with open(tfile) as f:
-        b = json.load(f).get(config, {}).get(group)
-    if b is None:
+        b = json.load(f).get(config, {}).get("bytes_per_step", {}).get(group)
+    if b is None or not calls_per_step:
         return None
-    per_call = {"spmm_max_fwd": 1 + (engine.dg.fwd.n_merges > 0), "spmm_max_bwd": 2 + (engine.dg.bwd.n_merges > 0)}
-    return round(b * per_call.get(group, 1))
+    return round(b / calls_per_step)
 
 
 def _job_of(rank, mode):
@@ -334,7 +331,9 @@ def run(args, rank, world, dev, dist, mode, breakdown=True):
         from plagnn import dist as pdist
 
         engine.broadcast_params()  # identical starting replicas
-        allreduce = pdist.allreduce_mean
+        # two gradient buckets (top SAGE layer + MLP, then the layers below); over RCCL both
+        # all-reduces are captured into the step graph, the first under the rest of the backward
+        allreduce = pdist.BucketAllReduce(engine.gflat, engine.grad_buckets())
 
     if args.eager:  # PMC passes: every launch a plain dispatch (counters see graph replays poorly)
         for _ in range(args.warmup):
@@ -383,14 +382,26 @@ def run(args, rank, world, dev, dist, mode, breakdown=True):
                  "value_at_median": round(edges.item() / (med / 1e3), 1)}
     allreduce_ms = None
     if allreduce is not None and not args.eager:
-        # the gradient all-reduce alone: HIP events around it on the replay stream, over as
-        # many more steps (each rank's median, then the max over ranks)
-        engine.ar_events = []
-        for _ in range(n_med):
-            step()
-        torch.cuda.synchronize(dev)
-        ar = torch.tensor([_median_ms(engine.ar_events)], dtype=torch.float64, device=dev)
-        engine.ar_events = None
+        if engine.allreduce_in_graph:
+            # the collective is inside the step graph: time the same bucket all-reduces alone,
+            # eagerly on the replay stream, as many times (the gradients are rewritten by the
+            # next step's backward, so averaging them again changes nothing that is kept)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_med)]
+            for ea, eb in evs:
+                ea.record()
+                allreduce()
+                eb.record()
+            torch.cuda.synchronize(dev)
+            ar = torch.tensor([_median_ms(evs)], dtype=torch.float64, device=dev)
+        else:
+            # between the two replayed graphs: HIP events around it on the replay stream, over
+            # as many more steps (each rank's median, then the max over ranks)
+            engine.ar_events = []
+            for _ in range(n_med):
+                step()
+            torch.cuda.synchronize(dev)
+            ar = torch.tensor([_median_ms(engine.ar_events)], dtype=torch.float64, device=dev)
+            engine.ar_events = None
         dist.all_reduce(ar, op=dist.ReduceOp.MAX)
         allreduce_ms = ar.item()
     loss_tr, loss_va = engine.losses()
@@ -412,17 +423,27 @@ def run(args, rank, world, dev, dist, mode, breakdown=True):
     ar_info = None
     if allreduce_ms is not None:
         nbytes = engine.gflat.numel() * engine.gflat.element_size()
-        ar_info = {"ms_per_step": round(allreduce_ms, 4), "bytes": nbytes, "op": "AVG (one flat f32 bucket)",
-                   "timing": "HIP events around the eager all-reduce between the two replayed graphs, "
-                             "median over steps, max over ranks",
+        inside = engine.allreduce_in_graph
+        ar_info = {"ms_per_step": round(allreduce_ms, 4), "bytes": nbytes,
+                   "op": f"AVG, {len(allreduce.buckets)} f32 buckets of one flat buffer "
+                         f"({', '.join(str((b - a) * 4) for a, b in allreduce.buckets)} B)",
+                   "in_step_graph": inside,
+                   "timing": ("the collective alone: HIP events around the buckets' eager all-reduces on the replay "
+                              "stream, median over steps, max over ranks; in the step it runs inside the graph on a "
+                              "communication stream, the first bucket beside the rest of the backward"
+                              if inside else
+                              "HIP events around the eager all-reduce between the two replayed graphs, "
+                              "median over steps, max over ranks"),
                    "share_of_step": round(allreduce_ms / med, 4)}
     if not breakdown:
         return {"value": round(value, 1), "unit": "edges/s", "ms_per_step": round(t_max / args.steps * 1e3, 4),
                 "step_distribution": step_dist,
                 "scaling": "strong" if not summed else "weak",
+                "overhead_only": not summed,
                 "what": ("one shared model; every rank runs the full-graph step on its shard of the train rows, "
                          f"one {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} all-reduce of the "
-                         "gradients per step; value = ONE model's edges/s"
+                         "gradients per step; value = ONE model's edges/s, so it cannot exceed the N = 1 value: "
+                         "this leg measures what the collective costs (overhead only), not a speed-up"
                          if not summed else "a different graph per rank; value sums the ranks"),
                 "allreduce": ar_info, "loss": {"train": loss_tr, "val": loss_va}}
 
@@ -438,7 +459,7 @@ def run(args, rank, world, dev, dist, mode, breakdown=True):
     rf = roof(dom)
     rf["timing"] = ("HIP events around back-to-back replays of a graph holding this group's launches of one step "
                     "(the step's own buffers), per step")
-    rf["traffic"] = _traffic(args.config, dom, engine)
+    rf["traffic"] = _traffic(args.config, dom, rf.get("launches_per_step"))
     if world > 1:
         par = (f"replicas{world}: independent (round, fold) trainings, no collective" if mode == "replicas" else
                f"dp{world}: shared model, one gradient all-reduce per step, "

@@ -265,6 +265,16 @@ __device__ unsigned long long pg_x3_stamp[64][66][4];
 template <int BM, int BN>
 constexpr int x3_depth() { return BM * BN <= 128 * 64 ? 2 : 1; }
 
+// Waves per SIMD the register allocation must allow. 128 x 128 tiles (48 KB of LDS, three
+// per CU by LDS): left unbounded the compiler took 152 VGPRs + 64 AGPRs (216 allocated:
+// two waves per SIMD, so two workgroups per CU); bounded to three it fits 145-153 VGPRs,
+// no AGPRs, no spills.
+#ifndef PG_X3_WAVES_BIG
+#define PG_X3_WAVES_BIG 3
+#endif
+template <int BM, int BN>
+constexpr int x3_waves() { return x3_depth<BM, BN>() == 2 ? 4 : PG_X3_WAVES_BIG; }
+
 template <int BM, int BN>
 constexpr int x3_lds_u16() {
   constexpr int STAGE_U16 = 2 * 3 * (BM * KS + BN * KS);  // two buffers of [A_h A_m A_l | B_h B_m B_l]
@@ -454,7 +464,7 @@ __device__ __forceinline__ int x3_item(int items) {
 }
 
 template <int BM, int BN, bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_depth<BM, BN>() == 2 ? 4 : 1)))
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_waves<BM, BN>())))
 void gemm_x3_kernel(
     int M, int N, int K, int k_per_split, int tiles_n, int tiles, float alpha,
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
@@ -472,7 +482,7 @@ void gemm_x3_kernel(
 // laid end to end, one launch for all of them (the step's weight gradients: the slab bytes
 // then scale with the group's workgroups, not with each product's).
 template <int BM, int BN, bool TA, bool TB>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_depth<BM, BN>() == 2 ? 4 : 1)))
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_waves<BM, BN>())))
 void gemm_x3_group_kernel(X3Group g) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[x3_lds_u16<BM, BN>()];
   const int item = x3_item(g.items);

@@ -8,10 +8,12 @@ from __future__ import annotations
 
 import ctypes
 import os
+import warnings
 
 import torch  # noqa: F401  (load order: see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+ABI_VERSION = 9  # pg_version() of the library this package binds (include/plagnn.h)
 # PLAGNN_LIB overrides the library path (A/B builds of tuning variants)
 LIB_PATH = os.environ.get("PLAGNN_LIB") or os.path.join(_HERE, "libplagnn.so")
 
@@ -188,12 +190,21 @@ def lib():
                 f"{LIB_PATH} is missing: build the HIP extension first "
                 "(make -C pla-gnn_amd, or __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)
+        missing = []
         for name, (res, args) in SIGNATURES.items():
             if os.environ.get("PLAGNN_LIB") and not hasattr(L, name):
-                continue  # an older A/B build (scripts/*_ab.sh) without this entry point
+                missing.append(name)  # an older A/B build (scripts/*_ab.sh) without this entry point
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        abi = int(L.pg_version()) if hasattr(L, "pg_version") else -1
+        if abi != ABI_VERSION or missing:
+            # only reachable through PLAGNN_LIB (the product library exports every symbol or
+            # getattr above raised): say what this build lacks instead of failing later
+            warnings.warn(f"{LIB_PATH}: ABI {abi} (this package expects {ABI_VERSION}); "
+                          f"{len(missing)} declared entry points missing: {', '.join(missing[:12])}"
+                          f"{' ...' if len(missing) > 12 else ''}", RuntimeWarning, stacklevel=2)
         _LIB = L
     return _LIB
 

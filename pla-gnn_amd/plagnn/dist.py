@@ -37,15 +37,66 @@ def init(backend: Optional[str] = None, device: Optional[torch.device] = None) -
     return True
 
 
+def _average(t: torch.Tensor) -> None:
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(t, op=dist.ReduceOp.AVG)
+    else:  # gloo has no AVG
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t.div_(dist.get_world_size())
+
+
 def allreduce_mean(t: torch.Tensor) -> torch.Tensor:
     """In-place average over ranks (one collective on the whole bucket)."""
     if dist.is_initialized() and dist.get_world_size() > 1:
-        if dist.get_backend() == "nccl":
-            dist.all_reduce(t, op=dist.ReduceOp.AVG)
-        else:  # gloo has no AVG
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            t.div_(dist.get_world_size())
+        _average(t)
     return t
+
+
+class BucketAllReduce:
+    """The step's gradient all-reduce as several buckets of one flat buffer, each averaged
+    as soon as the backward has finished it (TrainEngine.grad_buckets: the top SAGE layer +
+    the MLP first, then the layers below), so the first bucket's collective overlaps the
+    rest of the backward.
+
+    * RCCL (backend "nccl"): `launch(i)` issues bucket i's all-reduce on a communication
+      stream that forks from the current one, `join()` makes the current stream wait for
+      it. Both are capturable, so TrainEngine.capture() puts the whole dp step, collective
+      included, into ONE HIP graph.
+    * gloo (CPU collectives: tests, rehearsals): not capturable; `__call__` averages the
+      buckets one after the other on the current stream, between the two graphs.
+    Averaging is element-wise, so splitting the buffer changes no value when each element's
+    sum runs in the same rank order (two ranks: always; tests/test_dist.py)."""
+
+    def __init__(self, flat: torch.Tensor, buckets):
+        self.flat = flat
+        self.buckets = [(int(a), int(b)) for a, b in buckets if b > a]
+        # (a one-rank RCCL group still runs the collective: scripts/probes/dp_capture_probe.py)
+        self.active = dist.is_initialized()
+        self.capturable = flat.is_cuda and self.active and dist.get_backend() == "nccl"
+        self.stream = torch.cuda.Stream(flat.device) if self.capturable else None
+
+    def view(self, i: int) -> torch.Tensor:
+        a, b = self.buckets[i]
+        return self.flat[a:b]
+
+    def launch(self, i: int) -> None:
+        """Bucket i's all-reduce on the communication stream (RCCL), ordered after the work
+        issued so far on the current stream."""
+        cur = torch.cuda.current_stream(self.flat.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            _average(self.view(i))
+
+    def join(self) -> None:
+        torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
+
+    def __call__(self, flat: Optional[torch.Tensor] = None) -> None:
+        """Every bucket, in order, on the current stream (eager; any backend)."""
+        if flat is not None and flat.data_ptr() != self.flat.data_ptr():
+            raise ValueError("BucketAllReduce: another buffer than the one it was built for")
+        if self.active:
+            for i in range(len(self.buckets)):
+                _average(self.view(i))
 
 
 def broadcast_(tensors: Iterable[torch.Tensor], src: int = 0) -> None:

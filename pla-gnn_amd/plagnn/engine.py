@@ -38,6 +38,7 @@ from .graph import CSRGraph, DeviceGraph
 from .ops import LEAKY_SLOPE, round4
 
 RELU, LEAKY, NONE = _lib.PG_ACT_RELU, _lib.PG_ACT_LEAKY, _lib.PG_ACT_NONE
+MAX_GROUP_PARTS = 16  # pg_gemm_*_group: up to 16 parts per call (include/plagnn.h)
 
 
 def launch_group(site: str) -> str:
@@ -84,6 +85,8 @@ class TrainEngine:
     _filter: Optional[str] = None  # group_times: issue only this launch group
     _issued = 0
     _rec: Optional[list] = None    # gemm_bytes_per_step's dry-run record
+    _split_buckets = False         # dp: the weight gradients as two grouped launches (grad_buckets)
+    _ar_inline = None              # dp over RCCL: the BucketAllReduce launched from inside the backward
 
     def __init__(self, graph: CSRGraph, features: torch.Tensor, labels: torch.Tensor,
                  dims: Sequence[int], class_weight, train_index, val_index=None,
@@ -228,16 +231,51 @@ class TrainEngine:
             self._gemm_plans[(M_, N_, K_)] = sk
             need = max(need, L.pg_gemm_f32_workspace(M_, N_, K_, sk))
         if self.GROUP_WGRAD:
-            # the grouped launch's slabs: sized from the shapes alone (transposed A, plain B)
-            shapes = self._wgrad_shapes()
-            parts = (_lib.PgGemmPart * len(shapes))()
-            for i, (M_, N_, K_) in enumerate(shapes):
-                parts[i].transa, parts[i].transb, parts[i].M, parts[i].N, parts[i].K = 1, 0, M_, N_, K_
-            self.gws = torch.empty(int(L.pg_gemm_f32_group_workspace(parts, len(shapes))), dtype=torch.uint8,
+            # the grouped launches' slabs, sized from the shapes alone (transposed A, plain B)
+            self.gws = torch.empty(self._group_ws_bytes(L.pg_gemm_f32_group_workspace), dtype=torch.uint8,
                                    device=dev)
         need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
         self.ws_bytes = self.ws.numel()
+
+    def _wgrad_groupings(self):
+        """The weight-gradient parts (shapes, in the order the backward issues them) of every
+        grouped launch the step can make: all of them at once (one bucket), or [top SAGE layer
+        + MLP] and [the layers below] (two buckets, grad_buckets), each chunked to the
+        library's part limit."""
+        sh = self._wgrad_shapes()
+        L = self.L
+        order = [sh[-1], sh[-2]] + [x for l in reversed(range(L)) for x in (sh[2 * l], sh[2 * l + 1])]
+        groups = [order]
+        if L > 1:
+            groups += [order[:4], order[4:]]
+        out = []
+        for g in groups:
+            out += [g[i:i + MAX_GROUP_PARTS] for i in range(0, len(g), MAX_GROUP_PARTS)]
+        return out
+
+    def _group_ws_bytes(self, ws_fn) -> int:
+        need = 0
+        for g in self._wgrad_groupings():
+            parts = (_lib.PgGemmPart * len(g))()
+            for i, (M_, N_, K_) in enumerate(g):
+                parts[i].transa, parts[i].transb, parts[i].M, parts[i].N, parts[i].K = 1, 0, M_, N_, K_
+            n = int(ws_fn(parts, len(g)))
+            if n == 0:
+                raise ValueError(f"grouped weight gradients: no workspace size for {len(g)} parts")
+            need = max(need, n)
+        return need
+
+    def grad_buckets(self):
+        """Ranges of the flat gradient buffer in the order the backward completes them: the
+        top SAGE layer + the MLP (their weight gradients are done once the top layer's max
+        backward has run: one contiguous tail of the flat layout), then the layers below.
+        One bucket for a one-layer model."""
+        n = self.gflat.numel()
+        if self.L < 2:
+            return [(0, n)]
+        off = self.flat_layout.offsets[f"conv{self.L}.Wcp"]
+        return [(off, n), (0, off)]
 
     # ------------------------------------------------------------------ parameters
     def _wgrad_shapes(self):
@@ -438,8 +476,13 @@ class TrainEngine:
         K = A.shape[0] if transa else A.shape[1]
         N = B.shape[0] if transb else B.shape[1]
         self._rec_gemm(A, B, C, M, N, K, beta, dact)
-        sk = self._gemm_plans.get((M, N, K), 1) if (bias is None and act == NONE and dact is None) else 1
-        if self.GROUP_WGRAD and (M, N, K) in self._gemm_plans and bias is None and act == NONE and dact is None:
+        # weight gradients (they feed only Adam) are recognised by their launch site, never by
+        # shape: an input gradient of the same shape is read right after it is written
+        wgrad = tag.startswith("gemm.wgrad")
+        if wgrad and (bias is not None or act != NONE or dact is not None):
+            raise ValueError(f"{tag}: a weight gradient takes no epilogue")
+        sk = self._gemm_plans.get((M, N, K), 1) if wgrad else 1
+        if self.GROUP_WGRAD and wgrad:
             q = _lib.PgGemmPart()
             q.transa, q.transb, q.M, q.N, q.K = int(transa), int(transb), M, N, K
             q.A, q.lda, q.B, q.ldb = ptr(A), A.stride(0), ptr(B), B.stride(0)
@@ -478,10 +521,11 @@ class TrainEngine:
 
     def _reduce_deferred(self) -> None:
         parts, self._parts = self._parts, []
-        if parts:
-            arr = (_lib.PgGemmPart * len(parts))(*[q for q, _ in parts])
-            with self._t("gemm.wgrad.group", sum(w for _, w in parts)):
-                self._call("pg_gemm_f32_group", arr, len(parts), ptr(self.gws), self.gws.numel(), self._s())
+        for i in range(0, len(parts), MAX_GROUP_PARTS):  # the library's part limit per launch
+            chunk = parts[i:i + MAX_GROUP_PARTS]
+            arr = (_lib.PgGemmPart * len(chunk))(*[q for q, _ in chunk])
+            with self._t("gemm.wgrad.group", sum(w for _, w in chunk)):
+                self._call("pg_gemm_f32_group", arr, len(chunk), ptr(self.gws), self.gws.numel(), self._s())
         jobs, self._jobs = self._jobs, []
         for i in range(0, len(jobs), 16):
             part = jobs[i:i + 16]
@@ -555,12 +599,26 @@ class TrainEngine:
             # d Wpool = dP^T H, d bpool = sum_nodes dP
             self._gemm(dP, HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
                        tag=f"gemm.wgrad.pool.l{l + 1}")
+            self._wgrad_bucket_boundary(l)
             if l > 0:
                 # dH = ([dY | dP] [Wself ; Wpool]) * leaky'(H), one K = Fo + Fi product: the
                 # lower layer's dY (H is the previous layer's output)
                 self._gemm(DYP, P[p + "Wstack"], self.DYP[l - 1][:, :Fi], act=LEAKY, dact=HM[:, :Fi],
                            tag=f"gemm.dgrad.stack.l{l + 1}")
         self._reduce_deferred()
+        self._bucket_done(len(self.grad_buckets()) - 1)
+
+    def _wgrad_bucket_boundary(self, l: int) -> None:
+        """After the top SAGE layer's weight gradients are issued (dp with two buckets): run
+        that bucket's grouped launch now, and with RCCL start its all-reduce, which then
+        overlaps the rest of the backward."""
+        if self._split_buckets and l == self.L - 1 and self.L > 1:
+            self._reduce_deferred()
+            self._bucket_done(0)
+
+    def _bucket_done(self, i: int) -> None:
+        if self._ar_inline is not None and self._filter is None:
+            self._ar_inline.launch(i)
 
     def adam(self) -> None:
         st = self._s()
@@ -569,10 +627,21 @@ class TrainEngine:
             self._call("pg_adam_apply", ptr(self.flat), ptr(self.gflat), ptr(self.m), ptr(self.v),
                  self.flat.numel(), ptr(self.adam_state), self.betas[0], self.betas[1], self.eps, 0.0, st)
 
+    def _uses_buckets(self, allreduce) -> None:
+        self._split_buckets = allreduce is not None and len(getattr(allreduce, "buckets", ())) > 1
+
     def step_eager(self, allreduce=None) -> None:
-        self.forward()
-        self.backward()
-        if allreduce is not None:
+        self._uses_buckets(allreduce)
+        inline = allreduce is not None and getattr(allreduce, "capturable", False)
+        self._ar_inline = allreduce if inline else None
+        try:
+            self.forward()
+            self.backward()
+        finally:
+            self._ar_inline = None
+        if inline:
+            allreduce.join()
+        elif allreduce is not None:
             allreduce(self.gflat)
         self.adam()
         self.steps_done += 1
@@ -580,10 +649,14 @@ class TrainEngine:
     # ------------------------------------------------------------------ graph capture
     def capture(self, warmup: int = 2, allreduce=None) -> None:
         """Capture the step into HIP graphs. Warm-up steps run eagerly first (they are real
-        training steps and count as such). With `allreduce` (multi-GPU data parallel),
-        forward+backward and Adam are two graphs and the gradient all-reduce runs between
-        them on the same stream."""
+        training steps and count as such). With `allreduce` (multi-GPU data parallel): a
+        capturable one (plagnn.dist.BucketAllReduce over RCCL) goes INTO the step's one
+        graph, each gradient bucket's collective on a communication stream as soon as the
+        backward has finished that bucket; any other (gloo, or a plain function) runs
+        eagerly between two graphs, forward+backward and Adam."""
         self.allreduce = allreduce
+        self._uses_buckets(allreduce)
+        inline = allreduce is not None and getattr(allreduce, "capturable", False)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -591,12 +664,18 @@ class TrainEngine:
                 self.step_eager(allreduce)
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
-        if allreduce is None:
+        self.graph_adam = None
+        if allreduce is None or inline:
             with torch.cuda.graph(self.graph):
-                self.forward()
-                self.backward()
+                self._ar_inline = allreduce if inline else None
+                try:
+                    self.forward()
+                    self.backward()
+                finally:
+                    self._ar_inline = None
+                if inline:
+                    allreduce.join()
                 self.adam()
-            self.graph_adam = None
         else:
             with torch.cuda.graph(self.graph):
                 self.forward()
@@ -604,6 +683,10 @@ class TrainEngine:
             self.graph_adam = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_adam):
                 self.adam()
+
+    @property
+    def allreduce_in_graph(self) -> bool:
+        return self.graph is not None and self.allreduce is not None and self.graph_adam is None
 
     def step(self) -> None:
         if self.graph is None:

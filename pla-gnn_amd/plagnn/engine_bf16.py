@@ -24,7 +24,7 @@ import torch
 
 from . import _lib, ops
 from ._lib import PG_ARG_DEAD_NONE as DEAD_NONE, ptr
-from .engine import LEAKY, NONE, RELU, TrainEngine, _Flat
+from .engine import LEAKY, MAX_GROUP_PARTS, NONE, RELU, TrainEngine, _Flat
 
 BF16, F32 = _lib.PG_DTYPE_BF16, _lib.PG_DTYPE_F32
 LEAKY_SLOPE = ops.LEAKY_SLOPE
@@ -131,11 +131,7 @@ class TrainEngineBF16(TrainEngine):
         self._parts = []
         if self.GROUP_WGRAD:
             # the grouped weight gradients' slabs: sized from the shapes alone
-            shapes = self._wgrad_shapes()
-            parts = (_lib.PgGemmPart * len(shapes))()
-            for i, (M_, N_, K_) in enumerate(shapes):
-                parts[i].transa, parts[i].transb, parts[i].M, parts[i].N, parts[i].K = 1, 0, M_, N_, K_
-            self.gws = torch.empty(int(L.pg_gemm_bf16_group_workspace(parts, len(shapes))), dtype=torch.uint8,
+            self.gws = torch.empty(self._group_ws_bytes(L.pg_gemm_bf16_group_workspace), dtype=torch.uint8,
                                    device=dev)
         # the fused head (pg_mlp_head, run by forward()) and the standalone loss kernel
         need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C))
@@ -150,17 +146,18 @@ class TrainEngineBF16(TrainEngine):
         N = B.shape[0] if transb else B.shape[1]
         self._rec_gemm(A, B, C, M, N, K, beta, dact)
         obf = C.dtype == torch.bfloat16
-        if (self.GROUP_WGRAD and not obf and bias is None and act == NONE and dact is None
-                and (M, N, K) in self._gemm_plans):
+        # weight gradients are recognised by their launch site, never by shape
+        wgrad = tag.startswith("gemm.wgrad")
+        if wgrad and (obf or bias is not None or act != NONE or dact is not None):
+            raise ValueError(f"{tag}: a weight gradient has an f32 output and no epilogue")
+        if self.GROUP_WGRAD and wgrad:
             q = _lib.PgGemmPart()
             q.transa, q.transb, q.M, q.N, q.K = int(transa), int(transb), M, N, K
             q.A, q.lda, q.B, q.ldb = ptr(A), A.stride(0), ptr(B), B.stride(0)
             q.beta, q.C, q.ldc, q.rowsum = beta, ptr(C), C.stride(0), ptr(rowsum)
             self._parts.append((q, 2.0 * M * N * K))
             return
-        sk = 1
-        if not obf and bias is None and act == NONE and dact is None:
-            sk = self._gemm_plans.get((M, N, K), 1)
+        sk = self._gemm_plans.get((M, N, K), 1) if wgrad else 1
         ep = _lib.epilogue(bias, act, LEAKY_SLOPE, dact, rowsum)
         with self._t(tag, 2.0 * M * N * K):
             self._call("pg_gemm_bf16", int(transa), int(transb), M, N, K, 1.0, ptr(A), A.stride(0), ptr(B),
@@ -214,6 +211,7 @@ class TrainEngineBF16(TrainEngine):
                      ptr(self.ws), self.ws_bytes, st)
             self._gemm(dP, HM[:, :Fi], G[p + "Wpool"], transa=True, rowsum=G[p + "bpool"],
                        tag=f"gemm.wgrad.pool.l{l + 1}")
+            self._wgrad_bucket_boundary(l)
             if l > 0:
                 # dH = ([dY | dP] [Wself ; Wpool]) * leaky'(H) -> the lower layer's dY
                 if self.STACK_T:
@@ -223,15 +221,17 @@ class TrainEngineBF16(TrainEngine):
                     self._gemm(DYP, W[p + "Wstack"], self.DYP[l - 1][:, :Fi], act=LEAKY, dact=HM[:, :Fi],
                                tag=f"gemm.dgrad.stack.l{l + 1}")
         self._reduce_deferred()
+        self._bucket_done(len(self.grad_buckets()) - 1)
 
     def _reduce_deferred(self) -> None:
         """Every weight gradient of the step as one grouped split-K launch + one combine
         (pg_gemm_bf16_group): they only feed Adam, so they all wait for the backward's end."""
         parts, self._parts = self._parts, []
-        if parts:
-            arr = (_lib.PgGemmPart * len(parts))(*[q for q, _ in parts])
-            with self._t("gemm.wgrad.group", sum(w for _, w in parts)):
-                self._call("pg_gemm_bf16_group", arr, len(parts), ptr(self.gws), self.gws.numel(), self._s())
+        for i in range(0, len(parts), MAX_GROUP_PARTS):  # the library's part limit per launch
+            chunk = parts[i:i + MAX_GROUP_PARTS]
+            arr = (_lib.PgGemmPart * len(chunk))(*[q for q, _ in chunk])
+            with self._t("gemm.wgrad.group", sum(w for _, w in chunk)):
+                self._call("pg_gemm_bf16_group", arr, len(chunk), ptr(self.gws), self.gws.numel(), self._s())
 
     def adam(self) -> None:
         super().adam()

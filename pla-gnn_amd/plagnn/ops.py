@@ -7,6 +7,7 @@ message passing and to torch-CPU for the dense algebra, as DGL's CPU backend doe
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -382,9 +383,11 @@ def sage_width(F: int) -> int:
 
 
 # layer inputs that take no gradient (the features: the same tensor every epoch) keep their
-# padded [H | M] buffer: {key: [HM, version, busy]}. A buffer whose forward saved it for a
-# backward that has not run yet is busy (its M half must not be overwritten): another
-# forward then gets a fresh buffer.
+# padded [H | M] buffer: {key: [HM, weakref(h), version, busy]}. A hit needs the SAME tensor
+# object (identity through the weak reference, not only its address: a freed input's memory
+# is handed to the next same-size allocation, which starts at the same version) with an
+# unchanged version. A buffer whose forward saved it for a backward that has not run yet is
+# busy (its M half must not be overwritten): another forward then gets a fresh buffer.
 _HM_CACHE: dict = {}
 
 
@@ -395,17 +398,17 @@ def _hm_buffer(h: torch.Tensor, Fp: int, keep: bool):
     key = (h.data_ptr(), tuple(h.shape), str(h.device), Fp) if not h.requires_grad else None
     if key is not None:
         hit = _HM_CACHE.get(key)
-        if hit is not None and hit[1] == h._version and not hit[2]:
-            hit[2] = keep
+        if hit is not None and hit[1]() is h and hit[2] == h._version and not hit[3]:
+            hit[3] = keep
             return hit[0], (key if keep else None)
     HM = torch.empty(N, 2 * Fp, dtype=torch.float32, device=h.device)
     HM[:, :Fin].copy_(h)
     if Fp > Fin:
         HM[:, Fin:Fp].zero_()
-    if key is not None and (key not in _HM_CACHE or not _HM_CACHE[key][2]):
+    if key is not None and (key not in _HM_CACHE or not _HM_CACHE[key][3]):
         if len(_HM_CACHE) > 8:
             _HM_CACHE.clear()
-        _HM_CACHE[key] = [HM, h._version, keep]
+        _HM_CACHE[key] = [HM, weakref.ref(h), h._version, keep]
         return HM, (key if keep else None)
     return HM, None
 
@@ -413,7 +416,7 @@ def _hm_buffer(h: torch.Tensor, Fp: int, keep: bool):
 def _hm_release(key) -> None:
     hit = _HM_CACHE.get(key) if key is not None else None
     if hit is not None:
-        hit[2] = False
+        hit[3] = False
 
 
 class SagePool(torch.autograd.Function):

@@ -2,8 +2,11 @@
 (scripts/pmc_traffic.sh): HBM-side bytes per launch of each kernel group, with the gfx950
 corrections of MI355X_MICROARCH.md "HBM" (FETCH_SIZE counts half of a wide coalesced read:
 x2; WRITE_SIZE exact; both in KB): bytes = 2 FETCH_SIZE + WRITE_SIZE, summed over every
-dispatch of the group in the headline process and divided by its dispatch count: per
-launch, like bench.py's roofline "achieved". Infinity-Cache hits are counted by these
+dispatch of the group in the headline process and divided by the STEPS that process ran
+(head dispatches / 2: head_kernel + head_final_kernel once per step, in the timing graphs
+too), so a library call made of several dispatches (the grouped weight gradients:
+partials + combine) is counted whole; bench.py divides by the group's library calls per
+step for "per call" figures. Infinity-Cache hits are counted by these
 counters (L2 memory-side requests), so for tables that fit the 256 MiB MALL this is fabric
 traffic, an upper bound on true HBM bytes. Groups: scripts/prof_groups.py's.
 
@@ -58,13 +61,20 @@ def main():
             f, w = fk[k], wk.get(k, [0.0, 1])
             print(f"{k:70s} n={f[1]:5d} fetch2x {2 * f[0] / f[1] / 1e6:9.2f} MB  write {w[0] / max(w[1], 1) / 1e6:9.2f} MB")
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
-    cfg = {}
+    steps_f = fetch.get("head", [0.0, 0])[1] / 2
+    steps_w = write.get("head", [0.0, 0])[1] / 2
+    if steps_f <= 0 or steps_w <= 0:
+        raise SystemExit("no head dispatches in the counter files: cannot count steps")
+    per_step = {}
     for g in sorted(set(fetch) | set(write)):
         if g == "other":
             continue
-        f = fetch.get(g, [0.0, 1])
-        w = write.get(g, [0.0, 1])
-        cfg[a.gemm_group if g == "gemm" else g] = 2.0 * f[0] / max(f[1], 1) + w[0] / max(w[1], 1)
+        f = fetch.get(g, [0.0, 0])
+        w = write.get(g, [0.0, 0])
+        per_step[a.gemm_group if g == "gemm" else g] = round(2.0 * f[0] / steps_f + w[0] / steps_w)
+    cfg = {"bytes_per_step": per_step, "steps": [steps_f, steps_w],
+           "dispatches_per_step": {a.gemm_group if g == "gemm" else g: round(v[1] / steps_f, 2)
+                                   for g, v in fetch.items() if g != "other"}}
     out[a.config] = cfg
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)

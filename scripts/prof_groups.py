@@ -67,16 +67,25 @@ def main():
             summary[proc]["groups"][g] = {"launches": v["count"], "total_us": round(v["ns"] / 1e3, 1),
                                           "us_per_launch": round(avg, 3)}
     if bench is not None and pid is not None and str(pid) in summary:
+        # compare PER STEP: a library call can be more than one kernel dispatch (the grouped
+        # weight gradients are a partials launch + a combine launch), so per-dispatch
+        # averages do not compare with the bench's per-call figures. Steps = head dispatches
+        # / 2 (head_kernel + head_final_kernel every step, in every timing graph too).
         rf = bench["roofline"]
-        g = summary[str(pid)]["groups"].get("gemm")
-        if g and "us_per_launch" in rf:
-            ratio = rf["us_per_launch"] / g["us_per_launch"]
-            flops_per_launch = rf["flops_per_step"] / rf["launches_per_step"]
-            prof_tf = flops_per_launch / (g["us_per_launch"] * 1e-6) / 1e12
-            print(f"# bench gemm {rf['us_per_launch']} us/launch (graph replay incl. dispatch gaps) vs rocprof "
-                  f"{g['us_per_launch']:.2f} us/launch: ratio {ratio:.3f}; rocprof -> {prof_tf:.1f} TFLOP/s, "
+        grp = summary[str(pid)]["groups"]
+        g = grp.get("gemm")
+        if g and "ms_per_step" in rf and grp.get("head"):
+            steps = grp["head"]["launches"] / 2
+            prof_ms = g["total_us"] / steps / 1e3
+            ratio = rf["ms_per_step"] / prof_ms
+            prof_tf = rf["flops_per_step"] / (prof_ms * 1e-3) / 1e12
+            print(f"# {steps:.0f} steps; gemm {g['launches'] / steps:.0f} dispatches / {rf['launches_per_step']} "
+                  f"library calls per step; bench {rf['ms_per_step']} ms/step (graph replay incl. dispatch gaps) vs "
+                  f"rocprof {prof_ms:.4f} ms/step: ratio {ratio:.3f}; rocprof -> {prof_tf:.1f} TFLOP/s, "
                   f"frac {prof_tf / rf['peak']:.4f} (bench frac {rf['frac']})")
-            summary["check"] = {"bench_us_per_launch": rf["us_per_launch"], "rocprof_us_per_launch": g["us_per_launch"],
+            summary["check"] = {"steps": steps, "dispatches_per_step": round(g["launches"] / steps, 2),
+                                "calls_per_step": rf["launches_per_step"],
+                                "bench_ms_per_step": rf["ms_per_step"], "rocprof_ms_per_step": round(prof_ms, 5),
                                 "ratio": round(ratio, 4), "rocprof_tflops": round(prof_tf, 2),
                                 "rocprof_frac": round(prof_tf / rf["peak"], 4), "bench_frac": rf["frac"]}
     if a.json:

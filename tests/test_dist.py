@@ -93,3 +93,40 @@ def test_two_rank_gradient_allreduce_matches_serial(tmp_path, oracle_mod):
     opt.step()
     for k in p0:
         torch.testing.assert_close(got[0][k], opt_params[k].detach(), rtol=1e-5, atol=1e-6, msg=k)
+
+
+def _worker_buckets(rank, world, port, outdir):
+    import sys
+
+    sys.path[:0] = [PKG, ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from plagnn import dist as pdist
+
+    assert pdist.init("gloo")
+    rng = np.random.default_rng(10 + rank)
+    base = torch.from_numpy(rng.standard_normal(50_000).astype(np.float32) * np.float32(1e3) ** rng.integers(-2, 3, 50_000))
+    flat = base.clone()
+    pdist.allreduce_mean(flat)
+    two = base.clone()
+    # TrainEngine.grad_buckets' shape: a tail (top layer + MLP) first, then the head
+    ar = pdist.BucketAllReduce(two, [(31_232, 50_000), (0, 31_232)])
+    assert not ar.capturable
+    ar(two)
+    torch.save({"flat": flat, "two": two}, os.path.join(outdir, f"b{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_bucket_allreduce_equals_flat_bitwise(tmp_path):
+    """The dp step's gradient all-reduce in two buckets (plagnn.dist.BucketAllReduce, as
+    TrainEngine reduces its top layer + MLP bucket before the rest of the backward has run)
+    equals one all-reduce of the whole flat buffer bit for bit, on every rank (gloo, two
+    ranks: each element is the same two-term sum either way)."""
+    world = 2
+    mp.start_processes(_worker_buckets, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    got = [torch.load(tmp_path / f"b{r}.pt", weights_only=True) for r in range(world)]
+    for r in range(world):
+        assert torch.equal(got[r]["two"], got[r]["flat"]), f"rank {r}: bucketed != flat"
+        assert torch.equal(got[r]["two"], got[0]["two"])

@@ -1,7 +1,8 @@
 """The engine's multi-GPU path (bench.py --gpus N): world_size 2 over gloo with both ranks
 on cuda:0. Every rank builds a TrainEngine on its own graph from the same parameters,
-captures the step with `allreduce=allreduce_mean` (forward+backward graph, the bucket
-all-reduce, the Adam graph) and replays it. Checked against the serial computation on the
+captures the step with a two-bucket plagnn.dist.BucketAllReduce (gloo: forward+backward
+graph with the weight gradients in two grouped launches, the buckets' all-reduces, the Adam
+graph) and replays it. Checked against the serial computation on the
 oracle: p_{t+1} = Adam(p_t, (g_rank0(p_t) + g_rank1(p_t)) / 2) for both steps, and the two
 ranks must hold bitwise identical parameters afterwards."""
 import os
@@ -58,7 +59,10 @@ def _worker(rank, world, port, outdir):
     g = plagnn.CSRGraph(np.concatenate([src, loops]), np.concatenate([dst, loops]), n)
     eng = plagnn.TrainEngine(g, x, labels, DIMS, _weights(), tr, va, lr=LR, device="cuda:0", params=_params())
     pdist.broadcast_([eng.flat])
-    eng.capture(warmup=1, allreduce=pdist.allreduce_mean)
+    ar = pdist.BucketAllReduce(eng.gflat, eng.grad_buckets())
+    assert len(ar.buckets) == 2 and not ar.capturable  # gloo: between the two graphs
+    eng.capture(warmup=1, allreduce=ar)
+    assert not eng.allreduce_in_graph
     eng.step()
     torch.cuda.synchronize()
     torch.save({k: v.cpu() for k, v in eng.state_dict().items()}, os.path.join(outdir, f"rank{rank}.pt"))
@@ -197,3 +201,53 @@ def test_cfg4_two_replicas_allreduce_matches_serial_adam(tmp_path, oracle_mod):
             err = ((p1 - pr.double()).abs() * settled).max().item()
             assert err <= 1e-4 * scale, f"rank{r} adam {k}: {err:.3e} vs scale {scale:.3e}"
             assert (p1 - po.double()).abs().max().item() <= 1e-6 * scale, f"rank{r} adam(own grads) {k}"
+
+
+def _worker_rccl_one_rank(rank, world, port, outdir):
+    """RCCL with ONE rank (a one-GPU box cannot hold two RCCL ranks): the all-reduce of
+    both buckets captured INTO the step graph on the communication stream (the N > 1
+    path of bench.py), against the same engine run eagerly with the buckets reduced on the
+    step's stream. An average over one rank is the identity, so the two must agree bitwise."""
+    import sys
+
+    sys.path[:0] = [PKG, ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import plagnn
+    from plagnn import dist as pdist
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    src, dst, n, x, labels, tr, va = _problem(0)
+    loops = np.arange(n)
+    g = plagnn.CSRGraph(np.concatenate([src, loops]), np.concatenate([dst, loops]), n)
+    out = {}
+    for mode in ("graph", "eager"):
+        eng = plagnn.TrainEngine(g, x, labels, DIMS, _weights(), tr, va, lr=LR, device="cuda:0", params=_params())
+        ar = pdist.BucketAllReduce(eng.gflat, eng.grad_buckets())
+        assert ar.capturable and len(ar.buckets) == 2
+        if mode == "graph":
+            eng.capture(warmup=1, allreduce=ar)
+            assert eng.allreduce_in_graph
+            for _ in range(3):
+                eng.step()
+        else:
+            for _ in range(4):
+                eng._uses_buckets(ar)
+                eng.forward()
+                eng.backward()
+                ar()
+                eng.adam()
+        torch.cuda.synchronize()
+        out[mode] = {k: v.cpu() for k, v in eng.state_dict().items()}
+    torch.save(out, os.path.join(outdir, "rccl1.pt"))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_rccl_allreduce_in_step_graph_one_rank(tmp_path):
+    mp.start_processes(_worker_rccl_one_rank, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+                       start_method="spawn")
+    got = torch.load(tmp_path / "rccl1.pt", weights_only=True)
+    for k, v in got["eager"].items():
+        assert torch.equal(got["graph"][k], v), f"in-graph RCCL step differs from the eager one on {k}"

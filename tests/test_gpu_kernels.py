@@ -215,6 +215,44 @@ def test_spmm_max_bwd_hub_past_lds_histogram(oracle_mod, F):
         assert np.all(np.abs(dX - ref) <= 1e-5 * mag + 1e-6)
 
 
+@pytest.mark.parametrize("F", [128, 512])
+@pytest.mark.parametrize("dead", [False, True])
+def test_spmm_max_bwd_wide_items_split_rows(oracle_mod, F, dead):
+    """The large-graph backward schedule (graph.default_chunk_bwd above 65 536 nodes: 512
+    out-edges per item) on a graph small enough for the oracle: sources with 700 / 1 500 /
+    3 000 out-edges are split into 2 / 3 / 6 items whose partials go through sum_merge;
+    bit-exact on unsplit rows, split rows within the summation-order bound."""
+    import plagnn
+    from plagnn import ops
+
+    n = 2500
+    rng = np.random.default_rng(F + dead)
+    srcs, dsts = [rng.integers(0, n, 8 * n)], [rng.integers(0, n, 8 * n)]
+    for u, d in ((3, 700), (5, 1500), (9, 3000)):
+        srcs.append(np.full(d, u))
+        dsts.append(rng.integers(0, n, d))
+    src = np.concatenate(srcs + [np.arange(n)]).astype(np.int64)
+    dst = np.concatenate(dsts + [np.arange(n)]).astype(np.int64)
+    g = plagnn.CSRGraph(src, dst, n, chunk=256, chunk_bwd=512)
+    assert g.bwd.chunk == 512 and g.bwd.n_merges >= 3
+    split_rows = set(g.bwd.merges.reshape(-1, 4)[: g.bwd.n_merges, 0].tolist())
+    assert {3, 5, 9} <= split_rows
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False)
+    X = np.maximum(rng.standard_normal((n, F)), 0).astype(np.float32)
+    dZ = rng.standard_normal((n, F)).astype(np.float32)
+    dg = g.on(DEV)
+    Xd = torch.from_numpy(X).to(DEV)
+    _, argx, arge = oracle_mod.spmm_max(og, X)
+    ref = np.where(X > 0, oracle_mod.spmm_max_bwd(og, argx, arge, dZ), 0.0)
+    mag = np.abs(oracle_mod.spmm_max_bwd(og, argx, arge, np.abs(dZ)))
+    _, argpos = ops.spmm_max(dg, Xd, dead_none=dead)
+    dX = ops.spmm_max_backward(dg, argpos, torch.from_numpy(dZ).to(DEV), mask=Xd, dead_none=dead).cpu().numpy()
+    exact = np.array([u not in split_rows for u in range(n)])
+    np.testing.assert_array_equal(dX[exact], ref[exact])
+    assert np.all(np.abs(dX - ref) <= 1e-5 * mag + 1e-6)
+    assert np.abs(dX[[3, 5, 9]]).sum() > 0
+
+
 @pytest.mark.parametrize("mean", [False, True])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_spmm_sum_fwd_bwd(oracle_mod, mean, weighted):
