@@ -183,6 +183,54 @@ def dropin_leg(wl, dims, dev, steps: int, warmup: int):
                     "torch.optim.Adam (code/train.py:197-207)"}
 
 
+def dropin_epoch_with_eval(wl, dims, dev, epochs: int = 2) -> dict:
+    """The epoch a `main_normal.py -d cuda` user pays (code/train.py:197-218): the shim step
+    (plagnn.model + multi_loss + autograd + Adam) plus the reference's own per-epoch
+    evaluation as its code runs it: protein_loc_correction's per-row loop over all N rows
+    (train.py:36-38) and performances_record's host copies and per-row loops on the train
+    and val rows (52-53, 60-78), then the two loss values read on the host (217-218).
+    Median of `epochs` epochs after one warm-up epoch (each takes seconds)."""
+    import dgl
+    from plagnn.model import GNN
+    from plagnn.train import loc_correction_per_row, multi_loss, performances_per_row
+
+    src, dst, _ = wl.edges_without_loops()
+    g = dgl.add_self_loop(dgl.graph((torch.from_numpy(src), torch.from_numpy(dst)), num_nodes=wl.n)).to(dev)
+    features = torch.from_numpy(wl.ds.feat).to(dev)
+    labels = torch.from_numpy(wl.ds.loc.astype(np.float32)).to(dev)
+    tr = torch.as_tensor(wl.train_index, device=dev)
+    va = torch.as_tensor(wl.val_index, device=dev)
+    torch.manual_seed(0)
+    model = GNN(dims).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=5e-5)
+    times, evals = [], []
+    for e in range(epochs + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        model.train()
+        logits = model(g, features)
+        train_loss = multi_loss(logits[tr], labels[tr], wl.class_weight)
+        train_loss.backward()
+        opt.step()
+        model.eval()
+        val_loss = multi_loss(logits[va], labels[va], wl.class_weight)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        pred = loc_correction_per_row(logits.detach(), ALPHA)
+        performances_per_row(labels[tr], pred[tr.cpu()])
+        performances_per_row(labels[va], pred[va.cpu()])
+        train_loss.item(), val_loss.item()
+        t2 = time.perf_counter()
+        if e > 0:
+            times.append(t2 - t0)
+            evals.append(t2 - t1)
+    return {"ms": round(float(np.median(times)) * 1e3, 2), "eval_ms": round(float(np.median(evals)) * 1e3, 2),
+            "epochs": epochs,
+            "what": "shim step + the reference's per-epoch evaluation as its code runs it (per-row Python loops over "
+                    "the N rows and the labelled rows, host copies; code/train.py:19-86, 197-218)"}
+
+
 def dropin_device_time(wl, dims, dev, reps: int = 20) -> float:
     """The device time of the shim model's forward + backward alone (without the reference's
     multi_loss host loop and Adam): zero_grad + model(g, features).backward(G) with a fixed
@@ -562,6 +610,7 @@ def main():
         out = dropin_leg(wl, wl.dims, torch.device("cuda"), steps=min(args.steps, 20), warmup=3)
         if out is not None:
             out["model_fwd_bwd_device_ms"] = round(dropin_device_time(wl, wl.dims, torch.device("cuda")), 4)
+            out["epoch_with_reference_eval"] = dropin_epoch_with_eval(wl, wl.dims, torch.device("cuda"))
         print(json.dumps(out))
         return
     subs = sub_configs(args) if (world == 1 and args.sub_configs) else None
@@ -618,6 +667,10 @@ def main():
             if dropin.get("model_fwd_bwd_device_ms"):
                 dropin["model_vs_engine"] = round(dropin["model_fwd_bwd_device_ms"] / eng, 3)
             legs["dropin"] = dropin
+            # beside the engine's epoch with eval: the epoch a main_normal.py -d cuda user pays
+            ref_ep = dropin.get("epoch_with_reference_eval")
+            if ref_ep:
+                legs["dropin_epoch_with_reference_eval_ms"] = ref_ep["ms"]
     out.update(legs)
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not args.config.startswith("cfg5"):

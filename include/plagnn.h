@@ -119,7 +119,10 @@ typedef struct pg_csr {
   const int32_t* ptr;    /* [n_rows + 1] */
   const int32_t* col;    /* [nnz] */
   const int32_t* eslot;  /* [nnz] or NULL (NULL: slot == k) */
-  const int32_t* epos;   /* [nnz] transposed CSR only: position inside the in-CSR row */
+  const int32_t* epos;   /* [nnz] transposed CSR: position inside the in-CSR row; in-CSR
+                          * (optional, ABI 10): the transposed index of each slot, used by
+                          * pg_spmm_max_bwd[_bf16] to store list descriptors where the pull
+                          * reads them in order (NULL: at the slots) */
   const float* ew;       /* edge weights indexed by in-CSR slot, or NULL */
   const int32_t* items;  /* [4 * n_items] */
   int64_t n_items;
@@ -330,6 +333,18 @@ int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float a
                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
                 int64_t ldc, const pg_gemm_epilogue_t* ep, int split_k, void* ws,
                 size_t ws_bytes, pg_stream_t stream);
+/* pg_gemm_f32 with both operands given as two pieces concatenated along K (ABI 10):
+ * C = alpha [A1 | A2] op([B1 ; B2]) + beta C (+ bias, leaky_relu), A1 M x K1, A2 M x K2 (not
+ * transposed), op(B1) K1 x N, op(B2) K2 x N: the dgl shim's SAGEConv products
+ * [H | M] [Wself | Wneigh]^T and [dY | dP] [Wself ; Wpool] without copying the pieces
+ * together (code/model.py:13-15, 20-25). Three-piece kernel only: K1 a multiple of 4, each
+ * piece's operands 16-B aligned with leading dimensions and contiguous extents multiples of
+ * 4, else PG_ERR_UNSUPPORTED (the caller concatenates instead); ep: bias and act none |
+ * leaky only. */
+int pg_gemm_f32_cat(int transb, int64_t M, int64_t N, int64_t K1, int64_t K2, float alpha, const float* A1,
+                    int64_t lda1, const float* A2, int64_t lda2, const float* B1, int64_t ldb1, const float* B2,
+                    int64_t ldb2, float beta, float* C, int64_t ldc, const pg_gemm_epilogue_t* ep,
+                    pg_stream_t stream);
 
 /* ---------------- device: bf16 storage mode (f32 accumulate) ---------------- */
 
@@ -466,7 +481,8 @@ int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-
                          workspace; 8: pg_csr_t without einv; max backward lists as 8-B
                          records with the edge weight folded in; with fwd_out alone the
                          relu' mask is applied, only PG_ARG_DEAD_NONE implies it;
-                         9: pg_gemm_f32_group */
+                         9: pg_gemm_f32_group; 10: the in-CSR's epos = transposed
+                         indices (transposed max-backward descriptors) */
 
 #ifdef __cplusplus
 }

@@ -70,7 +70,8 @@ constexpr int kSplitBM = PG_SPLIT_TILE / 1000, kSplitBN = PG_SPLIT_TILE % 1000;
 #define PG_X3_TILE_FORCE 0
 #endif
 #ifndef PG_X3_GROUP_TARGET
-#define PG_X3_GROUP_TARGET 768  // workgroups of a grouped split-K launch (three 128 x 128 per CU)
+// workgroups of a grouped split-K launch: three 128 x 128 per CU, two 128 x 256 per CU
+#define PG_X3_GROUP_TARGET (kX3GroupBN > 128 ? 512 : 768)
 #endif
 #ifndef PG_X3_MIN_SLICE
 #define PG_X3_MIN_SLICE 128  // shortest K slice of a split product of the three-piece kernel
@@ -752,6 +753,10 @@ inline bool x3_ok(int transa, int transb, int64_t M, int64_t N, int64_t K, const
                   const float* B, int64_t ldb, const float* C, int64_t ldc, const pg_gemm_epilogue_t* ep,
                   bool split, const void* ws) {
   if constexpr (PG_GEMM_ALGO == 0) return false;
+  // the three-piece kernel addresses each operand by 32-bit byte offsets
+  const int64_t a_ext = transa ? (K - 1) * lda + M : (M - 1) * lda + K;
+  const int64_t b_ext = transb ? (N - 1) * ldb + K : (K - 1) * ldb + N;
+  if (a_ext * 4 >= ((int64_t)1 << 32) - 64 || b_ext * 4 >= ((int64_t)1 << 32) - 64) return false;
   return al16(A) && lda % 4 == 0 && (transa ? M : K) % 4 == 0 && al16(B) && ldb % 4 == 0 &&
          (transb ? K : N) % 4 == 0 && N % 4 == 0 &&
          (split ? al16(ws) : (al16(C) && ldc % 4 == 0)) && (!ep->bias || al16(ep->bias)) &&
@@ -922,6 +927,41 @@ __global__ __launch_bounds__(256) void splitk_reduce_batch_kernel(BatchArgs a) {
 }  // namespace
 
 extern "C" {
+
+int pg_gemm_f32_cat(int transb, int64_t M, int64_t N, int64_t K1, int64_t K2, float alpha, const float* A1,
+                    int64_t lda1, const float* A2, int64_t lda2, const float* B1, int64_t ldb1, const float* B2,
+                    int64_t ldb2, float beta, float* C, int64_t ldc, const pg_gemm_epilogue_t* ep,
+                    pg_stream_t stream) {
+  const pg_gemm_epilogue_t none{nullptr, PG_ACT_NONE, 0.f, nullptr, 0, nullptr};
+  if (!ep) ep = &none;
+  const int64_t K = K1 + K2;
+  if (M < 0 || N < 0 || K1 < 0 || K2 < 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32_cat: bad sizes");
+  if (ldc < N || lda1 < K1 || lda2 < K2 || (transb ? (ldb1 < K1 || ldb2 < K2) : (ldb1 < N || ldb2 < N)))
+    return pg::set_error(PG_ERR_INVALID, "pg_gemm_f32_cat: leading dimension too small");
+  if (ep->act != PG_ACT_NONE && ep->act != PG_ACT_LEAKY)
+    return pg::set_error(PG_ERR_UNSUPPORTED, "pg_gemm_f32_cat: act none or leaky");
+  if (ep->dact || ep->rowsum)
+    return pg::set_error(PG_ERR_UNSUPPORTED, "pg_gemm_f32_cat: no dact / rowsum epilogue");
+  if (M == 0 || N == 0) return pg::ok();
+  if (K1 % 4 != 0 || K2 <= 0 || K1 <= 0 ||
+      !x3_ok(0, transb, M, N, K1, A1, lda1, B1, ldb1, C, ldc, ep, false, nullptr) ||
+      !x3_ok(0, transb, M, N, K2, A2, lda2, B2, ldb2, C, ldc, ep, false, nullptr))
+    return pg::set_error(PG_ERR_UNSUPPORTED,
+                         "pg_gemm_f32_cat: needs K1 %% 4 == 0 and operands the three-piece kernel takes");
+  int bm, bn;
+  pick_tile_x3(M, N, K, 1, bm, bn);
+  const int tiles_n = (int)((N + bn - 1) / bn);
+  const int tiles = tiles_n * (int)((M + bm - 1) / bm);
+  const int epi = ep->act == PG_ACT_LEAKY ? EPI_LEAKY : EPI_NONE;
+  const X3Args xa{false, transb != 0, bm, bn, epi, (int)M, (int)N, (int)K, (int)K, tiles_n, tiles, 1, alpha, A1,
+                  lda1, B1, ldb1, beta, C, ldc, ep->bias, ep->slope, nullptr, 0, nullptr, nullptr, nullptr};
+  const int rc = gemm_x3_cat_launch(xa, A2, lda2, B2, ldb2, (int)K1, (hipStream_t)stream);
+  const hipError_t e = hipGetLastError();
+  if (rc != PG_OK || e != hipSuccess)
+    return pg::set_error(rc != PG_OK ? rc : (int)e, "pg_gemm_f32_cat: launch failed");
+  return pg::ok();
+}
 
 int pg_gemm_f32(int transa, int transb, int64_t M, int64_t N, int64_t K, float alpha,
                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,

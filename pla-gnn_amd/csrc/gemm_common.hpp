@@ -148,11 +148,18 @@ struct X3Args {
   float* ws_rowsum;
 };
 int gemm_x3_launch(const X3Args& a, hipStream_t st);
+// The same with both operands concatenated along K: op(A) = [A | A2], op(B) = [B ; B2]
+// (k < kcat from the first; kcat a multiple of 4; no split-K; ta = false; EPI_NONE or
+// EPI_LEAKY).
+int gemm_x3_cat_launch(const X3Args& a, const float* A2, int64_t lda2, const float* B2, int64_t ldb2, int kcat,
+                       hipStream_t st);
 
-// Grouped split-K partials (pg_gemm_f32_group): one tile shape (128 x 128 measured best) and
-// one (ta, tb) for the group.
+// Grouped split-K partials (pg_gemm_f32_group): one tile shape and one (ta, tb) for the
+// group. 128 x 256 (two workgroups per CU, each wave 64 x 128: a third less staging per
+// MFMA than 128 x 128): cfg2 GEMM 0.796 -> 0.790 ms per step, cfg3 1.867 -> 1.857
+// (scripts/ab_lib.sh, round 5); 128 x 64 was slower in round 4.
 #ifndef PG_X3_GROUP_TILE
-#define PG_X3_GROUP_TILE 128128  // variant builds: BM * 1000 + BN
+#define PG_X3_GROUP_TILE 128256  // variant builds: BM * 1000 + BN
 #endif
 constexpr int kX3GroupBM = PG_X3_GROUP_TILE / 1000, kX3GroupBN = PG_X3_GROUP_TILE % 1000;
 struct X3Part {

@@ -95,6 +95,21 @@ __device__ __forceinline__ void split4(const float4 v, uint2 (&out)[3]) {
 // = (k, 4 rows).
 __device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written; read as a float4
 
+#ifndef PG_X3_BUFLOAD
+#define PG_X3_BUFLOAD 1  // K tiles by buffer loads with per-unit 32-bit offsets (0: 64-bit addresses)
+#endif
+
+// One operand's buffer descriptor (wave-uniform: built from readfirstlane'd inputs, so the
+// compiler keeps it in SGPRs) covering `bytes` from P; every byte offset of the operand is
+// below 2^32 (x3_ok checks the extent on the host).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t x3_rsrc(const float* P, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(P);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* base = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr uint32_t kX3Oob = 0xFFFFFFF0u;  // a byte offset past every descriptor's range: reads 0
+
 template <int ROWS, bool KMAJ>
 struct Stage {
   static constexpr int UNITS = ROWS * KS / 4;
@@ -111,6 +126,34 @@ struct Stage {
       row = (q % (ROWS / 4)) << 2;
     }
   }
+#if PG_X3_BUFLOAD
+  template <typename Addr>
+  __device__ __forceinline__ void load(const Addr& a, __amdgpu_buffer_rsrc_t rs, uint32_t step_bytes, int kt, int kz1) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const uint32_t o = kt + a.kq(i) < kz1 ? a.off(i) + step_bytes : kX3Oob;
+      v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0));
+    }
+  }
+  // K-concatenated operand: k < kcat from the first, the rest from the second (kcat a
+  // multiple of 4, so no unit straddles it; a K step may). Each unit loads through both
+  // descriptors, the one it does not use at an out-of-range offset (zeros), and ORs the
+  // bits: exact.
+  template <typename Addr>
+  __device__ __forceinline__ void load_cat(const Addr& a1, const Addr& a2, __amdgpu_buffer_rsrc_t rs1,
+                                           __amdgpu_buffer_rsrc_t rs2, uint32_t step1, uint32_t step2,
+                                           int kcat, int kt, int kz1) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = kt + a1.kq(i);
+      const uint32_t o1 = k < kcat && k < kz1 ? a1.off(i) + step1 : kX3Oob;
+      const uint32_t o2 = k >= kcat && k < kz1 ? a2.off(i) + step2 : kX3Oob;
+      const uint4 x = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs1, (int)o1, 0, 0));
+      const uint4 y = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs2, (int)o2, 0, 0));
+      v[i] = __builtin_bit_cast(float4, make_uint4(x.x | y.x, x.y | y.y, x.z | y.z, x.w | y.w));
+    }
+  }
+#else
   // rows past R read a clamped valid row (never stored); k past kz1 read as 0
   __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int r0, int R, int k0,
                                        int kz1, int tid) {
@@ -127,6 +170,7 @@ struct Stage {
       v[i] = *reinterpret_cast<const float4*>(gk < kz1 ? p : g_zero4);
     }
   }
+#endif
   // split and store the three pieces (images of IMG u16 each, consecutive)
   template <int IMG>
   __device__ __forceinline__ void store(uint16_t* __restrict__ S, int tid) const {
@@ -155,6 +199,47 @@ struct Stage {
     }
   }
 };
+
+#if PG_X3_BUFLOAD
+// A K tile's addressing, set up once per tile (shared by the register slots of a deeper
+// pipeline): the byte offset of each unit at the slice's first k (rows past R clamped to a
+// valid row, never stored) and its k within a K step. A step then costs one add, one
+// compare and one select per unit (a unit at or past kz1 reads through an out-of-range
+// offset: zeros), no 64-bit address arithmetic.
+template <int ROWS, bool KMAJ>
+struct StageAddr {
+  static constexpr int PER = Stage<ROWS, KMAJ>::PER;
+  // k image: unit i of a thread sits KQS k-rows below unit 0 in the same 4 rows, so one
+  // offset and a wave-uniform stride describe them all; row image: every unit its own row
+  // (clamped), one k
+  static constexpr int KQS = KMAJ ? NT / (ROWS / 4) : 0;
+  static constexpr int NOFF = KMAJ ? 1 : PER;
+  uint32_t off_[NOFF];
+  uint32_t ustride;  // KMAJ: bytes between consecutive units (wave-uniform)
+  int kq0;
+  __device__ __forceinline__ void setup(int64_t ld, int r0, int R, int k0, int tid) {
+    int row, k;
+    Stage<ROWS, KMAJ>::unit_pos(tid, row, k);
+    kq0 = k;
+    if constexpr (KMAJ) {
+      off_[0] = ((uint32_t)(k0 + k) * (uint32_t)ld + (uint32_t)min(r0 + row, R - 4)) * 4u;
+      ustride = (uint32_t)KQS * (uint32_t)ld * 4u;
+    } else {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        Stage<ROWS, KMAJ>::unit_pos(tid + i * NT, row, k);
+        off_[i] = ((uint32_t)min(r0 + row, R - 1) * (uint32_t)ld + (uint32_t)(k0 + k)) * 4u;
+      }
+      ustride = 0;
+    }
+  }
+  __device__ __forceinline__ uint32_t off(int i) const {
+    if constexpr (KMAJ) return off_[0] + (uint32_t)i * ustride;
+    else return off_[i];
+  }
+  __device__ __forceinline__ int kq(int i) const { return kq0 + i * KQS; }
+};
+#endif
 
 // The accumulator tile leaves through LDS in PASSES row bands (16-B stores), with the
 // epilogue (alpha, beta C, bias, act / act', or the split-K partial slab).
@@ -273,7 +358,9 @@ constexpr int x3_depth() { return BM * BN <= 128 * 64 ? 2 : 1; }
 #define PG_X3_WAVES_BIG 3
 #endif
 template <int BM, int BN>
-constexpr int x3_waves() { return x3_depth<BM, BN>() == 2 ? 4 : PG_X3_WAVES_BIG; }
+constexpr int x3_waves() {
+  return x3_depth<BM, BN>() == 2 ? 4 : BM * BN <= 128 * 128 ? PG_X3_WAVES_BIG : 2;
+}
 
 template <int BM, int BN>
 constexpr int x3_lds_u16() {
@@ -284,13 +371,23 @@ constexpr int x3_lds_u16() {
 }
 
 // One output tile (tm, tn) over the K slice kz of the product: the whole workgroup's work.
-template <int BM, int BN, bool TA, bool TB, int EPI>
+// KCAT: both operands are concatenations along K, [A | A2] and [B ; B2] (op(B)), split at
+// k = cat.kcat (a multiple of 4; no split-K): the drop-in layer's [H | M] [Wself | Wneigh]^T
+// and [dY | dP] [Wself ; Wpool] without building the concatenations.
+struct X3Cat {
+  const float* A2;
+  int64_t lda2;
+  const float* B2;
+  int64_t ldb2;
+  int kcat;
+};
+template <int BM, int BN, bool TA, bool TB, int EPI, bool KCAT = false>
 __device__ __forceinline__ void x3_tile(
     uint16_t* __restrict__ lds, int M, int N, int K, int k_per_split, int kz, int tm, int tn, float alpha,
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
     float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
     const float* __restrict__ dact, int64_t lddact, float* __restrict__ rowsum,
-    float* __restrict__ ws, float* __restrict__ ws_rowsum) {
+    float* __restrict__ ws, float* __restrict__ ws_rowsum, X3Cat cat = {}) {
   constexpr bool AK = TA, BKM = !TB;
   constexpr bool SPLIT = EPI == EPI_SPLIT;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -317,6 +414,55 @@ __device__ __forceinline__ void x3_tile(
 
   Stage<BM, AK> sa;
   Stage<BN, BKM> sb;
+  static_assert(!KCAT || PG_X3_BUFLOAD, "K-concatenated operands need the buffer-load addressing");
+#if PG_X3_BUFLOAD
+  // operand extents in bytes (row image: R rows of ld; k image: K rows of ld)
+  const uint32_t a_bytes = (uint32_t)(AK ? ((int64_t)(K - 1) * lda + M) * 4 : ((int64_t)(M - 1) * lda + K) * 4);
+  const uint32_t b_bytes = (uint32_t)(BKM ? ((int64_t)(K - 1) * ldb + N) * 4 : ((int64_t)(N - 1) * ldb + K) * 4);
+  const __amdgpu_buffer_rsrc_t rsa = x3_rsrc(A, a_bytes), rsb = x3_rsrc(B, b_bytes);
+  const uint32_t a_kstride = AK ? (uint32_t)lda * 4u : 4u, b_kstride = BKM ? (uint32_t)ldb * 4u : 4u;
+  StageAddr<BM, AK> aa;
+  StageAddr<BN, BKM> ab;
+  aa.setup(lda, m0, M, kz0, tid);
+  ab.setup(ldb, n0, N, kz0, tid);
+  // KCAT: the second operands' addressing (their own k starts at 0 where the first ends)
+  StageAddr<BM, AK> aa2;
+  StageAddr<BN, BKM> ab2;
+  __amdgpu_buffer_rsrc_t rsa2 = rsa, rsb2 = rsb;
+  uint32_t a2_kstride = 0, b2_kstride = 0;
+  if constexpr (KCAT) {
+    const int K2 = K - cat.kcat;
+    const uint32_t a2_bytes =
+        (uint32_t)(AK ? ((int64_t)(K2 - 1) * cat.lda2 + M) * 4 : ((int64_t)(M - 1) * cat.lda2 + K2) * 4);
+    const uint32_t b2_bytes =
+        (uint32_t)(BKM ? ((int64_t)(K2 - 1) * cat.ldb2 + N) * 4 : ((int64_t)(N - 1) * cat.ldb2 + K2) * 4);
+    rsa2 = x3_rsrc(cat.A2, a2_bytes);
+    rsb2 = x3_rsrc(cat.B2, b2_bytes);
+    a2_kstride = AK ? (uint32_t)cat.lda2 * 4u : 4u;
+    b2_kstride = BKM ? (uint32_t)cat.ldb2 * 4u : 4u;
+    aa2.setup(cat.lda2, m0, M, 0, tid);
+    ab2.setup(cat.ldb2, n0, N, 0, tid);
+  }
+  auto load_a = [&](Stage<BM, AK>& st, int kt) {
+    if constexpr (KCAT) {
+      st.load_cat(aa, aa2, rsa, rsa2, (uint32_t)(kt - kz0) * a_kstride, (uint32_t)(kt - cat.kcat) * a2_kstride,
+                  cat.kcat, kt, kz1);
+    } else {
+      st.load(aa, rsa, (uint32_t)(kt - kz0) * a_kstride, kt, kz1);
+    }
+  };
+  auto load_b = [&](Stage<BN, BKM>& st, int kt) {
+    if constexpr (KCAT) {
+      st.load_cat(ab, ab2, rsb, rsb2, (uint32_t)(kt - kz0) * b_kstride, (uint32_t)(kt - cat.kcat) * b2_kstride,
+                  cat.kcat, kt, kz1);
+    } else {
+      st.load(ab, rsb, (uint32_t)(kt - kz0) * b_kstride, kt, kz1);
+    }
+  };
+#else
+  auto load_a = [&](Stage<BM, AK>& st, int kt) { st.load(A, lda, m0, M, kt, kz1, tid); };
+  auto load_b = [&](Stage<BN, BKM>& st, int kt) { st.load(B, ldb, n0, N, kt, kz1, tid); };
+#endif
   double rs[Stage<BM, AK>::RSN];
 #pragma unroll
   for (int i = 0; i < Stage<BM, AK>::RSN; ++i) rs[i] = 0.0;
@@ -353,11 +499,11 @@ __device__ __forceinline__ void x3_tile(
     // earlier instead of during the same step's MFMAs)
     Stage<BM, AK> sa2;
     Stage<BN, BKM> sb2;
-    sa.load(A, lda, m0, M, kz0, kz1, tid);
-    sb.load(B, ldb, n0, N, kz0, kz1, tid);
+    load_a(sa, kz0);
+    load_b(sb, kz0);
     const int k1c = kz0 + min(1, nk - 1) * KS;
-    sa2.load(A, lda, m0, M, k1c, kz1, tid);
-    sb2.load(B, ldb, n0, N, k1c, kz1, tid);
+    load_a(sa2, k1c);
+    load_b(sb2, k1c);
     if (do_rs) sa.rowsum(rs);
     sa.template store<IA>(lds, tid);
     sb.template store<IB>(lds + 3 * IA, tid);
@@ -367,8 +513,8 @@ __device__ __forceinline__ void x3_tile(
     auto kstep = [&](int t, Stage<BM, AK>& la, Stage<BN, BKM>& lb, Stage<BM, AK>& na, Stage<BN, BKM>& nb) {
       const int cur = t & 1;
       const int kl = kz0 + min(t + 2, nk - 1) * KS;
-      la.load(A, lda, m0, M, kl, kz1, tid);
-      lb.load(B, ldb, n0, N, kl, kz1, tid);
+      load_a(la, kl);
+      load_b(lb, kl);
       if (t < nk) {
         const uint16_t* As = lds + cur * BUF;
         mfmas(As, As + 3 * IA);
@@ -387,8 +533,8 @@ __device__ __forceinline__ void x3_tile(
     }
   } else if (nk > 0) {
     X3_STAMP(0, 0);
-    sa.load(A, lda, m0, M, kz0, kz1, tid);
-    sb.load(B, ldb, n0, N, kz0, kz1, tid);
+    load_a(sa, kz0);
+    load_b(sb, kz0);
     if (do_rs) sa.rowsum(rs);
     sa.template store<IA>(lds, tid);
     sb.template store<IB>(lds + 3 * IA, tid);
@@ -398,8 +544,8 @@ __device__ __forceinline__ void x3_tile(
       const bool more = t + 1 < nk;
       X3_STAMP(t + 1, 0);
       if (more) {
-        sa.load(A, lda, m0, M, kz0 + (t + 1) * KS, kz1, tid);
-        sb.load(B, ldb, n0, N, kz0 + (t + 1) * KS, kz1, tid);
+        load_a(sa, kz0 + (t + 1) * KS);
+        load_b(sb, kz0 + (t + 1) * KS);
       }
       const uint16_t* As = lds + cur * BUF;
       mfmas(As, As + 3 * IA);
@@ -478,6 +624,20 @@ void gemm_x3_kernel(
                                ldb, beta, C, ldc, bias, slope, dact, lddact, rowsum, ws, ws_rowsum);
 }
 
+// K-concatenated operands (X3Cat), no split-K: the drop-in layers' products
+template <int BM, int BN, bool TA, bool TB, int EPI>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_waves<BM, BN>())))
+void gemm_x3_cat_kernel(
+    int M, int N, int K, int tiles_n, int tiles, float alpha,
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
+    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, float slope,
+    const float* __restrict__ dact, int64_t lddact, X3Cat cat) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[x3_lds_u16<BM, BN>()];
+  const int tile = x3_item(tiles);
+  x3_tile<BM, BN, TA, TB, EPI, true>(lds, M, N, K, K, 0, tile / tiles_n, tile % tiles_n, alpha, A, lda, B, ldb, beta, C,
+                                     ldc, bias, slope, dact, lddact, nullptr, nullptr, nullptr, cat);
+}
+
 // Grouped split-K partials: the items of every part (its tiles x its K slices, slice-major)
 // laid end to end, one launch for all of them (the step's weight gradients: the slab bytes
 // then scale with the group's workgroups, not with each product's).
@@ -541,6 +701,39 @@ int gemm_x3_group_launch(const X3Group& g, bool ta, bool tb, hipStream_t st) {
 #undef PG_G
   return PG_OK;
 }
+
+#if PG_X3_BUFLOAD
+template <int BM, int BN>
+int launch_cat(const X3Args& a, const X3Cat& c, hipStream_t st) {
+  if (a.ta || (a.epi != EPI_NONE && a.epi != EPI_LEAKY)) return PG_ERR_UNSUPPORTED;
+  const dim3 grid((unsigned)a.tiles), block(NT);
+#define PG_C(TB_, EPI_)                                                                                  \
+  hipLaunchKernelGGL((gemm_x3_cat_kernel<BM, BN, false, TB_, EPI_>), grid, block, 0, st, a.M, a.N, a.K, \
+                     a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb, a.beta, a.C, a.ldc, a.bias, a.slope, \
+                     a.dact, a.lddact, c)
+  if (a.tb) {
+    if (a.epi == EPI_NONE) PG_C(true, EPI_NONE); else PG_C(true, EPI_LEAKY);
+  } else {
+    if (a.epi == EPI_NONE) PG_C(false, EPI_NONE); else PG_C(false, EPI_LEAKY);
+  }
+#undef PG_C
+  return PG_OK;
+}
+
+int gemm_x3_cat_launch(const X3Args& a, const float* A2, int64_t lda2, const float* B2, int64_t ldb2, int kcat,
+                       hipStream_t st) {
+  const X3Cat c{A2, lda2, B2, ldb2, kcat};
+  if (a.bm == 128 && a.bn == 128) return launch_cat<128, 128>(a, c, st);
+  if (a.bm == 128 && a.bn == 64) return launch_cat<128, 64>(a, c, st);
+  if (a.bm == 64 && a.bn == 128) return launch_cat<64, 128>(a, c, st);
+  if (a.bm == 64 && a.bn == 64) return launch_cat<64, 64>(a, c, st);
+  return PG_ERR_INVALID;
+}
+#else
+int gemm_x3_cat_launch(const X3Args&, const float*, int64_t, const float*, int64_t, int, hipStream_t) {
+  return PG_ERR_UNSUPPORTED;
+}
+#endif
 
 int gemm_x3_launch(const X3Args& a, hipStream_t st) {
   if (a.bm == 128 && a.bn == 128) return launch_trans<128, 128>(a, st);

@@ -420,15 +420,43 @@ __global__ __launch_bounds__(kBlock) void max_bwd_kernel(
 // 4-B slot and destination (coalesced), one 4-B descriptor (random; 8 B {v F + start,
 // count} before: twice the footprint for the caches to hold) and one short contiguous run
 // of records (~F/deg entries).
-// (Descriptors stored at the transposed index instead, read coalesced but written
-// scattered by the pack: pull 35.6 vs 43.5 us, pack 28.3 vs 15.9 us at F = 256, no gain.
-// A source-ordered record layout, DESIGN.md §7, measured slower still.)
+// Transposed descriptors (round 5; when the caller gives the in-CSR slots' transposed
+// indices, g->epos): the descriptor of slot s is stored at its transposed index einv[s],
+// and only for edges that win something (about half win nothing: their descriptors stay
+// the zero the launch clears the array to). The pull then reads its out-edges' descriptors
+// in order, coalesced, and fetches lists only for the edges that have one: one random
+// access per live edge instead of two per edge. (Round 3 stored every descriptor at the
+// transposed index, empty ones included: pull 35.6 vs 43.5 us, pack 28.3 vs 15.9 us at
+// F = 256, no gain. A source-ordered record layout, DESIGN.md §7, measured slower still.)
 constexpr int kHistMax = 4096;
 constexpr int kGroupMaxF = 1024;  // (starts and counts <= F fit the descriptor's 16-bit halves)
 
 __device__ __forceinline__ uint32_t desc_make(int start, int count) {
   return (uint32_t)start | ((uint32_t)count << 16);
 }
+
+// Where the pack puts a descriptor: at the in-CSR slot (TR = false), or at the slot's
+// transposed index when the list is not empty (TR = true; the array was cleared first).
+template <bool TR>
+struct DescOut {
+  uint32_t* glist;
+  const int32_t* einv;
+  // the transposed index of slot s, loaded ahead of the write (TR only)
+  __device__ __forceinline__ int pre(int s) const {
+    if constexpr (TR) return einv[s];
+    else return s;
+  }
+  __device__ __forceinline__ void put(int pre_s, int start, int count) const {
+    if constexpr (TR) {
+      if (count > 0) glist[pre_s] = desc_make(start, count);
+    } else {
+      glist[pre_s] = desc_make(start, count);
+    }
+  }
+};
+#ifndef PG_BWD_TRANS
+#define PG_BWD_TRANS 1  // variant builds: 0 keeps the descriptors at the in-CSR slots
+#endif
 #ifndef PG_BWD_DIRECT
 #define PG_BWD_DIRECT 0
 #endif
@@ -513,11 +541,11 @@ __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   return total;
 }
 
-template <typename A, typename T, typename R>
+template <typename A, typename T, typename R, typename D>
 __device__ __forceinline__ void pack_short_row(
     int v, int wave, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, D dsc,
     int* __restrict__ lds) {
   constexpr int MAXW = kGroupMaxF / kWave;  // features per lane
   const int lane = lane_id();
@@ -551,7 +579,7 @@ __device__ __forceinline__ void pack_short_row(
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int p = lane * B + q;
-    ei[q] = (q < B && p < deg) ? rs + p : 0;
+    ei[q] = dsc.pre((q < B && p < deg) ? rs + p : rs);
   }
   int* hist = lds + wave * (kPackWaveMax + 4);
   for (int p = lane; p < deg; p += kWave) hist[p] = 0;
@@ -577,7 +605,7 @@ __device__ __forceinline__ void pack_short_row(
     const int p = lane * B + q;
     if (q < B && p < deg) {
       hist[p] = run;
-      glist[ei[q]] = desc_make(run, c[q]);
+      dsc.put(ei[q], run, c[q]);
       run += c[q];
     }
   }
@@ -601,11 +629,11 @@ __device__ __forceinline__ void pack_short_row(
 template <int NV>
 constexpr int pack_wave_ints() { return kPackWaveMax + 4 + NV * 512; }  // hist | records (8 B)
 
-template <int NV, typename A, typename T, typename R>
+template <int NV, typename A, typename T, typename R, typename D>
 __device__ __forceinline__ void pack_short_row_v(
     int v, int wave, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, D dsc,
     int* __restrict__ lds) {
   const int lane = lane_id();
   const int rs = ptr[v];
@@ -644,7 +672,7 @@ __device__ __forceinline__ void pack_short_row_v(
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int p = lane * B + q;
-    ei[q] = (q < B && p < deg) ? rs + p : 0;
+    ei[q] = dsc.pre((q < B && p < deg) ? rs + p : rs);
   }
   int* hist = lds + wave * pack_wave_ints<NV>();
   typename R::W* lr = reinterpret_cast<typename R::W*>(hist + kPackWaveMax + 4);  // 16-B aligned: 260 ints
@@ -674,7 +702,7 @@ __device__ __forceinline__ void pack_short_row_v(
     const int p = lane * B + q;
     if (q < B && p < deg) {
       hist[p] = run;
-      glist[ei[q]] = desc_make(run, cq[q]);
+      dsc.put(ei[q], run, cq[q]);
       run += cq[q];
     }
   }
@@ -707,11 +735,11 @@ __device__ __forceinline__ void pack_short_row_v(
   }
 }
 
-template <typename A, typename T, typename R>
+template <typename A, typename T, typename R, typename D>
 __device__ __forceinline__ void pack_long_row(
     int v, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
-    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist,
+    const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, D dsc,
     int* __restrict__ lds) {
   int* hist = lds;
   uint16_t* feats = reinterpret_cast<uint16_t*>(lds + kHistMax + 8);
@@ -756,7 +784,7 @@ __device__ __forceinline__ void pack_long_row(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int p = p0 + j * kBlock;
-        e[j] = p < deg ? rs + p : 0;
+        e[j] = dsc.pre(p < deg ? rs + p : rs);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -764,7 +792,7 @@ __device__ __forceinline__ void pack_long_row(
         if (p < deg) {
           const int st = hist[p];
           const int en = p + 1 < deg ? hist[p + 1] : total;
-          glist[e[j]] = desc_make(st, en - st);
+          dsc.put(e[j], st, en - st);
         }
       }
     }
@@ -814,9 +842,10 @@ __device__ __forceinline__ void pack_long_row(
       return lo;
     };
     for (int p = threadIdx.x; p < deg; p += kBlock) {
+      const int es = dsc.pre(rs + p);
       const int st = lower((uint32_t)p << 16);
       const int en = lower((uint32_t)(p + 1) << 16);
-      glist[rs + p] = desc_make(st, en - st);
+      dsc.put(es, st, en - st);
     }
     if (threadIdx.x == 0) wsum[0] = lower(0xFFFFFFFFu);
     __syncthreads();
@@ -839,27 +868,28 @@ __device__ __forceinline__ void pack_long_row(
 constexpr int kPackLds = kHistMax + 8 + kGroupMaxF / 2 + 4;
 static_assert(kPackLds >= kWavesPerBlock * (kPackWaveMax + 4), "pack LDS");
 
-template <typename A, typename T, int NV, typename R>
+template <typename A, typename T, int NV, typename R, bool TR>
 __global__ __launch_bounds__(kBlock) void group_pack_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F,
     const T* __restrict__ dout, int64_t ldd, const T* __restrict__ fout, int64_t ldf,
-    const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist) {
+    const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist, const int32_t* __restrict__ einv) {
+  const DescOut<TR> dsc{glist, einv};
   constexpr int kLds = NV > 0 && kWavesPerBlock * pack_wave_ints<NV>() > kPackLds
                            ? kWavesPerBlock * pack_wave_ints<NV>() : kPackLds;
   __shared__ __attribute__((aligned(16))) int lds[kLds];
   const int b = blockIdx.x;
   if (b < n_long) {
-    pack_long_row<A, T, R>(rows ? rows[b].x : b, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
+    pack_long_row<A, T, R>(rows ? rows[b].x : b, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, dsc, lds);
   } else {
     const int wave = wave_id_uniform();
     const int v = (b - n_long) * kWavesPerBlock + wave;
     if (v < n_rows)
     {
       if constexpr (NV > 0)
-        pack_short_row_v<NV, A, T, R>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
+        pack_short_row_v<NV, A, T, R>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, dsc, lds);
       else
-        pack_short_row<A, T, R>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, glist, lds);
+        pack_short_row<A, T, R>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, dsc, lds);
     }
   }
 }
@@ -879,7 +909,7 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
 // rate on gfx950: scripts/probes/lds_rmw_probe.hip), measured slower on the engine's data:
 // a source that wins a feature at many destinations puts it many times into one segment,
 // and the swaps serialise.
-template <typename T, typename R>
+template <typename T, typename R, bool TR>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
     const int32_t* __restrict__ tdst, const uint32_t* __restrict__ glist, R gp, int F,
@@ -900,19 +930,20 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   auto tl_of = [&](int tw) { return tw + min(lane, t1 - tw - 1); };
   uint32_t dsc_next = 0;
   int vf_next = 0, ts_next = 0;
+  // TR: the descriptors sit at the transposed indices themselves (coalesced, no slot loads)
   if (t1 > t0) {
-    dsc_next = glist[tslot[tl_of(t0)]];
+    dsc_next = glist[TR ? tl_of(t0) : tslot[tl_of(t0)]];
     vf_next = tdst[tl_of(t0)] * F;
-    if (t0 + kWave < t1) ts_next = tslot[tl_of(t0 + kWave)];
+    if (!TR && t0 + kWave < t1) ts_next = tslot[tl_of(t0 + kWave)];
   }
   for (int tw = t0; tw < t1; tw += kWave) {
     const int nw = min(kWave, t1 - tw);
     // this window's edge (lane): its list's first record and its length
     const int2 dsc = make_int2(vf_next + (int)(dsc_next & 0xFFFFu), (int)(dsc_next >> 16));
     if (tw + kWave < t1) {
-      dsc_next = glist[ts_next];
+      dsc_next = glist[TR ? tl_of(tw + kWave) : ts_next];
       vf_next = tdst[tl_of(tw + kWave)] * F;
-      if (tw + 2 * kWave < t1) ts_next = tslot[tl_of(tw + 2 * kWave)];
+      if (!TR && tw + 2 * kWave < t1) ts_next = tslot[tl_of(tw + 2 * kWave)];
     }
     // segments: 64-entry pieces of single lists, U segments' loads in flight. Segment t
     // belongs to the edge i with excl_i <= t < excl_i + nseg_i, i.e.
@@ -1094,6 +1125,11 @@ __global__ __launch_bounds__(kBlock) void sum_kernel(
 }
 
 // ---- DGL-form scatter backward (float atomics) ----------------------------------------
+__global__ __launch_bounds__(kBlock) void clear_u4_kernel(uint4* __restrict__ x, int64_t n4) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock)
+    x[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 __global__ __launch_bounds__(kBlock) void fill2d_kernel(float* __restrict__ x, int64_t ldx,
                                                         int64_t rows, int cols, float val) {
   const int64_t n = rows * (int64_t)cols;
@@ -1446,12 +1482,23 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
                      ((uintptr_t)argpos & 7) == 0 && ((uintptr_t)dout & kTa) == 0 && ((uintptr_t)fwd_out & kTa) == 0;
     const dim3 pgrid((unsigned)(n_long + n_short_blocks));
     const int4* prow = listed ? (const int4*)g->merges : nullptr;
-    auto run = [&](auto gp) {
+    // transposed descriptors when the in-CSR slots' transposed indices are given (g->epos)
+    const bool tr = g->epos != nullptr && PG_BWD_TRANS && ((uintptr_t)glist & 15) == 0;
+    // cleared by a kernel of this library, not hipMemsetAsync: a memset issued while the
+    // stream is being captured into a HIP graph did not clear the array on replays (the
+    // engine's step graph trained on stale descriptors)
+    if (tr && g->nnz > 0) {
+      const int64_t n4 = (g->nnz + 3) / 4;  // glist is 256-B aligned and padded: whole uint4s
+      hipLaunchKernelGGL(clear_u4_kernel, dim3((unsigned)std::min<int64_t>(2048, (n4 + kBlock - 1) / kBlock)),
+                         dim3(kBlock), 0, st, reinterpret_cast<uint4*>(glist), n4);
+    }
+    auto run = [&](auto gp, auto tr_c) {
     using R = decltype(gp);
+    constexpr bool TR = decltype(tr_c)::value;
     auto pack = [&](auto nv_c) {
       constexpr int NV = decltype(nv_c)::value;
-      hipLaunchKernelGGL((group_pack_kernel<uint16_t, T, NV, R>), pgrid, dim3(kBlock), 0, st, prow, n_long, (int)N,
-                         g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, g->ew, gp, glist);
+      hipLaunchKernelGGL((group_pack_kernel<uint16_t, T, NV, R, TR>), pgrid, dim3(kBlock), 0, st, prow, n_long,
+                         (int)N, g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, g->ew, gp, glist, g->epos);
       return PG_OK;
     };
     if (vec) dispatch_nc_vec((int)((F + 255) / 256), pack);
@@ -1461,7 +1508,7 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     // in the lists has a maximum X[u,f] w != 0, so X[u,f] > 0; an element with no entries
     // sums to +0, which the mask would leave +0. With fwd_out alone the mask is applied.
     if (dead_none) mask_src = nullptr;
-    hipLaunchKernelGGL((max_bwd_pull_kernel<T, R>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
+    hipLaunchKernelGGL((max_bwd_pull_kernel<T, R, TR>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
                        (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
                        dx, ldx, w, ws_ld(F));
     if (gt->n_merges > 0)
@@ -1469,14 +1516,18 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
                          (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
                          mask_src, ldm, dx, ldx);
     };
+    auto run_tr = [&](auto gp) {
+      if (tr) run(gp, std::true_type{});
+      else run(gp, std::false_type{});
+    };
     if (sizeof(T) == 2 && !g->ew) {
       GPack4 gp;
       gp.r = (uint32_t*)recs;
-      run(gp);
+      run_tr(gp);
     } else {
       GPack gp;
       gp.r = (uint2*)recs;
-      run(gp);
+      run_tr(gp);
     }
     return hip_status("pg_spmm_max_bwd");
   }

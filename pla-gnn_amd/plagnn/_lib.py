@@ -13,7 +13,7 @@ import warnings
 import torch  # noqa: F401  (load order: see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 9  # pg_version() of the library this package binds (include/plagnn.h)
+ABI_VERSION = 10  # pg_version() of the library this package binds (include/plagnn.h)
 # PLAGNN_LIB overrides the library path (A/B builds of tuning variants)
 LIB_PATH = os.environ.get("PLAGNN_LIB") or os.path.join(_HERE, "libplagnn.so")
 
@@ -157,6 +157,8 @@ SIGNATURES = {
     "pg_gemm_f32_workspace": (_sz, [_i64, _i64, _i64, _i]),
     "pg_gemm_f32": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _ep,
                          _i, _vp, _sz, _vp]),
+    "pg_gemm_f32_cat": (_i, [_i, _i64, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _f, _vp,
+                             _i64, _ep, _vp]),
     "pg_gemm_bf16_split_k": (_i, [_i64, _i64, _i64]),
     "pg_gemm_bf16_workspace": (_sz, [_i64, _i64, _i64, _i]),
     "pg_gemm_bf16": (_i, [_i, _i, _i64, _i64, _i64, _f, _vp, _i64, _vp, _i64, _f, _vp, _i64, _i, _ep,

@@ -235,6 +235,32 @@ def gemm(A: torch.Tensor, B: torch.Tensor, transa: bool = False, transb: bool = 
     return out
 
 
+PG_ERR_UNSUPPORTED = -2
+
+
+def gemm_cat(A1: torch.Tensor, A2: torch.Tensor, B1: torch.Tensor, B2: torch.Tensor, transb: bool = False,
+             out: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+             act: int = _lib.PG_ACT_NONE) -> Optional[torch.Tensor]:
+    """C = [A1 | A2] @ op([B1 ; B2]) (+ bias, leaky_relu) without building either
+    concatenation (pg_gemm_f32_cat, GPU). Returns None when the library does not take these
+    operands (PG_ERR_UNSUPPORTED: the caller concatenates instead)."""
+    M, K1 = A1.shape
+    K2 = A2.shape[1]
+    N = B1.shape[0] if transb else B1.shape[1]
+    if A2.shape[0] != M or (B1.shape[1] if transb else B1.shape[0]) != K1 or \
+            (B2.shape[1] if transb else B2.shape[0]) != K2 or (B2.shape[0] if transb else B2.shape[1]) != N:
+        raise ValueError("gemm_cat: shapes do not concatenate")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=A1.device)
+    ep = _lib.epilogue(bias, act, LEAKY_SLOPE)
+    rc = _lib.lib().pg_gemm_f32_cat(int(transb), M, N, K1, K2, 1.0, ptr(A1), _ld(A1), ptr(A2), _ld(A2), ptr(B1),
+                                    _ld(B1), ptr(B2), _ld(B2), 0.0, ptr(out), _ld(out), ep, _stream(A1))
+    if rc == PG_ERR_UNSUPPORTED:
+        return None
+    _lib.check(rc, "pg_gemm_f32_cat")
+    return out
+
+
 def gemm_group(parts) -> None:
     """Several split-K products in one launch + one combine (pg_gemm_f32_group): each part
     (A, B, C, transa, transb, beta, rowsum) computes C = op(A) op(B) (+ C when beta = 1) and
@@ -455,6 +481,11 @@ class SagePool(torch.autograd.Function):
     def _forward_gpu(ctx, h, w_pool, b_pool, w_self, w_neigh, bias, dg, ew_slots):
         N, Fin = h.shape
         Fp = sage_width(Fin)
+        if Fp == Fin:
+            out = SagePool._forward_gpu_cat(ctx, h, w_pool, b_pool, w_self, w_neigh, bias, dg, ew_slots)
+            if out is not None:
+                return out
+        ctx.cat = False
         fpad = Fp - Fin
         keep = torch.is_grad_enabled() and any(ctx.needs_input_grad[:6])
         HM, ctx.hm_key = _hm_buffer(h, Fp, keep)
@@ -473,7 +504,66 @@ class SagePool(torch.autograd.Function):
         return Y
 
     @staticmethod
+    def _forward_gpu_cat(ctx, h, w_pool, b_pool, w_self, w_neigh, bias, dg, ew_slots):
+        """A layer whose input needs no padding (4-aligned width): H is the caller's tensor
+        and M its own buffer, fc_self + fc_neigh one product over the two K pieces
+        ([H | M] [Wself | Wneigh]^T, pg_gemm_f32_cat), no [H | M] copy and no weight
+        concatenation. None when the library does not take the operands."""
+        N, Fin = h.shape
+        w_pool, w_self, w_neigh = w_pool.contiguous(), w_self.contiguous(), w_neigh.contiguous()
+        P = torch.empty(N, Fin, dtype=torch.float32, device=h.device)
+        gemm(h, w_pool, transb=True, out=P, bias=b_pool.contiguous(), act=_lib.PG_ACT_RELU)
+        M = torch.empty(N, Fin, dtype=torch.float32, device=h.device)
+        argpos = torch.empty(N, Fin, dtype=dg.arg_dtype, device=h.device)
+        spmm_max(dg, P, ew_slots, out=M, argpos=argpos, dead_none=True)
+        Y = gemm_cat(h, M, w_self, w_neigh, transb=True, bias=bias)
+        if Y is None:
+            return None
+        ctx.gpu = ctx.cat = True
+        ctx.save_for_backward(h, M, P, argpos, w_pool, w_self, w_neigh, ew_slots)
+        ctx.fin = Fin
+        ctx.hm_key = None
+        return Y
+
+    @staticmethod
+    def _backward_gpu_cat(ctx, dY):
+        h, M, P, argpos, w_pool, w_self, w_neigh, ew_slots = ctx.saved_tensors
+        dg, Fin = ctx.dg, ctx.fin
+        dY = dY.contiguous()
+        N, Fo = dY.shape
+        need_h, need_wp, need_bp, need_ws, need_wn, need_b = ctx.needs_input_grad[:6]
+        d_b = torch.empty(Fo, dtype=torch.float32, device=dY.device) if (need_b and ctx.has_bias) else None
+        wgrads = []  # the layer's weight gradients, one grouped launch after the max backward
+        d_ws = torch.empty(Fo, Fin, dtype=torch.float32, device=dY.device) if need_ws else None
+        d_wn = torch.empty(Fo, Fin, dtype=torch.float32, device=dY.device) if need_wn else None
+        if d_ws is not None:
+            wgrads.append((dY, h, d_ws, True, False, 0.0, d_b))
+        if d_wn is not None:
+            wgrads.append((dY, M, d_wn, True, False, 0.0, d_b if d_ws is None else None))
+        if d_b is not None and not wgrads:
+            d_b = col_sum(dY)
+        dM = gemm(dY, w_neigh)
+        dP = torch.empty(N, Fin, dtype=torch.float32, device=dY.device)
+        spmm_max_backward(dg, argpos, dM, ew_slots, mask=P, dx=dP, dead_none=True)
+        d_bp = torch.empty(Fin, dtype=torch.float32, device=dY.device) if need_bp else None
+        d_wp = None
+        if need_wp:
+            d_wp = torch.empty(Fin, Fin, dtype=torch.float32, device=dY.device)
+            wgrads.append((dP, h, d_wp, True, False, 0.0, d_bp))
+        elif d_bp is not None:
+            d_bp = col_sum(dP)
+        gemm_group(wgrads)
+        d_h = None
+        if need_h:  # [dY | dP] [Wself ; Wpool] over the two K pieces
+            d_h = gemm_cat(dY, dP, w_self, w_pool)
+            if d_h is None:
+                d_h = gemm(torch.cat([dY, dP], 1), torch.cat([w_self, w_pool], 0))
+        return d_h, d_wp, d_bp, d_ws, d_wn, d_b, None, None
+
+    @staticmethod
     def backward(ctx, dY):
+        if ctx.gpu and ctx.cat:
+            return SagePool._backward_gpu_cat(ctx, dY)
         if ctx.gpu:
             return SagePool._backward_gpu(ctx, dY)
         h, w_pool, w_self, w_neigh, Pb, Mb, argpos, ew_slots = ctx.saved_tensors

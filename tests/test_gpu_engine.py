@@ -61,14 +61,15 @@ def test_shim_gnn32_on_gpu_matches_oracle(oracle_mod):
         _close(prm.grad, ref_grads[name], name=name)
 
 
-@pytest.mark.parametrize("dims", [(31, 24, 20, 16, 10, 12), (503, 64, 64, 12, 12)])
-def test_engine_step_matches_oracle(oracle_mod, dims):
+@pytest.mark.parametrize("dims,trans", [((31, 24, 20, 16, 10, 12), False), ((503, 64, 64, 12, 12), False),
+                                        ((503, 64, 64, 12, 12), True)])
+def test_engine_step_matches_oracle(oracle_mod, dims, trans):
     import plagnn
 
     src, dst, x, labels, w, tr, va, model = _problem(dims=dims)
     n = x.shape[0]
     loops = np.arange(n)
-    cg = plagnn.CSRGraph(np.concatenate([src, loops]), np.concatenate([dst, loops]), n)
+    cg = plagnn.CSRGraph(np.concatenate([src, loops]), np.concatenate([dst, loops]), n, bwd_trans=trans)
     og = oracle_mod.OracleGraph(src, dst, n)
     sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
     eng = plagnn.TrainEngine(cg, x, labels, dims, w, tr, va, lr=1e-3, device=DEV, params=sd)
@@ -95,14 +96,17 @@ def test_engine_step_matches_oracle(oracle_mod, dims):
         _close(after[k], t, name="adam " + k)
 
 
-def test_engine_graph_replay_equals_eager():
+@pytest.mark.parametrize("trans", [False, True])
+def test_engine_graph_replay_equals_eager(trans):
+    """trans: transposed max-backward descriptors (cleared by a kernel each call: a
+    hipMemsetAsync captured into the graph did not clear them on replays)."""
     import plagnn
 
     dims = (31, 24, 20, 16, 10, 12)
     src, dst, x, labels, w, tr, va, model = _problem(dims=dims, seed=4)
     n = x.shape[0]
     loops = np.arange(n)
-    cg = plagnn.CSRGraph(np.concatenate([src, loops]), np.concatenate([dst, loops]), n)
+    cg = plagnn.CSRGraph(np.concatenate([src, loops]), np.concatenate([dst, loops]), n, bwd_trans=trans)
     sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
     a = plagnn.TrainEngine(cg, x, labels, dims, w, tr, va, lr=1e-3, device=DEV, params=sd)
     b = plagnn.TrainEngine(cg, x, labels, dims, w, tr, va, lr=1e-3, device=DEV, params=sd)

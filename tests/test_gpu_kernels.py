@@ -16,10 +16,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _graph(src, dst, n, chunk=256):
+def _graph(src, dst, n, chunk=256, bwd_trans=None):
     import plagnn
 
-    return plagnn.CSRGraph(src, dst, n, chunk=chunk)
+    return plagnn.CSRGraph(src, dst, n, chunk=chunk, bwd_trans=bwd_trans)
 
 
 @pytest.mark.parametrize("F", [1, 3, 63, 64, 65, 128, 256, 300, 400, 503, 504, 512, 1100])
@@ -73,14 +73,17 @@ def test_spmm_max_fwd_special_values(oracle_mod, F):
 
 @pytest.mark.parametrize("F", [4, 65, 256, 503])
 @pytest.mark.parametrize("weighted", [False, True])
-def test_spmm_max_bwd(oracle_mod, F, weighted):
+@pytest.mark.parametrize("trans", [False, True])
+def test_spmm_max_bwd(oracle_mod, F, weighted, trans):
+    """trans: list descriptors at the transposed indices (the default on large graphs)."""
     from plagnn import ops
 
     n = 400
     src, dst = hub_graph(n, 1200, seed=F + 1)
     rng = np.random.default_rng(F)
     w = rng.uniform(-1, 2, len(src)).astype(np.float32) if weighted else None
-    g = _graph(src, dst, n)
+    g = _graph(src, dst, n, bwd_trans=trans)
+    assert g.bwd_trans == trans
     og = oracle_mod.OracleGraph(src, dst, n, self_loop=False, edge_weight=w)
     X = rng.standard_normal((n, F)).astype(np.float32)
     X[rng.random((n, F)) < 0.4] = 0.0
@@ -146,9 +149,10 @@ def test_spmm_empty_rows_and_edges():
     assert torch.equal(dX[2], torch.ones(4)) and dX[1].sum() == 0 and dX[0].sum() == 0
 
 
+@pytest.mark.parametrize("trans", [False, True])
 @pytest.mark.parametrize("dead", [False, True])
 @pytest.mark.parametrize("F", [4, 256])
-def test_spmm_max_bwd_sources_without_out_edges(oracle_mod, F, dead):
+def test_spmm_max_bwd_sources_without_out_edges(oracle_mod, F, dead, trans):
     """The highest-numbered nodes send no edges (their transposed rows are empty at the end
     of the entry range), and a graph with no edges at all: every dx row is still written
     (zeros for the empty ones), with and without dead-none records."""
@@ -158,7 +162,7 @@ def test_spmm_max_bwd_sources_without_out_edges(oracle_mod, F, dead):
     rng = np.random.default_rng(F + dead)
     src = rng.integers(0, n_src, 2000).astype(np.int64)
     dst = rng.integers(0, n, 2000).astype(np.int64)
-    g = _graph(src, dst, n)
+    g = _graph(src, dst, n, bwd_trans=trans)
     assert np.all(g.out_degrees()[n_src:] == 0) and np.any(g.in_degrees()[n_src:] > 0)
     og = oracle_mod.OracleGraph(src, dst, n, self_loop=False)
     X = np.maximum(rng.standard_normal((n, F)), 0).astype(np.float32)
@@ -174,7 +178,7 @@ def test_spmm_max_bwd_sources_without_out_edges(oracle_mod, F, dead):
     assert np.all(dx.cpu().numpy()[n_src:] == 0)
     # no edges at all
     e = np.zeros(0, np.int64)
-    g0 = _graph(e, e, 7)
+    g0 = _graph(e, e, 7, bwd_trans=trans)
     dg0 = g0.on(DEV)
     X0 = torch.rand(7, F, device=DEV)
     out0, arg0 = ops.spmm_max(dg0, X0, dead_none=dead)
@@ -184,8 +188,9 @@ def test_spmm_max_bwd_sources_without_out_edges(oracle_mod, F, dead):
     assert torch.all(dx0 == 0)
 
 
+@pytest.mark.parametrize("trans", [False, True])
 @pytest.mark.parametrize("F", [65, 256])
-def test_spmm_max_bwd_hub_past_lds_histogram(oracle_mod, F):
+def test_spmm_max_bwd_hub_past_lds_histogram(oracle_mod, F, trans):
     """A destination with 6 000 in-edges (u16 records; past the 4 096-entry LDS histogram of
     the count and place passes, whose list counters are then global integer atomics) and a
     source with 6 000 out-edges: bit-exact on unsplit rows."""
@@ -193,7 +198,7 @@ def test_spmm_max_bwd_hub_past_lds_histogram(oracle_mod, F):
 
     n = 3000
     src, dst = hub_graph(n, 6000, seed=F)
-    g = _graph(src, dst, n)
+    g = _graph(src, dst, n, bwd_trans=trans)
     assert g.in_degrees().max() > 4096 and g.arg_kind == 16
     og = oracle_mod.OracleGraph(src, dst, n, self_loop=False)
     rng = np.random.default_rng(F)
@@ -233,7 +238,7 @@ def test_spmm_max_bwd_wide_items_split_rows(oracle_mod, F, dead):
         dsts.append(rng.integers(0, n, d))
     src = np.concatenate(srcs + [np.arange(n)]).astype(np.int64)
     dst = np.concatenate(dsts + [np.arange(n)]).astype(np.int64)
-    g = plagnn.CSRGraph(src, dst, n, chunk=256, chunk_bwd=512)
+    g = plagnn.CSRGraph(src, dst, n, chunk=256, chunk_bwd=512, bwd_trans=dead)  # both placements
     assert g.bwd.chunk == 512 and g.bwd.n_merges >= 3
     split_rows = set(g.bwd.merges.reshape(-1, 4)[: g.bwd.n_merges, 0].tolist())
     assert {3, 5, 9} <= split_rows
@@ -696,3 +701,27 @@ def test_gemm_f32_edge_shapes_with_epilogue(ta, tb, M, N, K):
     scale = (a64.abs() @ b64.abs()) + C0.double().abs() + bias.double().abs()
     err = (Cd.cpu().double() - ref).abs()
     assert float((err / scale).max()) <= 2e-6
+
+
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("M,N,K1,K2", [(24041, 256, 256, 256), (1000, 300, 300, 400), (777, 200, 400, 300),
+                                      (300, 104, 4, 60), (513, 64, 100, 28)])
+def test_gemm_f32_cat_equals_concatenated(tb, M, N, K1, K2):
+    """pg_gemm_f32_cat ([A1 | A2] op([B1 ; B2]) over two K pieces, the split at any multiple
+    of 4, K steps straddling it included) equals pg_gemm_f32 on the concatenated operands
+    bit for bit (the same tile and k order), with and without bias + leaky_relu."""
+    from plagnn import _lib, ops
+
+    g = torch.Generator(device="cpu").manual_seed(M + N + K1)
+    A1 = torch.randn(M, K1, generator=g).to(DEV)
+    A2 = torch.randn(M, K2, generator=g).to(DEV)
+    B1 = torch.randn(*((N, K1) if tb else (K1, N)), generator=g).to(DEV)
+    B2 = torch.randn(*((N, K2) if tb else (K2, N)), generator=g).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    A = torch.cat([A1, A2], 1)
+    B = torch.cat([B1, B2], 1 if tb else 0)
+    for kw in ({}, {"bias": bias, "act": _lib.PG_ACT_LEAKY}):
+        got = ops.gemm_cat(A1, A2, B1, B2, transb=tb, **kw)
+        assert got is not None
+        want = ops.gemm(A, B, transb=tb, **kw)
+        assert torch.equal(got, want), float((got - want).abs().max())
