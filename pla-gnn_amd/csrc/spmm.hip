@@ -287,7 +287,8 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
 // 184 to 156 us (about 16 TB/s of gathered row bytes, close to the 17-19 TB/s the
 // microarchitecture guide measures for gathers served by L2); 128-B slices, whose part of X
 // fits an L2 whole, are no faster; on cfg5's 384 656-row bf16 graph slicing loses (8.1 ->
-// 12.1 ms per step), hence the size gate.
+// 12.1 ms per step), hence the size gate. The XCD mapping is what pays: the same kernel
+// with each slice spread over all XCDs (-DPG_FWD_SLICE_NOXCD) takes 113 us at F = 256.
 #ifndef PG_FWD_SLICE
 #define PG_FWD_SLICE 256  // bytes of a row per slice (0: whole-row tiles only)
 #endif
@@ -306,6 +307,9 @@ __global__ __launch_bounds__(kBlock) void max_fwd_slice_kernel(
   constexpr int CS = LPR * 4;
   constexpr int U = PG_EDGE_U < LPR ? PG_EDGE_U : LPR;
   static_assert(LPR <= 32 && LPR % U == 0, "slice lanes");
+#ifdef PG_FWD_SLICE_NOXCD  // probe builds: slice-major order, each slice spread over the XCDs
+  const int slice = blockIdx.x / n_iblk, iblk = blockIdx.x % n_iblk;
+#else
   const int g = blockIdx.x % 8, v = blockIdx.x / 8;
   int slice, iblk;
   if (n_slices >= 8) {
@@ -316,6 +320,7 @@ __global__ __launch_bounds__(kBlock) void max_fwd_slice_kernel(
     slice = g % n_slices;
     iblk = v * rep + g / n_slices;
   }
+#endif
   if (slice >= n_slices || iblk >= n_iblk) return;
   const int lane = lane_id();
   const int it = (iblk * kWavesPerBlock + wave_id_uniform()) * RPW + lane / LPR;
