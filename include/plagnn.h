@@ -387,6 +387,19 @@ int pg_spmm_max_bwd_bf16(const pg_csr_t* g, const pg_csr_t* gt, const void* argp
 int pg_cast_f32_bf16(const float* src, const int32_t* map, int64_t n, void* dst, pg_stream_t stream);
 int pg_cast_bf16_f32(const void* src, int64_t n, float* dst, pg_stream_t stream);
 
+/* Zero-padded 2-D copies in one launch (ABI 11): for each part, dst[r][c] = src[r][c] for
+ * r < rows, c < cols, else 0, over drows x dcols (row-major, leading dimensions lds / ldd).
+ * The drop-in SAGEConv's padded weight images (503 -> 512: [Wpool], bpool, [Wself | Wneigh])
+ * built from the layer's parameters each forward (code/model.py:13-15). */
+#define PG_PAD2D_MAX 8
+typedef struct pg_pad2d {
+  const float* src;
+  int64_t lds, rows, cols;
+  float* dst;
+  int64_t ldd, drows, dcols;
+} pg_pad2d_t;
+int pg_pad2d_group(const pg_pad2d_t* parts, int n, pg_stream_t stream);
+
 /* The PCA front end (code/data_preprocess.py:475-487 `pca`, scikit-learn 1.1.1
  * PCA(n_components, random_state=42) on the ECC / GCN*PPI matrices, 528-546): its randomized
  * SVD's products with the centred matrix, float64, as a CSR x dense SpMM with a rank-1 term:
@@ -482,7 +495,8 @@ int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-
                          records with the edge weight folded in; with fwd_out alone the
                          relu' mask is applied, only PG_ARG_DEAD_NONE implies it;
                          9: pg_gemm_f32_group; 10: the in-CSR's epos = transposed
-                         indices (transposed max-backward descriptors) */
+                         indices (transposed max-backward descriptors), pg_gemm_f32_cat;
+                         11: pg_pad2d_group */
 
 #ifdef __cplusplus
 }

@@ -387,6 +387,53 @@ int pg_adam_apply(float* param, const float* grad, float* exp_avg, float* exp_av
   return hip_status("pg_adam_apply");
 }
 
+}  // extern "C"
+
+namespace {
+// One launch for several zero-padded 2-D copies: part p owns the workgroups
+// [first[p], first[p+1]); each thread writes one element of dst (drows x dcols), the
+// source element or 0 past rows x cols.
+struct Pad2dGroup {
+  pg_pad2d_t p[PG_PAD2D_MAX];
+  int64_t first[PG_PAD2D_MAX + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(kBlock) void pad2d_group_kernel(Pad2dGroup g) {
+  int k = 0;
+  while (k + 1 < g.n && (int64_t)blockIdx.x >= g.first[k + 1]) ++k;
+  const pg_pad2d_t& p = g.p[k];
+  const int64_t i = ((int64_t)blockIdx.x - g.first[k]) * kBlock + threadIdx.x;
+  if (i >= p.drows * p.dcols) return;
+  const int64_t r = i / p.dcols, c = i % p.dcols;
+  p.dst[r * p.ldd + c] = (r < p.rows && c < p.cols) ? p.src[r * p.lds + c] : 0.f;
+}
+}  // namespace
+
+extern "C" {
+
+int pg_pad2d_group(const pg_pad2d_t* parts, int n, pg_stream_t stream) {
+  if (n < 0 || n > PG_PAD2D_MAX || (n > 0 && !parts))
+    return pg::set_error(PG_ERR_INVALID, "pg_pad2d_group: n = %d (at most %d parts)", n, PG_PAD2D_MAX);
+  Pad2dGroup g{};
+  g.n = n;
+  int64_t blocks = 0;
+  for (int k = 0; k < n; ++k) {
+    const pg_pad2d_t& p = parts[k];
+    if (p.rows < 0 || p.cols < 0 || p.rows > p.drows || p.cols > p.dcols || p.ldd < p.dcols ||
+        (p.rows > 0 && p.cols > 0 && (!p.src || p.lds < p.cols)) || (p.drows * p.dcols > 0 && !p.dst))
+      return pg::set_error(PG_ERR_INVALID, "pg_pad2d_group: bad part %d", k);
+    g.p[k] = p;
+    g.first[k] = blocks;
+    blocks += (p.drows * p.dcols + kBlock - 1) / kBlock;
+  }
+  g.first[n] = blocks;
+  if (blocks == 0) return pg::ok();
+  if (blocks > INT32_MAX) return pg::set_error(PG_ERR_UNSUPPORTED, "pg_pad2d_group: too large");
+  hipLaunchKernelGGL(pad2d_group_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, g);
+  return hip_status("pg_pad2d_group");
+}
+
 int pg_cast_f32_bf16(const float* src, const int32_t* map, int64_t n, void* dst,
                      pg_stream_t stream) {
   if (n < 0) return pg::set_error(PG_ERR_INVALID, "pg_cast_f32_bf16: n < 0");

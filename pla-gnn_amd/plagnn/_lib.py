@@ -13,7 +13,7 @@ import warnings
 import torch  # noqa: F401  (load order: see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 10  # pg_version() of the library this package binds (include/plagnn.h)
+ABI_VERSION = 11  # pg_version() of the library this package binds (include/plagnn.h)
 # PLAGNN_LIB overrides the library path (A/B builds of tuning variants)
 LIB_PATH = os.environ.get("PLAGNN_LIB") or os.path.join(_HERE, "libplagnn.so")
 
@@ -61,6 +61,23 @@ class PgGemmEpilogue(ctypes.Structure):
         ("rowsum", ctypes.c_void_p),
     ]
 
+
+class PgPad2d(ctypes.Structure):
+    """pg_pad2d_t (include/plagnn.h)."""
+
+    _fields_ = [
+        ("src", ctypes.c_void_p),
+        ("lds", ctypes.c_int64),
+        ("rows", ctypes.c_int64),
+        ("cols", ctypes.c_int64),
+        ("dst", ctypes.c_void_p),
+        ("ldd", ctypes.c_int64),
+        ("drows", ctypes.c_int64),
+        ("dcols", ctypes.c_int64),
+    ]
+
+
+PG_PAD2D_MAX = 8
 
 _i = ctypes.c_int
 _i32 = ctypes.c_int32
@@ -168,6 +185,7 @@ SIGNATURES = {
                                   _i64, _vp, _sz, _vp]),
     "pg_cast_f32_bf16": (_i, [_vp, _vp, _i64, _vp, _vp]),
     "pg_cast_bf16_f32": (_i, [_vp, _i64, _vp, _vp]),
+    "pg_pad2d_group": (_i, [ctypes.POINTER(PgPad2d), _i, _vp]),
     "pg_spmm_max_fwd_cpu": (_i, [_csr, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i]),
     "pg_spmm_max_bwd_cpu": (_i, [_csr, _csr, _vp, _i64, _i, _vp, _i64, _i64, _vp, _i64, _vp, _i64]),
     "pg_spmm_sum_cpu": (_i, [_csr, _vp, _i64, _i64, _i, _vp, _vp, _i64]),

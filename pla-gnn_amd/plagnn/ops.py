@@ -337,6 +337,29 @@ def cast_bf16(src: torch.Tensor, index: Optional[torch.Tensor] = None,
     return out
 
 
+def pad2d_group(parts) -> None:
+    """dst[:rows, :cols] = src, the rest of dst zero, for each (src, dst) pair of 2-D f32
+    tensors (unit column stride): one pg_pad2d_group launch per PG_PAD2D_MAX parts on the
+    GPU, torch on the CPU."""
+    parts = [(s.contiguous(), d) for s, d in parts]
+    if not parts:
+        return
+    if parts[0][1].device.type != "cuda":
+        for src, dst in parts:
+            dst.zero_()
+            dst[:src.shape[0], :src.shape[1]].copy_(src)
+        return
+    for i in range(0, len(parts), _lib.PG_PAD2D_MAX):
+        chunk = parts[i:i + _lib.PG_PAD2D_MAX]
+        arr = (_lib.PgPad2d * len(chunk))()
+        for k, (src, dst) in enumerate(chunk):
+            if dst.stride(1) != 1 or src.dtype != torch.float32 or dst.dtype != torch.float32:
+                raise ValueError("pad2d_group: f32 operands with unit column stride expected")
+            arr[k] = _lib.PgPad2d(ptr(src), _ld(src), src.shape[0], src.shape[1], ptr(dst), dst.stride(0),
+                                  dst.shape[0], dst.shape[1])
+        call("pg_pad2d_group", arr, len(chunk), _stream(chunk[0][1]))
+
+
 def col_sum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False
             ) -> torch.Tensor:
     rows, cols = x.shape
@@ -489,10 +512,13 @@ class SagePool(torch.autograd.Function):
         fpad = Fp - Fin
         keep = torch.is_grad_enabled() and any(ctx.needs_input_grad[:6])
         HM, ctx.hm_key = _hm_buffer(h, Fp, keep)
-        Wpool = torch.nn.functional.pad(w_pool, (0, fpad, 0, fpad)) if fpad else w_pool.contiguous()
-        bpool = torch.nn.functional.pad(b_pool, (0, fpad)) if fpad else b_pool.contiguous()
-        Wcat = torch.cat([torch.nn.functional.pad(w_self, (0, fpad)), torch.nn.functional.pad(w_neigh, (0, fpad))], 1) \
-            if fpad else torch.cat([w_self, w_neigh], 1)
+        # the padded weight images in one launch (pg_pad2d_group)
+        Fo = w_self.shape[0]
+        Wpool = torch.empty(Fp, Fp, dtype=torch.float32, device=h.device)
+        bpool = torch.empty(Fp, dtype=torch.float32, device=h.device)
+        Wcat = torch.empty(Fo, 2 * Fp, dtype=torch.float32, device=h.device)
+        pad2d_group([(w_pool, Wpool), (b_pool.view(1, -1), bpool.view(1, -1)), (w_self, Wcat[:, :Fp]),
+                     (w_neigh, Wcat[:, Fp:])])
         P = torch.empty(N, Fp, dtype=torch.float32, device=h.device)
         gemm(HM[:, :Fp], Wpool, transb=True, out=P, bias=bpool, act=_lib.PG_ACT_RELU)
         argpos = torch.empty(N, Fp, dtype=dg.arg_dtype, device=h.device)
@@ -606,10 +632,15 @@ class SagePool(torch.autograd.Function):
         N, Fp = P.shape
         Fo = dY.shape[1]
         need_h, need_wp, need_bp, need_ws, need_wn, need_b = ctx.needs_input_grad[:6]
-        # [dY | dP]: dY copied in, dP written by the max backward
-        DYP = torch.empty(N, Fo + Fp, dtype=torch.float32, device=dY.device)
-        DYP[:, :Fo].copy_(dY)
-        dY = DYP[:, :Fo]
+        # [dY | dP]: dY copied in, dP written by the max backward (only for the stacked
+        # input-gradient product: the first layer's input, the features, takes none)
+        if need_h:
+            DYP = torch.empty(N, Fo + Fp, dtype=torch.float32, device=dY.device)
+            DYP[:, :Fo].copy_(dY)
+            dY = DYP[:, :Fo]
+        else:
+            dY = dY.contiguous()
+            DYP = None
         d_b = torch.empty(Fo, dtype=torch.float32, device=dY.device) if (need_b and ctx.has_bias) else None
         d_ws = d_wn = None
         wgrads = []  # the layer's weight gradients, one grouped launch after the max backward
@@ -621,8 +652,8 @@ class SagePool(torch.autograd.Function):
             d_b = col_sum(dY)
         dM = gemm(dY, Wcat[:, Fp:])
         # dead-none records: the relu' mask of P is implied (P is not read)
-        spmm_max_backward(dg, argpos, dM, ew_slots, mask=P, dx=DYP[:, Fo:], dead_none=True)
-        dP = DYP[:, Fo:]
+        dP = DYP[:, Fo:] if DYP is not None else torch.empty(N, Fp, dtype=torch.float32, device=dY.device)
+        spmm_max_backward(dg, argpos, dM, ew_slots, mask=P, dx=dP, dead_none=True)
         d_bp_p = torch.empty(Fp, dtype=torch.float32, device=dY.device) if need_bp else None
         d_wp = d_bp = None
         if need_wp:

@@ -725,3 +725,24 @@ def test_gemm_f32_cat_equals_concatenated(tb, M, N, K1, K2):
         assert got is not None
         want = ops.gemm(A, B, transb=tb, **kw)
         assert torch.equal(got, want), float((got - want).abs().max())
+
+
+@pytest.mark.gpu
+def test_pad2d_group_matches_torch():
+    """pg_pad2d_group: zero-padded copies of several operands in one launch (the drop-in
+    SAGEConv's weight images), including strided destinations and an empty part."""
+    from plagnn import ops
+
+    torch.manual_seed(3)
+    srcs = [torch.randn(503, 503, device=DEV), torch.randn(1, 503, device=DEV), torch.randn(256, 503, device=DEV),
+            torch.randn(256, 503, device=DEV), torch.randn(0, 7, device=DEV)]
+    W = torch.full((512, 512), 7.0, device=DEV)
+    b = torch.full((1, 512), 7.0, device=DEV)
+    Wcat = torch.full((256, 1024), 7.0, device=DEV)
+    E = torch.full((3, 9), 7.0, device=DEV)
+    ops.pad2d_group([(srcs[0], W), (srcs[1], b), (srcs[2], Wcat[:, :512]), (srcs[3], Wcat[:, 512:]), (srcs[4], E)])
+    want = [torch.nn.functional.pad(srcs[0], (0, 9, 0, 9)), torch.nn.functional.pad(srcs[1], (0, 9)),
+            torch.cat([torch.nn.functional.pad(srcs[2], (0, 9)), torch.nn.functional.pad(srcs[3], (0, 9))], 1),
+            torch.zeros(3, 9, device=DEV)]
+    for got, ref in zip([W, b, Wcat, E], want):
+        assert torch.equal(got, ref)
