@@ -23,6 +23,14 @@ for c in cfg2 cfg5; do
   if [ -d gpurun_out/pmc_$c ]; then
     G=gemm_f32; [ $c = cfg5 ] && G=gemm_bf16
     python3 scripts/make_traffic.py gpurun_out/pmc_$c $c --gemm-group $G --by-kernel > $DST/pmc_traffic_by_kernel_$c.txt
+  elif [ -f gpurun_out/pmc_traffic_$c.json ]; then  # pruned on the box (scripts/round_profiles.sh)
+    cp gpurun_out/pmc_traffic_by_kernel_$c.txt $DST/pmc_traffic_by_kernel_$c.txt
+    python3 -c "
+import json, os
+p = 'profiles/pmc_traffic.json'
+d = json.load(open(p)) if os.path.exists(p) else {}
+d.update(json.load(open('gpurun_out/pmc_traffic_$c.json')))
+json.dump(d, open(p, 'w'), indent=1)"
   fi
 done
 ls $DST

@@ -2,7 +2,7 @@
 bench.py's roofline against the profiler. Groups (the engine's launch
 groups, bench.py / TrainEngine.group_times):
   gemm          gemm_x3_kernel, gemm_dma_kernel, gemm_*_kernel, splitk_reduce*, gemm_bf16*
-  spmm_max_fwd  max_fwd_kernel, max_merge_kernel
+  spmm_max_fwd  max_fwd_kernel, max_fwd_slice_kernel, max_merge_kernel
   spmm_max_bwd  group_pack_kernel, max_bwd_pull_kernel, sum_merge_kernel
   head          head_kernel, head_final_kernel;   adam  adam_*, cast_*
 Usage: python scripts/prof_groups.py <rocprof -d dir> [--bench bench.json] [--json out.json]
@@ -15,7 +15,7 @@ import json
 import os
 import re
 
-RULES = [("gemm", r"gemm_|splitk_reduce"), ("spmm_max_fwd", r"max_fwd_kernel|max_merge_kernel"),
+RULES = [("gemm", r"gemm_|splitk_reduce"), ("spmm_max_fwd", r"max_fwd_kernel|max_fwd_slice_kernel|max_merge_kernel"),
          ("spmm_max_bwd", r"group_pack_kernel|max_bwd_pull_kernel|sum_merge_kernel"),
          ("head", r"head_kernel|head_final_kernel"), ("adam", r"adam_|cast_f32_bf16")]
 
