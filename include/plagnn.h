@@ -36,6 +36,10 @@
  *                           f32 in / f32 out with f32 accuracy: aligned operands run as
  *                           three-piece bf16 splits on v_mfma_f32_32x32x16_bf16
  *                           (gemm_x3.hip), the rest on v_mfma_f32_32x32x2_f32 (gemm.hip)
+ *   pg_gemm_f32_cat      <- fc_self(h) + fc_neigh(h_neigh) (code/model.py:13-15) as one
+ *                           product over two K pieces, and its input gradient
+ *   pg_gemm_*_group      <- a step's weight-gradient GEMMs (code/train.py:204), one launch
+ *   pg_pad2d_group       <- the drop-in SAGEConv's zero-padded weight images (503 -> 512)
  *   pg_gemm_bf16,        <- the same layers and aggregation in the bf16-storage mode
  *   pg_spmm_max_*_bf16      (BASELINE configs[4]: bf16 storage, f32 accumulate); not run
  *   pg_cast_*               by the reference (fp32 only): reference-unpinned
