@@ -152,7 +152,7 @@ int pg_csr_transpose(const int32_t* ptr, const int32_t* col, int64_t n_rows, int
 /* Work schedule sizes for rows of `ptr` split at `chunk` entries. */
 int pg_schedule_count(const int32_t* ptr, int64_t n_rows, int32_t chunk, int64_t* n_items,
                       int64_t* n_merges, int64_t* n_slots, int32_t* max_deg);
-/* Fill items[4*n_items] (longest first) and merges[4*n_merges]. */
+/* Fill items[4*n_items] and merges[4*n_merges] (both longest first). */
 int pg_schedule_build(const int32_t* ptr, int64_t n_rows, int32_t chunk, int32_t* items,
                       int32_t* merges);
 

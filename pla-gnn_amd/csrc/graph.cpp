@@ -7,6 +7,7 @@
 // ascending edge id. Also builds the transposed (out-)CSR used by the deterministic
 // max backward, and the per-row work schedule the device kernels consume.
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <new>
 #include <vector>
@@ -164,6 +165,14 @@ int pg_schedule_build(const int32_t* ptr, int64_t n_rows, int32_t chunk, int32_t
       }
       slot += n;
     }
+  }
+  // split rows longest first too (the sliced max forward takes each as a whole workgroup,
+  // in this order); a stable sort keeps equal lengths in row order
+  if (merges && m > 1) {
+    std::vector<std::array<int32_t, 4>> ms((size_t)m);
+    for (int64_t i = 0; i < m; ++i) std::copy(merges + 4 * i, merges + 4 * i + 4, ms[(size_t)i].begin());
+    std::stable_sort(ms.begin(), ms.end(), [](const auto& a, const auto& b) { return a[2] > b[2]; });
+    for (int64_t i = 0; i < m; ++i) std::copy(ms[(size_t)i].begin(), ms[(size_t)i].end(), merges + 4 * i);
   }
   const int64_t n_items = (int64_t)raw.size() / 4;
   std::vector<int64_t> bucket((size_t)chunk + 2, 0);

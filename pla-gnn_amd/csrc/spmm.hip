@@ -295,23 +295,13 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
 #ifndef PG_FWD_SLICE_MAXTAB
 #define PG_FWD_SLICE_MAXTAB (32ll << 20)  // largest slice of X (rows x slice bytes) sliced
 #endif
-template <int LPR, bool HAS_W, typename A, typename T = float>
-__global__ __launch_bounds__(kBlock) void max_fwd_slice_kernel(
-    const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
-    const int32_t* __restrict__ eslot, const float* __restrict__ ew,
-    const int4* __restrict__ items, int n_items, const T* __restrict__ X, int64_t ldx, int F,
-    T* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
-    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, int n_slices, int n_iblk,
-    int dead_none) {
-  constexpr int RPW = kWave / LPR;
-  constexpr int CS = LPR * 4;
-  constexpr int U = PG_EDGE_U < LPR ? PG_EDGE_U : LPR;
-  static_assert(LPR <= 32 && LPR % U == 0, "slice lanes");
+// (slice, item block) of workgroup b over n_iblk item blocks, XCD-affine (see above)
+__device__ __forceinline__ void slice_of_block(int b, int n_slices, int n_iblk, int& slice, int& iblk) {
 #ifdef PG_FWD_SLICE_NOXCD  // probe builds: slice-major order, each slice spread over the XCDs
-  const int slice = blockIdx.x / n_iblk, iblk = blockIdx.x % n_iblk;
+  slice = b / n_iblk;
+  iblk = b % n_iblk;
 #else
-  const int g = blockIdx.x % 8, v = blockIdx.x / 8;
-  int slice, iblk;
+  const int g = b % 8, v = b / 8;
   if (n_slices >= 8) {
     slice = g + 8 * (v / n_iblk);
     iblk = v % n_iblk;
@@ -321,72 +311,129 @@ __global__ __launch_bounds__(kBlock) void max_fwd_slice_kernel(
     iblk = v * rep + g / n_slices;
   }
 #endif
-  if (slice >= n_slices || iblk >= n_iblk) return;
-  const int lane = lane_id();
-  const int it = (iblk * kWavesPerBlock + wave_id_uniform()) * RPW + lane / LPR;
-  if (it >= n_items) return;
-  const int f = slice * CS + (lane % LPR) * 4;
-  const int4 item = items[it];
-  const int row = item.x, k0 = item.y, len = item.z - item.y, slot = item.w;
-  const int rs = ptr[row];
-  const float ninf = -std::numeric_limits<float>::infinity();
-  float best[4];
-  int bpos[4];
+}
+
+// One lane group's running maximum over `len` edges from in-CSR slot k0 (positions
+// relative to rs), LPR edges' ids per load, U row pieces in flight. (A macro, not a
+// function: passed by reference the running maxima took 109-126 registers against 72-75
+// written out in the kernel.)
+#define PG_SLICE_RUN(LPR, HAS_W, T, k0_, len_, rs_)                                                  \
+  do {                                                                                               \
+    constexpr int U_ = PG_EDGE_U < (LPR) ? PG_EDGE_U : (LPR);                                        \
+    static_assert((LPR) <= 32 && (LPR) % U_ == 0, "slice lanes");                                    \
+    const int sk0 = (k0_), slen = (len_), srs = (rs_);                                               \
+    const int q_ = lane % (LPR);                                                                     \
+    const int gbase = 4 * (lane - q_);                                                               \
+    for (int j = 0; j < slen; j += (LPR)) {                                                          \
+      const int kq = sk0 + j + min(q_, slen - j - 1);                                                \
+      const int idv = col[kq];                                                                       \
+      float wv = 1.f;                                                                                \
+      if constexpr (HAS_W) wv = ew[eslot ? eslot[kq] : kq];                                          \
+      _Pragma("unroll") for (int e0 = 0; e0 < (LPR); e0 += U_) {                                     \
+        if (j + e0 >= slen) break;                                                                   \
+        float x[U_][4];                                                                              \
+        _Pragma("unroll") for (int e = 0; e < U_; ++e) {                                             \
+          const int id = __builtin_amdgcn_ds_bpermute(gbase + 4 * (e0 + e), idv);                    \
+          load_tile<4, T>(X + (int64_t)id * ldx, f, F, x[e], ninf);                                  \
+        }                                                                                            \
+        _Pragma("unroll") for (int e = 0; e < U_; ++e) {                                             \
+          if (j + e0 + e < slen) {                                                                   \
+            const int pos = sk0 + j + e0 + e - srs;                                                  \
+            float w = 1.f;                                                                           \
+            if constexpr (HAS_W)                                                                     \
+              w = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(gbase + 4 * (e0 + e),       \
+                                                                          __builtin_bit_cast(int, wv))); \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                          \
+              const float m = HAS_W ? x[e][i] * w : x[e][i];                                         \
+              if (m > best[i]) {                                                                     \
+                best[i] = m;                                                                         \
+                bpos[i] = pos;                                                                       \
+              }                                                                                      \
+            }                                                                                        \
+          }                                                                                          \
+        }                                                                                            \
+      }                                                                                              \
+    }                                                                                                \
+  } while (0)
+
+template <int LPR, typename A, typename T>
+__device__ __forceinline__ void slice_store(T* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
+                                            int row, int f, int F, float (&best)[4], int (&bpos)[4],
+                                            int dead_none) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    best[i] = ninf;
-    bpos[i] = arg_none<A>();
+    if (__builtin_isinf(best[i])) best[i] = 0.f;
+    if (dead_none && best[i] == 0.f) bpos[i] = arg_none<A>();
   }
-  // each group of LPR lanes loads the ids (and weights) of its next LPR edges with one
-  // instruction; edge e's id reaches the whole group by a ds_bpermute from member e
-  const int q = lane % LPR;
-  const int gbase = 4 * (lane - q);
-  for (int j = 0; j < len; j += LPR) {
-    const int kq = k0 + j + min(q, len - j - 1);
-    const int idv = col[kq];
-    float wv = 1.f;
-    if constexpr (HAS_W) wv = ew[eslot ? eslot[kq] : kq];
-#pragma unroll
-    for (int e0 = 0; e0 < LPR; e0 += U) {
-      if (j + e0 >= len) break;
-      float x[U][4];
-#pragma unroll
-      for (int e = 0; e < U; ++e) {
-        const int id = __builtin_amdgcn_ds_bpermute(gbase + 4 * (e0 + e), idv);
-        load_tile<4, T>(X + (int64_t)id * ldx, f, F, x[e], ninf);
-      }
-#pragma unroll
-      for (int e = 0; e < U; ++e) {
-        if (j + e0 + e < len) {
-          const int pos = k0 + j + e0 + e - rs;
-          float w = 1.f;
-          if constexpr (HAS_W)
-            w = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(gbase + 4 * (e0 + e),
-                                                                        __builtin_bit_cast(int, wv)));
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float m = HAS_W ? x[e][i] * w : x[e][i];
-            if (m > best[i]) {
-              best[i] = m;
-              bpos[i] = pos;
-            }
-          }
-        }
-      }
-    }
-  }
-  if (slot < 0) {
+  store_tile<4, T>(out + (int64_t)row * ldo, f, F, best);
+  store_arg<4, A>(arg + (int64_t)row * lda, f, F, bpos);
+}
+
+// Rows longer than the schedule's chunk (its split rows, `merges`, longest first): one
+// workgroup per (row, slice), launched before the other rows' kernel. Its 16 lane groups
+// take contiguous runs of the row's edges, in order, and combine their maxima through LDS
+// in run order (strict >: the earliest maximal edge wins, as in one sequential pass), so
+// no partial slots and no merge launch; max_fwd_slice_kernel skips the schedule's pieces
+// of those rows.
+template <int LPR, bool HAS_W, typename A, typename T = float>
+__global__ __launch_bounds__(kBlock) void max_fwd_slice_kernel(
+    const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
+    const int32_t* __restrict__ eslot, const float* __restrict__ ew,
+    const int4* __restrict__ items, int n_items, const int4* __restrict__ hubs, int n_hub, int hub_grid,
+    const T* __restrict__ X, int64_t ldx, int F, T* __restrict__ out, int64_t ldo, A* __restrict__ arg,
+    int64_t lda, int n_slices, int n_iblk, int dead_none) {
+  constexpr int RPW = kWave / LPR;
+  constexpr int CS = LPR * 4;
+  constexpr int NG = RPW * kWavesPerBlock;  // lane groups per workgroup
+  __shared__ float hv[NG][CS];
+  __shared__ int hp[NG][CS];
+  const int lane = lane_id();
+  const float ninf = -std::numeric_limits<float>::infinity();
+  float best[4] = {ninf, ninf, ninf, ninf};
+  int bpos[4] = {arg_none<A>(), arg_none<A>(), arg_none<A>(), arg_none<A>()};
+  int b = blockIdx.x;
+  int slice, iblk;
+  if (b < hub_grid) {
+    // a split row, whole: the workgroup's lane groups take contiguous runs of its edges
+    slice_of_block(b, n_slices, n_hub, slice, iblk);
+    if (slice >= n_slices || iblk >= n_hub) return;  // uniform over the workgroup
+    const int row = hubs[iblk].x;
+    const int rs = ptr[row], deg = ptr[row + 1] - rs;
+    const int grp = wave_id_uniform() * RPW + lane / LPR;
+    const int run = (deg + NG - 1) / NG;
+    const int k0 = min(deg, grp * run);
+    const int len = min(deg, k0 + run) - k0;
+    const int c = (lane % LPR) * 4;
+    const int f = slice * CS + c;
+    PG_SLICE_RUN(LPR, HAS_W, T, rs + k0, len, rs);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (__builtin_isinf(best[i])) best[i] = 0.f;
-      if (dead_none && best[i] == 0.f) bpos[i] = arg_none<A>();
+      hv[grp][c + i] = best[i];
+      hp[grp][c + i] = bpos[i];
     }
-    store_tile<4, T>(out + (int64_t)row * ldo, f, F, best);
-    store_arg<4, A>(arg + (int64_t)row * lda, f, F, bpos);
-  } else {
-    store_tile<4>(ws_val + (int64_t)slot * ldw, f, F, best);
-    store_arg<4, A>(ws_arg + (int64_t)slot * ldw, f, F, bpos);
+    __syncthreads();
+    if (grp == 0) {
+      for (int r = 1; r < NG; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (hv[r][c + i] > best[i]) {
+            best[i] = hv[r][c + i];
+            bpos[i] = hp[r][c + i];
+          }
+      slice_store<LPR, A, T>(out, ldo, arg, lda, row, f, F, best, bpos, dead_none);
+    }
+    return;
   }
+  slice_of_block(b - hub_grid, n_slices, n_iblk, slice, iblk);
+  if (slice >= n_slices || iblk >= n_iblk) return;
+  const int it = (iblk * kWavesPerBlock + wave_id_uniform()) * RPW + lane / LPR;
+  if (it >= n_items) return;
+  const int4 item = items[it];
+  if (item.w >= 0) return;  // a piece of a split row: taken whole above
+  const int row = item.x;
+  const int f = slice * CS + (lane % LPR) * 4;
+  PG_SLICE_RUN(LPR, HAS_W, T, item.y, item.z - item.y, ptr[row]);
+  slice_store<LPR, A, T>(out, ldo, arg, lda, row, f, F, best, bpos, dead_none);
 }
 
 // Combine the partial maxima of split rows in chunk order (earlier chunk wins ties).
@@ -1385,26 +1432,28 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
   // every feature tile in one launch (blocks interleaved over the tiles), one merge launch
   // over the whole F
   const int n_ft = (int)((F + tp.tile - 1) / tp.tile);
-  if constexpr (PG_FWD_SLICE > 0) if (tp.vec && g->n_items > 0) {
-    // XCD column slices (max_fwd_slice_kernel)
+  if constexpr (PG_FWD_SLICE > 0) if (tp.vec && g->n_items > 0 && (g->n_merges == 0 || g->merges)) {
+    // XCD column slices (max_fwd_slice_kernel); split rows whole, first
     constexpr int LPR = std::min(32, PG_FWD_SLICE / (4 * (int)sizeof(T)));
     constexpr int RPW = kWave / LPR;
     const int n_sl = (int)((F + 4 * LPR - 1) / (4 * LPR));
     if ((n_sl % 8 == 0 || n_sl == 1 || n_sl == 2 || n_sl == 4) &&
         g->n_cols * (int64_t)(4 * LPR * sizeof(T)) <= PG_FWD_SLICE_MAXTAB) {
+      auto grid_of = [&](int64_t n_iblk) -> int64_t {
+        if (n_iblk == 0) return 0;
+        return n_sl >= 8 ? n_iblk * n_sl : 8 * ((n_iblk + 8 / n_sl - 1) / (8 / n_sl));
+      };
       const int n_iblk = (int)((g->n_items + RPW * kWavesPerBlock - 1) / (RPW * kWavesPerBlock));
-      const int64_t grid = n_sl >= 8 ? (int64_t)n_iblk * n_sl : 8 * (int64_t)((n_iblk + 8 / n_sl - 1) / (8 / n_sl));
+      const int n_hub = (int)g->n_merges;
       auto go = [&](auto hw_c) {
         constexpr bool HW = decltype(hw_c)::value;
-        hipLaunchKernelGGL((max_fwd_slice_kernel<LPR, HW, A, T>), dim3((unsigned)grid), dim3(kBlock), 0, st,
-                           g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items, X, ldx,
-                           (int)F, out, ldo, arg, lda, ws_val, ws_arg, ldw, n_sl, n_iblk, dead_none);
+        const int64_t hub_grid = grid_of(n_hub);
+        hipLaunchKernelGGL((max_fwd_slice_kernel<LPR, HW, A, T>), dim3((unsigned)(hub_grid + grid_of(n_iblk))),
+                           dim3(kBlock), 0, st, g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items,
+                           (int)g->n_items, (const int4*)g->merges, n_hub, (int)hub_grid, X, ldx, (int)F, out, ldo,
+                           arg, lda, n_sl, n_iblk, dead_none);
       };
       if (has_w) go(std::true_type{}); else go(std::false_type{});
-      if (g->n_merges > 0)
-        hipLaunchKernelGGL((max_merge_kernel<A, T>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
-                           (const int4*)g->merges, (int)g->n_merges, (int)F, ws_val, ws_arg, ldw, out, ldo,
-                           arg, lda, dead_none);
       return hip_status("pg_spmm_max_fwd");
     }
   }
