@@ -420,7 +420,8 @@ int pg_pad2d_group(const pg_pad2d_t* parts, int n, pg_stream_t stream) {
   int64_t blocks = 0;
   for (int k = 0; k < n; ++k) {
     const pg_pad2d_t& p = parts[k];
-    if (p.rows < 0 || p.cols < 0 || p.rows > p.drows || p.cols > p.dcols || p.ldd < p.dcols ||
+    if (p.rows < 0 || p.cols < 0 || p.drows < 0 || p.dcols < 0 || p.rows > p.drows || p.cols > p.dcols ||
+        p.ldd < p.dcols ||
         (p.rows > 0 && p.cols > 0 && (!p.src || p.lds < p.cols)) || (p.drows * p.dcols > 0 && !p.dst))
       return pg::set_error(PG_ERR_INVALID, "pg_pad2d_group: bad part %d", k);
     g.p[k] = p;

@@ -316,7 +316,8 @@ __device__ __forceinline__ void slice_of_block(int b, int n_slices, int n_iblk, 
 // One lane group's running maximum over `len` edges from in-CSR slot k0 (positions
 // relative to rs), LPR edges' ids per load, U row pieces in flight. (A macro, not a
 // function: passed by reference the running maxima took 109-126 registers against 72-75
-// written out in the kernel.)
+// written out in the kernel.) It reads the enclosing kernel's `lane`, `col`, `eslot`, `ew`,
+// `X`, `ldx`, `f`, `F`, `ninf` and updates its `best[4]` / `bpos[4]`.
 #define PG_SLICE_RUN(LPR, HAS_W, T, k0_, len_, rs_)                                                  \
   do {                                                                                               \
     constexpr int U_ = PG_EDGE_U < (LPR) ? PG_EDGE_U : (LPR);                                        \
