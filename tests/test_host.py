@@ -69,6 +69,29 @@ def test_schedule_covers_rows_longest_first():
         cover[k0:k1] += 1
     assert np.all(cover == 1)
     assert g.fwd.n_merges >= 1 and g.fwd.max_deg > 1000
+    # split rows: every row past the chunk once, with its slot run, longest first
+    ms = g.fwd.merges.reshape(-1, 4)[: g.fwd.n_merges]
+    deg = np.diff(g.fwd.ptr)
+    assert sorted(ms[:, 0].tolist()) == np.flatnonzero(deg > 64).tolist()
+    assert np.all(np.diff(ms[:, 2]) <= 0)
+    assert np.all(ms[:, 2] == (deg[ms[:, 0]] + 63) // 64)
+
+
+def test_pad2d_group_rejects_bad_parts():
+    """pg_pad2d_group validates every part before launching anything (no GPU needed)."""
+    import ctypes
+
+    from plagnn import _lib
+
+    L = _lib.lib()
+    src = np.zeros((2, 3), np.float32)
+    dst = np.zeros((4, 4), np.float32)
+    good = dict(src=src.ctypes.data, lds=3, rows=2, cols=3, dst=dst.ctypes.data, ldd=4, drows=4, dcols=4)
+    for bad in (dict(drows=-1, rows=0), dict(rows=5), dict(cols=5), dict(ldd=3), dict(lds=2), dict(dst=None)):
+        part = _lib.PgPad2d(**{**good, **bad})
+        assert L.pg_pad2d_group(ctypes.byref(part), 1, None) != 0, bad
+    assert L.pg_pad2d_group(None, _lib.PG_PAD2D_MAX + 1, None) != 0
+    assert L.pg_pad2d_group(None, 0, None) == 0  # nothing to do
 
 
 @pytest.mark.parametrize("F", [1, 5, 64, 130])
