@@ -71,6 +71,34 @@ def test_spmm_max_fwd_special_values(oracle_mod, F):
     assert np.all(~won[:, 0]) and won.mean() > 0.5
 
 
+@pytest.mark.parametrize("F", [256, 512, 1100])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_max_fwd_ties_across_split_rows(oracle_mod, F, weighted):
+    """Few distinct values, so most maxima are ties, on a graph whose hub rows are taken
+    whole by one workgroup per slice (F = 256 / 512: the sliced kernel, runs combined in
+    order) or split into chunks and merged (F = 1100: the whole-row kernel): the earliest
+    maximal edge must win everywhere, as in one sequential pass."""
+    from plagnn import ops
+
+    n = 600
+    src, dst = hub_graph(n, 3000, seed=F)
+    rng = np.random.default_rng(F + 1)
+    w = rng.choice(np.array([0.5, 1.0, 2.0], np.float32), len(src)) if weighted else None
+    g = _graph(src, dst, n)
+    assert g.fwd.n_merges >= 1
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False, edge_weight=w)
+    X = rng.integers(0, 4, (n, F)).astype(np.float32)
+    dg = g.on(DEV)
+    ews = dg.edge_weight_slots(None if w is None else torch.from_numpy(w))
+    out, argpos = ops.spmm_max(dg, torch.from_numpy(X).to(DEV), ews)
+    ref, argx, _ = oracle_mod.spmm_max(og, X, use_weight=weighted)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    got = ops.argpos_to_src(dg, argpos).cpu().numpy()
+    won = got >= 0
+    np.testing.assert_array_equal(got[won], argx[won])
+    assert np.all(ref[~won] == 0)
+
+
 @pytest.mark.parametrize("F", [4, 65, 256, 503])
 @pytest.mark.parametrize("weighted", [False, True])
 @pytest.mark.parametrize("trans", [False, True])
