@@ -314,13 +314,13 @@ __device__ __forceinline__ void slice_of_block(int b, int n_slices, int n_iblk, 
 }
 
 // One lane group's running maximum over `len` edges from in-CSR slot k0 (positions
-// relative to rs), LPR edges' ids per load, U row pieces in flight. (A macro, not a
+// relative to rs), LPR edges' ids per load, UE row pieces in flight. (A macro, not a
 // function: passed by reference the running maxima took 109-126 registers against 72-75
 // written out in the kernel.) It reads the enclosing kernel's `lane`, `col`, `eslot`, `ew`,
 // `X`, `ldx`, `f`, `F`, `ninf` and updates its `best[4]` / `bpos[4]`.
-#define PG_SLICE_RUN(LPR, HAS_W, T, k0_, len_, rs_)                                                  \
+#define PG_SLICE_RUN(LPR, UE, HAS_W, T, k0_, len_, rs_)                                              \
   do {                                                                                               \
-    constexpr int U_ = PG_EDGE_U < (LPR) ? PG_EDGE_U : (LPR);                                        \
+    constexpr int U_ = (UE) < (LPR) ? (UE) : (LPR);                                                  \
     static_assert((LPR) <= 32 && (LPR) % U_ == 0, "slice lanes");                                    \
     const int sk0 = (k0_), slen = (len_), srs = (rs_);                                               \
     const int q_ = lane % (LPR);                                                                     \
@@ -377,7 +377,7 @@ __device__ __forceinline__ void slice_store(T* __restrict__ out, int64_t ldo, A*
 // no partial slots and no merge launch. The other workgroups take the schedule's items and
 // skip its pieces of those rows. (As a launch of its own before the other rows, the split
 // rows' tail ran alone: 0.350 vs 0.301 ms per cfg2 step.)
-template <int LPR, bool HAS_W, typename A, typename T = float>
+template <int LPR, int UE, bool HAS_W, typename A, typename T = float>
 __global__ __launch_bounds__(kBlock) void max_fwd_slice_kernel(
     const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
     const int32_t* __restrict__ eslot, const float* __restrict__ ew,
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void max_fwd_slice_kernel(
     const int len = min(deg, k0 + run) - k0;
     const int c = (lane % LPR) * 4;
     const int f = slice * CS + c;
-    PG_SLICE_RUN(LPR, HAS_W, T, rs + k0, len, rs);
+    PG_SLICE_RUN(LPR, UE, HAS_W, T, rs + k0, len, rs);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       hv[grp][c + i] = best[i];
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(kBlock) void max_fwd_slice_kernel(
   if (item.w >= 0) return;  // a piece of a split row: taken whole above
   const int row = item.x;
   const int f = slice * CS + (lane % LPR) * 4;
-  PG_SLICE_RUN(LPR, HAS_W, T, item.y, item.z - item.y, ptr[row]);
+  PG_SLICE_RUN(LPR, UE, HAS_W, T, item.y, item.z - item.y, ptr[row]);
   slice_store<LPR, A, T>(out, ldo, arg, lda, row, f, F, best, bpos, dead_none);
 }
 
@@ -1447,15 +1447,28 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
       };
       const int n_iblk = (int)((g->n_items + RPW * kWavesPerBlock - 1) / (RPW * kWavesPerBlock));
       const int n_hub = (int)g->n_merges;
-      auto go = [&](auto hw_c) {
+      // row pieces in flight per lane group: 4 with one slice per XCD and no edge weights
+      // (cfg2's F = 512: 147.8-148.2 vs 151.8 us), else 8 (F = 256: 81.6 vs 88.5 us; cfg3's
+      // weighted F = 512: 169-171 vs 177-180 us)
+      auto go = [&](auto hw_c, auto ue_c) {
         constexpr bool HW = decltype(hw_c)::value;
+        constexpr int UE = decltype(ue_c)::value;
         const int64_t hub_grid = grid_of(n_hub);
-        hipLaunchKernelGGL((max_fwd_slice_kernel<LPR, HW, A, T>), dim3((unsigned)(hub_grid + grid_of(n_iblk))),
+        hipLaunchKernelGGL((max_fwd_slice_kernel<LPR, UE, HW, A, T>), dim3((unsigned)(hub_grid + grid_of(n_iblk))),
                            dim3(kBlock), 0, st, g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items,
                            (int)g->n_items, (const int4*)g->merges, n_hub, (int)hub_grid, X, ldx, (int)F, out, ldo,
                            arg, lda, n_sl, n_iblk, dead_none);
       };
-      if (has_w) go(std::true_type{}); else go(std::false_type{});
+      using U4 = std::integral_constant<int, 4>;
+      using U8 = std::integral_constant<int, 8>;
+#ifndef PG_SLICE_U_FIXED
+#define PG_SLICE_U_FIXED 0  // variant builds: 8 keeps 8 pieces in flight for every slice count
+#endif
+      if (n_sl >= 8 && !has_w && PG_SLICE_U_FIXED != 8) {
+        go(std::false_type{}, U4{});
+      } else {
+        if (has_w) go(std::true_type{}, U8{}); else go(std::false_type{}, U8{});
+      }
       return hip_status("pg_spmm_max_fwd");
     }
   }
