@@ -292,6 +292,12 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
 #ifndef PG_FWD_SLICE
 #define PG_FWD_SLICE 256  // bytes of a row per slice (0: whole-row tiles only)
 #endif
+#ifndef PG_FWD_SLICE_NO_WIDE
+#define PG_FWD_SLICE_NO_WIDE 0  // variant builds: 1 keeps widths that need wider slices on whole rows
+#endif
+#ifndef PG_SLICE_U_FIXED
+#define PG_SLICE_U_FIXED 0  // variant builds: 8 keeps 8 pieces in flight for every slice count
+#endif
 #ifndef PG_FWD_SLICE_MAXTAB
 #define PG_FWD_SLICE_MAXTAB (32ll << 20)  // largest slice of X (rows x slice bytes) sliced
 #endif
@@ -1435,12 +1441,16 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
   // over the whole F
   const int n_ft = (int)((F + tp.tile - 1) / tp.tile);
   if constexpr (PG_FWD_SLICE > 0) if (tp.vec && g->n_items > 0 && (g->n_merges == 0 || g->merges)) {
-    // XCD column slices (max_fwd_slice_kernel); split rows whole, first
-    constexpr int LPR = std::min(32, PG_FWD_SLICE / (4 * (int)sizeof(T)));
-    constexpr int RPW = kWave / LPR;
-    const int n_sl = (int)((F + 4 * LPR - 1) / (4 * LPR));
-    if ((n_sl % 8 == 0 || n_sl == 1 || n_sl == 2 || n_sl == 4) &&
-        g->n_cols * (int64_t)(4 * LPR * sizeof(T)) <= PG_FWD_SLICE_MAXTAB) {
+    // XCD column slices (max_fwd_slice_kernel); split rows whole, first. The slices must share
+    // out over the 8 XCDs (1, 2, 4 or a multiple of 8 of them): a width whose PG_FWD_SLICE-byte
+    // slices do not (F = 400 f32: 7 of 64 columns) tries slices twice as wide (4 of 128).
+    auto try_slices = [&](auto lpr_c) -> bool {
+      constexpr int LPR = decltype(lpr_c)::value;
+      constexpr int RPW = kWave / LPR;
+      const int n_sl = (int)((F + 4 * LPR - 1) / (4 * LPR));
+      if (!(n_sl % 8 == 0 || n_sl == 1 || n_sl == 2 || n_sl == 4) ||
+          g->n_cols * (int64_t)(4 * LPR * sizeof(T)) > PG_FWD_SLICE_MAXTAB)
+        return false;
       auto grid_of = [&](int64_t n_iblk) -> int64_t {
         if (n_iblk == 0) return 0;
         return n_sl >= 8 ? n_iblk * n_sl : 8 * ((n_iblk + 8 / n_sl - 1) / (8 / n_sl));
@@ -1461,16 +1471,18 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
       };
       using U4 = std::integral_constant<int, 4>;
       using U8 = std::integral_constant<int, 8>;
-#ifndef PG_SLICE_U_FIXED
-#define PG_SLICE_U_FIXED 0  // variant builds: 8 keeps 8 pieces in flight for every slice count
-#endif
       if (n_sl >= 8 && !has_w && PG_SLICE_U_FIXED != 8) {
         go(std::false_type{}, U4{});
       } else {
         if (has_w) go(std::true_type{}, U8{}); else go(std::false_type{}, U8{});
       }
-      return hip_status("pg_spmm_max_fwd");
-    }
+      return true;
+    };
+    constexpr int LPR0 = std::min(32, PG_FWD_SLICE / (4 * (int)sizeof(T)));
+    bool done = try_slices(std::integral_constant<int, LPR0>{});
+    if constexpr (2 * LPR0 <= 32 && !PG_FWD_SLICE_NO_WIDE)
+      if (!done) done = try_slices(std::integral_constant<int, 2 * LPR0>{});
+    if (done) return hip_status("pg_spmm_max_fwd");
   }
   {
     const int64_t f0 = 0;
