@@ -62,6 +62,30 @@ ALPHA = 0.1               # main_normal.py -a default (code/main_normal.py:29)
 # MI355X_MICROARCH.md "Indexed rows": rows gathered from an XCD's L2 16.8-18.8 TB/s chip-wide
 # (a uniformly random 38 MB table from the Infinity Cache: 8.6 TB/s)
 L2_GATHER_GBS = 17800.0
+# the same section: uniformly random rows of a 151 MB table (Infinity-Cache resident) 7.4-7.9
+# TB/s; rows of a buffer far larger than the Infinity Cache 5.5-5.8 TB/s (register gather)
+MALL_GATHER_GBS = 7900.0
+HBM_GATHER_GBS = 5800.0
+MALL_BYTES = 256 << 20
+
+
+def gather_regime(n_rows: int, elem_bytes: int):
+    """The random-row gather ceiling that applies to the max forward, chosen by the bytes of
+    one 256-column feature tile of X (the table one gather pass draws rows from): up to
+    32 MiB the library cuts the tile's columns into 256-B slices dealt to the XCDs (S0: 6.2 MB
+    per slice, L2 hit 0.77 with the power-law reuse), so the L2-served rate applies; up to the
+    256 MiB Infinity Cache the 151-MB random-row rate; beyond it the HBM random-row rate.
+    Returns (bound, peak GB/s, peak_is)."""
+    tile = n_rows * 256 * elem_bytes
+    if tile <= 32 << 20:
+        return "l2_gather", L2_GATHER_GBS, (f"L2-served random-row gather ceiling (MI355X_MICROARCH.md, indexed rows): "
+                                            f"a {tile / 2**20:.1f} MiB feature tile, sliced over the XCDs")
+    if tile <= MALL_BYTES:
+        return "mall_gather", MALL_GATHER_GBS, (f"Infinity-Cache random-row gather ceiling, 151 MB table "
+                                                f"(MI355X_MICROARCH.md, indexed rows: 7.4-7.9 TB/s): a {tile / 2**20:.0f} MiB "
+                                                f"feature tile fits the 256 MiB Infinity Cache, not the 4 MiB L2s")
+    return "hbm_gather", HBM_GATHER_GBS, (f"HBM random-row gather rate (MI355X_MICROARCH.md: 5.5-5.8 TB/s): a "
+                                          f"{tile / 2**20:.0f} MiB feature tile exceeds the Infinity Cache")
 
 
 def _cpu_model() -> str:
@@ -321,11 +345,12 @@ def _roofline(engine, gt, bf16):
         if gname == "spmm_max_fwd":
             # per-edge row gathers (SURVEY.md §8d bytes) are served mostly by the L2s and the
             # 256 MiB Infinity Cache, not HBM (PMC: the fabric sees a quarter of them on S0):
-            # the bound is the L2-served random-row gather rate; the HBM figure stays beside it
-            return {"bound": "l2_gather", "achieved": round(ach, 1), "peak": L2_GATHER_GBS, "unit": "GB/s",
-                    "frac": round(ach / L2_GATHER_GBS, 4), **base, "bytes_per_step": int(g["work"]),
-                    "peak_is": "L2-served random-row gather ceiling (MI355X_MICROARCH.md, indexed rows)",
-                    "peak_hbm": PEAK_HBM_GBS, "frac_vs_hbm": round(ach / PEAK_HBM_GBS, 4)}
+            # the bound is the random-row gather rate of the regime the feature tile's size
+            # puts it in; the HBM figure stays beside it
+            bound, peak, peak_is = gather_regime(engine.N, 2 if bf16 else 4)
+            return {"bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
+                    "frac": round(ach / peak, 4), **base, "bytes_per_step": int(g["work"]),
+                    "peak_is": peak_is, "peak_hbm": PEAK_HBM_GBS, "frac_vs_hbm": round(ach / PEAK_HBM_GBS, 4)}
         return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(ach / PEAK_HBM_GBS, 4), **base, "bytes_per_step": int(g["work"])}
 
@@ -573,7 +598,40 @@ def sub_configs(args):
     return out
 
 
-def main():
+def _device(local_rank: int) -> torch.device:
+    """One rank per GPU; more ranks than GPUs (a rehearsal of the N-rank flow on a smaller
+    box, with PLAGNN_BENCH_BACKEND=gloo) share them round-robin."""
+    local_dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    return torch.device("cuda", local_dev)
+
+
+def _device_info(dev) -> dict:
+    props = torch.cuda.get_device_properties(dev)
+    return {"device": dev.index, "name": props.name, "pci_bus_id": getattr(props, "pci_bus_id", None),
+            "uuid": str(getattr(props, "uuid", ""))}
+
+
+def guarded_dp_leg(args, rank, world, dev, dist, ctrl):
+    """The N > 1 RCCL data-parallel leg beside the replicas headline, as a leg: a failure
+    (on any rank) is recorded as {"error": ...} and the headline still prints. Every rank
+    takes the same path: each reports ok / failed over `ctrl` (a gloo group, usable even
+    when the RCCL communicator is what failed) and all of them agree on the outcome."""
+    err = None
+    res = None
+    try:
+        res = run(args, rank, world, dev, dist, "dp", breakdown=False)
+    except (Exception, SystemExit) as e:  # run() raises SystemExit on diverged replicas
+        err = f"rank {rank}: {type(e).__name__}: {e}"[-500:]
+        print(f"dp leg failed on {err}", file=sys.stderr, flush=True)
+    flag = torch.tensor([1 if err else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=ctrl)
+    if flag.item():
+        return {"error": err or "failed on another rank (see its stderr)"} if rank == 0 else None
+    return res
+
+
+def main(argv=None):
     from plagnn import workload as W
 
     ap = argparse.ArgumentParser()
@@ -593,7 +651,7 @@ def main():
     ap.add_argument("--dump-breakdown", default="", help="write the per-launch-site breakdown (JSON)")
     ap.add_argument("--dropin-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--chunk-bwd", type=int, default=0, help=argparse.SUPPRESS)  # tuning experiments
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.chunk_bwd:
         import plagnn.graph
 
@@ -620,36 +678,33 @@ def main():
             dropin = _child(args, ["--config", args.config, "--dropin-only"])
         except SystemExit as e:  # a leg, not the headline: report it and go on
             dropin = {"error": str(e)[-500:]}
-    # one rank per GPU; more ranks than GPUs (a rehearsal of the N-rank flow on a smaller
-    # box, with PLAGNN_BENCH_BACKEND=gloo) share them round-robin
-    local_dev = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_dev)
-    dev = torch.device("cuda", local_dev)
+    dev = _device(local_rank)
     dist = None
+    ctrl = None  # control-flag group (gloo) for the guarded dp leg
     if world > 1:
         import torch.distributed as dist
 
         backend = os.environ.get("PLAGNN_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+            ctrl = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(backend)
 
     dist_info = None
     if dist is not None:
-        props = torch.cuda.get_device_properties(dev)
-        me = {"rank": rank, "local_rank": local_rank, "device": dev.index, "name": props.name,
-              "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", ""))}
+        me = {"rank": rank, "local_rank": local_rank, **_device_info(dev)}
         every = [None] * world
         dist.all_gather_object(every, me)
         dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "ranks": every}
     out = run(args, rank, world, dev, dist, mode)
-    # N > 1: the RCCL data-parallel leg in the same job, after the replicas headline
+    # N > 1: the RCCL data-parallel leg in the same job, after the replicas headline; a leg,
+    # so its failure is reported in the line and does not cost the headline
     dp_leg = None
     if world > 1 and mode == "replicas" and args.mode == "auto":
-        dp_leg = run(args, rank, world, dev, dist, "dp", breakdown=False)
+        dp_leg = guarded_dp_leg(args, rank, world, dev, dist, ctrl)
     if out is None:
-        dist.destroy_process_group()
+        _finish(dist)
         return
     engine, wl = out.pop("_engine"), out.pop("_wl")
     if dist_info is not None:
@@ -681,8 +736,18 @@ def main():
     loss = out.pop("loss")
     out["loss"] = loss
     print(json.dumps(out), flush=True)
-    if dist is not None:
+    _finish(dist)
+
+
+def _finish(dist) -> None:
+    """Tear the process group down after the line is out; a communicator left broken by a
+    failed leg must not turn a printed result into a failed run."""
+    if dist is None:
+        return
+    try:
         dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        print(f"destroy_process_group: {e}", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":

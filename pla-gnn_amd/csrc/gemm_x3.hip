@@ -416,9 +416,11 @@ __device__ __forceinline__ void x3_tile(
   Stage<BN, BKM> sb;
   static_assert(!KCAT || PG_X3_BUFLOAD, "K-concatenated operands need the buffer-load addressing");
 #if PG_X3_BUFLOAD
-  // operand extents in bytes (row image: R rows of ld; k image: K rows of ld)
-  const uint32_t a_bytes = (uint32_t)(AK ? ((int64_t)(K - 1) * lda + M) * 4 : ((int64_t)(M - 1) * lda + K) * 4);
-  const uint32_t b_bytes = (uint32_t)(BKM ? ((int64_t)(K - 1) * ldb + N) * 4 : ((int64_t)(N - 1) * ldb + K) * 4);
+  // operand extents in bytes (row image: R rows of ld; k image: K rows of ld); with KCAT the
+  // first operands end at k = kcat (the host checked that extent, not K's)
+  const int K1 = KCAT ? cat.kcat : K;
+  const uint32_t a_bytes = (uint32_t)(AK ? ((int64_t)(K1 - 1) * lda + M) * 4 : ((int64_t)(M - 1) * lda + K1) * 4);
+  const uint32_t b_bytes = (uint32_t)(BKM ? ((int64_t)(K1 - 1) * ldb + N) * 4 : ((int64_t)(N - 1) * ldb + K1) * 4);
   const __amdgpu_buffer_rsrc_t rsa = x3_rsrc(A, a_bytes), rsb = x3_rsrc(B, b_bytes);
   const uint32_t a_kstride = AK ? (uint32_t)lda * 4u : 4u, b_kstride = BKM ? (uint32_t)ldb * 4u : 4u;
   StageAddr<BM, AK> aa;
@@ -727,7 +729,7 @@ int gemm_x3_cat_launch(const X3Args& a, const float* A2, int64_t lda2, const flo
   if (a.bm == 128 && a.bn == 64) return launch_cat<128, 64>(a, c, st);
   if (a.bm == 64 && a.bn == 128) return launch_cat<64, 128>(a, c, st);
   if (a.bm == 64 && a.bn == 64) return launch_cat<64, 64>(a, c, st);
-  return PG_ERR_INVALID;
+  return PG_ERR_UNSUPPORTED;  // a tile with no cat instantiation: the caller concatenates
 }
 #else
 int gemm_x3_cat_launch(const X3Args&, const float*, int64_t, const float*, int64_t, int, hipStream_t) {

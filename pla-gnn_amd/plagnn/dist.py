@@ -70,7 +70,8 @@ class BucketAllReduce:
     def __init__(self, flat: torch.Tensor, buckets):
         self.flat = flat
         self.buckets = [(int(a), int(b)) for a, b in buckets if b > a]
-        # (a one-rank RCCL group still runs the collective: scripts/probes/dp_capture_probe.py)
+        # (a one-rank RCCL group still runs the collective: captured and replayed in
+        # tests/test_gpu_dist_engine.py::test_rccl_allreduce_in_step_graph_one_rank)
         self.active = dist.is_initialized()
         self.capturable = flat.is_cuda and self.active and dist.get_backend() == "nccl"
         self.stream = torch.cuda.Stream(flat.device) if self.capturable else None

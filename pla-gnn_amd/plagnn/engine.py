@@ -613,8 +613,31 @@ class TrainEngine:
         that bucket's grouped launch now, and with RCCL start its all-reduce, which then
         overlaps the rest of the backward."""
         if self._split_buckets and l == self.L - 1 and self.L > 1:
+            self._check_bucket_pending(0)
             self._reduce_deferred()
             self._bucket_done(0)
+
+    def _check_bucket_pending(self, i: int) -> None:
+        """Bucket i's all-reduce may start only once every gradient inside its range has been
+        issued: each parameter block in the range must be the output (or row-sum output) of a
+        weight-gradient launch still pending in this flush (a Wcp block is written as its Wcat
+        rows and its Wpool rows; its zero pad is never written). Ungrouped weight gradients
+        (the GROUP_WGRAD = False A/B knob) were launched in stream order already."""
+        if not self.GROUP_WGRAD:
+            return
+        a, b = self.grad_buckets()[i]
+        pending = set()
+        for q, _ in self._parts:
+            pending.update((q.C or 0, q.rowsum or 0))
+        for j in getattr(self, "_jobs", []):
+            pending.update((j.C or 0, j.rowsum or 0))
+        need = []
+        for name, off in self.flat_layout.offsets.items():
+            if a <= off < b:
+                need += [name[:-3] + "Wcat", name[:-3] + "Wpool"] if name.endswith("Wcp") else [name]
+        missing = [n for n in need if ptr(self.G[n]) not in pending]
+        if missing:
+            raise RuntimeError(f"gradient bucket {i} {a}:{b} would be all-reduced before {missing} are written")
 
     def _bucket_done(self, i: int) -> None:
         if self._ar_inline is not None and self._filter is None:
@@ -628,7 +651,16 @@ class TrainEngine:
                  self.flat.numel(), ptr(self.adam_state), self.betas[0], self.betas[1], self.eps, 0.0, st)
 
     def _uses_buckets(self, allreduce) -> None:
-        self._split_buckets = allreduce is not None and len(getattr(allreduce, "buckets", ())) > 1
+        """A bucketed all-reduce must hold exactly grad_buckets(): the backward launches bucket
+        i by position (bucket 0 at the top layer's boundary, the last one at the end), so any
+        other list would reduce a range before the backward has written it, or index past it."""
+        bk = getattr(allreduce, "buckets", None) if allreduce is not None else None
+        if bk is not None:
+            want = [tuple(int(v) for v in b) for b in self.grad_buckets()]
+            got = [tuple(int(v) for v in b) for b in bk]
+            if got != want:
+                raise ValueError(f"all-reduce buckets {got} are not this engine's grad_buckets() {want}")
+        self._split_buckets = bk is not None and len(bk) > 1
 
     def step_eager(self, allreduce=None) -> None:
         self._uses_buckets(allreduce)

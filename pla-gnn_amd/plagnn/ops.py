@@ -534,7 +534,9 @@ class SagePool(torch.autograd.Function):
         """A layer whose input needs no padding (4-aligned width): H is the caller's tensor
         and M its own buffer, fc_self + fc_neigh one product over the two K pieces
         ([H | M] [Wself | Wneigh]^T, pg_gemm_f32_cat), no [H | M] copy and no weight
-        concatenation. None when the library does not take the operands."""
+        concatenation; where the library does not take the operands (a misaligned h or
+        bias, an odd output width), the same product on the two concatenations, reusing P, M
+        and argpos (the aggregation is not redone)."""
         N, Fin = h.shape
         w_pool, w_self, w_neigh = w_pool.contiguous(), w_self.contiguous(), w_neigh.contiguous()
         P = torch.empty(N, Fin, dtype=torch.float32, device=h.device)
@@ -544,7 +546,7 @@ class SagePool(torch.autograd.Function):
         spmm_max(dg, P, ew_slots, out=M, argpos=argpos, dead_none=True)
         Y = gemm_cat(h, M, w_self, w_neigh, transb=True, bias=bias)
         if Y is None:
-            return None
+            Y = gemm(torch.cat([h, M], 1), torch.cat([w_self, w_neigh], 1), transb=True, bias=bias)
         ctx.gpu = ctx.cat = True
         ctx.save_for_backward(h, M, P, argpos, w_pool, w_self, w_neigh, ew_slots)
         ctx.fin = Fin

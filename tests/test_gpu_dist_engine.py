@@ -251,3 +251,35 @@ def test_rccl_allreduce_in_step_graph_one_rank(tmp_path):
     got = torch.load(tmp_path / "rccl1.pt", weights_only=True)
     for k, v in got["eager"].items():
         assert torch.equal(got["graph"][k], v), f"in-graph RCCL step differs from the eager one on {k}"
+
+
+def test_engine_rejects_buckets_it_does_not_launch():
+    """the backward launches the all-reduce of bucket i by position, so a bucket
+    list other than grad_buckets() (one bucket for a two-bucket engine, or the two in the
+    natural order, whose lower range the backward has not written at the first launch) must
+    be rejected before anything runs; and bucket 0's launch point must find every gradient
+    of its range pending in the flush it follows."""
+    import plagnn
+    from plagnn import dist as pdist
+
+    src, dst, n, x, labels, tr, va = _problem(0)
+    loops = np.arange(n)
+    g = plagnn.CSRGraph(np.concatenate([src, loops]), np.concatenate([dst, loops]), n)
+    eng = plagnn.TrainEngine(g, x, labels, DIMS, _weights(), tr, va, lr=LR, device="cuda:0", params=_params())
+    (a, nn_), (z, a2) = eng.grad_buckets()
+    assert nn_ == eng.gflat.numel() and z == 0 and a2 == a
+    for bad in ([(0, nn_)], [(0, a), (a, nn_)]):
+        ar = pdist.BucketAllReduce(eng.gflat, bad)
+        with pytest.raises(ValueError, match="grad_buckets"):
+            eng.capture(warmup=1, allreduce=ar)
+        with pytest.raises(ValueError, match="grad_buckets"):
+            eng.step_eager(ar)
+    assert eng.steps_done == 0
+    # the boundary check itself: with the top layer's parts dropped from the flush, bucket 0
+    # is not fully written, and the check says which gradients are missing
+    eng._uses_buckets(pdist.BucketAllReduce(eng.gflat, eng.grad_buckets()))
+    eng.forward()
+    eng._parts = []
+    with pytest.raises(RuntimeError, match="liner1.W"):
+        eng._check_bucket_pending(0)
+    eng._parts = []
