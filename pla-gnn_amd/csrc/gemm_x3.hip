@@ -171,17 +171,6 @@ struct Stage {
     }
   }
 #endif
-  // unit i alone (the interleaved K step places the units between its MFMAs)
-  template <int IMG>
-  __device__ __forceinline__ void store_unit(uint16_t* __restrict__ S, int tid, int i) const {
-    int row, k;
-    unit_pos(tid + i * NT, row, k);
-    uint2 pc[3];
-    split4(v[i], pc);
-    const int off = img_off<ROWS, KMAJ>(row, k);
-#pragma unroll
-    for (int piece = 0; piece < 3; ++piece) *reinterpret_cast<uint2*>(S + piece * IMG + off) = pc[piece];
-  }
   // split and store the three pieces (images of IMG u16 each, consecutive)
   template <int IMG>
   __device__ __forceinline__ void store(uint16_t* __restrict__ S, int tid) const {
@@ -361,45 +350,16 @@ __device__ unsigned long long pg_x3_stamp[64][66][4];
 template <int BM, int BN>
 constexpr int x3_depth() { return BM * BN <= 128 * 64 ? 2 : 1; }
 
-#ifndef PG_X3_ILV
-#define PG_X3_ILV 0  // variant builds: staging of tile t + 1 interleaved with tile t's MFMAs
-#endif
-#ifndef PG_X3_ILV_BIGD2
-#define PG_X3_ILV_BIGD2 0  // interleaved: 128 x 128 tiles also two K tiles ahead
-#endif
-#ifndef PG_X3_ILV_P0_D2
-#define PG_X3_ILV_P0_D2 2  // sixteenths of a step's MFMAs issued before the staging (two ahead)
-#endif
-#ifndef PG_X3_ILV_P0_D1
-#define PG_X3_ILV_P0_D1 8  // the same, one ahead (its loads were issued at the step's top)
-#endif
-#ifndef PG_X3_ILV_PAT
-#define PG_X3_ILV_PAT 4  // 4: written-out order (3: sched_group_barrier pattern)
-#endif
-#ifndef PG_X3_ILV_VALU
-#define PG_X3_ILV_VALU 26  // VALU instructions of one unit's split (sched estimate)
-#endif
-// tiles that take the interleave without spilling (measured register counts): not the
-// k-image A operands (transposed A: split-K weight gradients outside the group), and of the
-// A B (B a k image) only tiles of <= 128 x 64 rows x columns
-template <int BM, int BN, bool TA, bool TB>
-constexpr bool x3_ilv_ok() { return PG_X3_ILV && !TA && (TB || (BM >= BN && BM * BN <= 128 * 64)); }
-template <int BM, int BN>
-constexpr int x3_ilv_depth() { return BM * BN <= 128 * 64 || (PG_X3_ILV_BIGD2 && BM * BN <= 128 * 128) ? 2 : 1; }
-
 // Waves per SIMD the register allocation must allow. 128 x 128 tiles (48 KB of LDS, three
 // per CU by LDS): left unbounded the compiler took 152 VGPRs + 64 AGPRs (216 allocated:
 // two waves per SIMD, so two workgroups per CU); bounded to three it fits 145-153 VGPRs,
 // no AGPRs, no spills.
-#ifndef PG_X3_WAVES_D2
-#define PG_X3_WAVES_D2 4
-#endif
 #ifndef PG_X3_WAVES_BIG
 #define PG_X3_WAVES_BIG 3
 #endif
 template <int BM, int BN>
 constexpr int x3_waves() {
-  return x3_depth<BM, BN>() == 2 ? PG_X3_WAVES_D2 : BM * BN <= 128 * 128 ? PG_X3_WAVES_BIG : 2;
+  return x3_depth<BM, BN>() == 2 ? 4 : BM * BN <= 128 * 128 ? PG_X3_WAVES_BIG : 2;
 }
 
 template <int BM, int BN>
@@ -421,10 +381,7 @@ struct X3Cat {
   int64_t ldb2;
   int kcat;
 };
-#ifndef PG_X3_ILV_GROUP
-#define PG_X3_ILV_GROUP 0  // the grouped weight gradients too (128 x 256: at the register limit)
-#endif
-template <int BM, int BN, bool TA, bool TB, int EPI, bool KCAT = false, bool ILV = PG_X3_ILV>
+template <int BM, int BN, bool TA, bool TB, int EPI, bool KCAT = false>
 __device__ __forceinline__ void x3_tile(
     uint16_t* __restrict__ lds, int M, int N, int K, int k_per_split, int kz, int tm, int tn, float alpha,
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
@@ -536,127 +493,6 @@ __device__ __forceinline__ void x3_tile(
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
       }
   };
-  if constexpr (ILV) {
-  // Interleaved K steps: the split and LDS stores of the next K tile are issued between the
-  // MFMAs of the current one (sched_group_barrier), so a wave's staging runs in the shadow
-  // of its own matrix-pipe work instead of after it (co-resident workgroups of one launch
-  // stay in phase, so their staging and MFMA phases did not overlap either). Every step is
-  // one basic block: its loads, fragment reads, MFMAs and stores are unconditional.
-  {
-    constexpr int DEPTH = x3_ilv_depth<BM, BN>();
-    constexpr int PA = Stage<BM, AK>::PER, PB = Stage<BN, BKM>::PER;
-    constexpr int NM = 6 * TM * TN;
-    constexpr int NRD = 3 * (TM * (AK ? 2 : 1) + TN * (BKM ? 2 : 1));
-    constexpr int NLD = (PA + PB) * (KCAT ? 2 : 1);
-    constexpr int NWR = 3 * (PA + PB);
-    constexpr int P0 = DEPTH == 2 ? PG_X3_ILV_P0_D2 * NM / 16 : PG_X3_ILV_P0_D1 * NM / 16;
-    constexpr int GAPS = NM - P0;
-    constexpr int VPG = (PG_X3_ILV_VALU * (PA + PB) + GAPS - 1) / GAPS;
-    constexpr int WPG = (NWR + GAPS - 1) / GAPS;
-    auto schedule = [&]() {
-#if PG_X3_ILV_PAT == 0 || PG_X3_ILV_PAT == 2
-      __builtin_amdgcn_sched_group_barrier(0x020, NLD, 0);  // VMEM reads: the next loads
-#endif
-#if PG_X3_ILV_PAT == 0 || PG_X3_ILV_PAT == 3
-      __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);  // DS reads: this tile's fragments
-#endif
-#pragma unroll
-      for (int i = 0; i < P0; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-#pragma unroll
-      for (int i = 0; i < GAPS; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);  // VALU: the split
-        __builtin_amdgcn_sched_group_barrier(0x200, WPG, 0);  // DS writes: the pieces
-      }
-    };
-    // step t: loads of tile kl into (la, lb), MFMAs of LDS buffer t & 1, tile t + 1 from
-    // (na, nb) split and stored into the other buffer; then its row sums and the barrier
-    auto step = [&](int t, int kl, Stage<BM, AK>& la, Stage<BN, BKM>& lb, Stage<BM, AK>& na, Stage<BN, BKM>& nb) {
-      const int cur = t & 1;
-      load_a(la, kl);
-      load_b(lb, kl);
-#if PG_X3_ILV_PAT >= 3
-      __builtin_amdgcn_sched_barrier(0);  // the loads (and their offsets) first, as their own region
-#endif
-      const uint16_t* As = lds + cur * BUF;
-      uint16_t* nx = lds + (cur ^ 1) * BUF;
-#if PG_X3_ILV_PAT == 4
-      // written-out order: every fragment read, then the MFMAs with unit u's split and
-      // stores after MFMA P0 + u (NM - P0) / NU, each such chunk fenced (sched_barrier)
-      {
-        const uint16_t* Bs = As + 3 * IA;
-        bf16x8 fa[3][TM], fb[3][TN];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i) fa[p][i] = frag<BM, AK>(As + p * IA, ra + i * 32, lane);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) fb[p][j] = frag<BN, BKM>(Bs + p * IB, rb + j * 32, lane);
-        }
-        constexpr int NU = PA + PB;
-        constexpr int PAIRS[6][2] = {{0, 2}, {2, 0}, {1, 1}, {0, 1}, {1, 0}, {0, 0}};
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-          const int ij = m / 6, q = m % 6, i = ij / TN, j = ij % TN;
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PAIRS[q][0]][i], fb[PAIRS[q][1]][j], acc[i][j], 0, 0, 0);
-#pragma unroll
-          for (int u = 0; u < NU; ++u) {
-            if (m == P0 + u * (NM - P0) / NU) {
-              if (u < PA) na.template store_unit<IA>(nx, tid, u);
-              else nb.template store_unit<IB>(nx + 3 * IA, tid, u - PA);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          }
-        }
-      }
-#else
-      mfmas(As, As + 3 * IA);
-      na.template store<IA>(nx, tid);
-      nb.template store<IB>(nx + 3 * IA, tid);
-      schedule();
-#endif
-      if (do_rs) na.rowsum(rs);
-      __syncthreads();
-    };
-    auto last = [&](int t) {
-      const uint16_t* As = lds + (t & 1) * BUF;
-      mfmas(As, As + 3 * IA);
-      __syncthreads();  // the epilogue reuses the LDS
-    };
-    if (nk > 0) {
-      load_a(sa, kz0);
-      load_b(sb, kz0);
-      if constexpr (DEPTH == 2) {
-        Stage<BM, AK> sa2;
-        Stage<BN, BKM> sb2;
-        const int k1c = kz0 + min(1, nk - 1) * KS;
-        load_a(sa2, k1c);
-        load_b(sb2, k1c);
-        if (do_rs) sa.rowsum(rs);
-        sa.template store<IA>(lds, tid);
-        sb.template store<IB>(lds + 3 * IA, tid);
-        __syncthreads();
-        int t = 0;
-        for (; t + 2 < nk; t += 2) {
-          step(t, kz0 + min(t + 2, nk - 1) * KS, sa, sb, sa2, sb2);
-          step(t + 1, kz0 + min(t + 3, nk - 1) * KS, sa2, sb2, sa, sb);
-        }
-        if (t + 1 < nk) {
-          step(t, kz0 + (nk - 1) * KS, sa, sb, sa2, sb2);
-          ++t;
-        }
-        last(t);
-      } else {
-        if (do_rs) sa.rowsum(rs);
-        sa.template store<IA>(lds, tid);
-        sb.template store<IB>(lds + 3 * IA, tid);
-        __syncthreads();
-        for (int t = 0; t + 1 < nk; ++t) step(t, kz0 + (t + 1) * KS, sa, sb, sa, sb);
-        last(nk - 1);
-      }
-    }
-  }
-  } else {
   if (x3_depth<BM, BN>() == 2 && nk > 0) {
     // tiles two K steps ahead in registers (two stage slots, the loop unrolled by two so
     // the slots are static): step t loads tile t + 2 (clamped to the last tile, so the
@@ -730,7 +566,6 @@ __device__ __forceinline__ void x3_tile(
       __syncthreads();  // the next buffer is complete; every wave is past its reads of this one
     }
   }
-  }
 
   // row sums of op(A) (float64 partials per thread, combined in a fixed order)
   if (do_rs) {
@@ -787,10 +622,8 @@ void gemm_x3_kernel(
   __shared__ __attribute__((aligned(16))) uint16_t lds[x3_lds_u16<BM, BN>()];
   const int item = x3_item(tiles * n_split);
   const int kz = item / tiles, tile = item % tiles;
-  x3_tile<BM, BN, TA, TB, EPI, false, x3_ilv_ok<BM, BN, TA, TB>()>(lds, M, N, K, k_per_split, kz, tile / tiles_n,
-                                                                  tile % tiles_n, alpha, A, lda, B, ldb, beta, C,
-                                                                  ldc, bias, slope, dact, lddact, rowsum, ws,
-                                                                  ws_rowsum);
+  x3_tile<BM, BN, TA, TB, EPI>(lds, M, N, K, k_per_split, kz, tile / tiles_n, tile % tiles_n, alpha, A, lda, B,
+                               ldb, beta, C, ldc, bias, slope, dact, lddact, rowsum, ws, ws_rowsum);
 }
 
 // K-concatenated operands (X3Cat), no split-K: the drop-in layers' products
@@ -803,7 +636,7 @@ void gemm_x3_cat_kernel(
     const float* __restrict__ dact, int64_t lddact, X3Cat cat) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[x3_lds_u16<BM, BN>()];
   const int tile = x3_item(tiles);
-  x3_tile<BM, BN, TA, TB, EPI, true, false>(lds, M, N, K, K, 0, tile / tiles_n, tile % tiles_n, alpha, A, lda, B, ldb, beta, C,
+  x3_tile<BM, BN, TA, TB, EPI, true>(lds, M, N, K, K, 0, tile / tiles_n, tile % tiles_n, alpha, A, lda, B, ldb, beta, C,
                                      ldc, bias, slope, dact, lddact, nullptr, nullptr, nullptr, cat);
 }
 
@@ -820,8 +653,7 @@ void gemm_x3_group_kernel(X3Group g) {
   const X3Part& p = g.p[k];
   const int local = item - p.first_item;
   const int kz = local / p.tiles, tile = local % p.tiles;
-  x3_tile<BM, BN, TA, TB, EPI_SPLIT, false, PG_X3_ILV_GROUP>(lds, p.M, p.N, p.K, p.kps, kz, tile / p.tiles_n,
-                                                             tile % p.tiles_n, 1.f, p.A,
+  x3_tile<BM, BN, TA, TB, EPI_SPLIT>(lds, p.M, p.N, p.K, p.kps, kz, tile / p.tiles_n, tile % p.tiles_n, 1.f, p.A,
                                      p.lda, p.B, p.ldb, 0.f, nullptr, 0, nullptr, 0.f, nullptr, 0, p.rowsum, p.ws,
                                      p.ws_rowsum);
 }

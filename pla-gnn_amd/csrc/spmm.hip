@@ -1161,115 +1161,6 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   }
 }
 
-#ifndef PG_PULL_PERS
-#define PG_PULL_PERS 0  // variant builds: persistent pull waves that prefetch the next items
-#endif
-#ifndef PG_PULL_PERS_BLOCKS
-#define PG_PULL_PERS_BLOCKS 2048  // 256 CUs x 8 workgroups of 4 waves (8 waves per SIMD)
-#endif
-
-// Pass 2 (pull) with persistent waves: wave w takes items w, w + S, w + 2S, ... (S = the
-// grid's waves; the schedule is longest-first, so the deal stays balanced) and carries a
-// pipeline across them: while item c's lists are fetched, item c + S's first-window
-// descriptors (and destinations) and item c + 2S's header and first-window slots are in
-// flight, so the dependent header -> slot -> descriptor chain of the next items overlaps
-// this item's list fetches instead of starting after its store. Same per-item arithmetic
-// and order as max_bwd_pull_kernel (bitwise the same sums). Loads are unconditional with
-// clamped indices (nnz >= 1: the caller runs the plain kernel on an edgeless graph).
-template <typename T, typename R, bool TR>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void max_bwd_pull_pers_kernel(
-    const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items, int nnz,
-    const int32_t* __restrict__ tdst, const uint32_t* __restrict__ glist, R gp, int F,
-    const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx, float* __restrict__ ws,
-    int64_t ldw) {
-  constexpr int U = PG_PULL_U;
-  __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
-  const int wave = wave_id_uniform();
-  const int S = gridDim.x * kWavesPerBlock;
-  int it = blockIdx.x * kWavesPerBlock + wave;
-  if (it >= n_items) return;
-  float* acc = accs[wave];
-  const int lane = lane_id();
-  for (int f = lane; f < F; f += kWave) acc[f] = 0.f;
-  // the lane's edge of the window starting at tw (clamped into the row, then into the array)
-  auto tl = [&](int tw, int t1) { return max(0, min(tw + min(lane, t1 - tw - 1), nnz - 1)); };
-  auto hdr = [&](int i) { return items[min(i, n_items - 1)]; };
-  int4 cur = items[it];
-  uint32_t dsc_c = glist[TR ? tl(cur.y, cur.z) : tslot[tl(cur.y, cur.z)]];
-  int vf_c = tdst[tl(cur.y, cur.z)] * F;
-  int4 nxt = hdr(it + S);
-  int ts_n = TR ? 0 : tslot[tl(nxt.y, nxt.z)];
-  for (;;) {
-    const int row = cur.x, t0 = cur.y, t1 = cur.z, slot = cur.w;
-    // in flight beside this item's lists: item it + S's first-window descriptors, item
-    // it + 2S's header
-    const uint32_t dsc_n = glist[TR ? tl(nxt.y, nxt.z) : ts_n];
-    const int vf_n = tdst[tl(nxt.y, nxt.z)] * F;
-    const int4 nn = hdr(it + 2 * S);
-    uint32_t dsc_next = dsc_c;
-    int vf_next = vf_c, ts_next = 0;
-    if (!TR && t0 + kWave < t1) ts_next = tslot[tl(t0 + kWave, t1)];
-    for (int tw = t0; tw < t1; tw += kWave) {
-      const int nw = min(kWave, t1 - tw);
-      const int2 dsc = make_int2(vf_next + (int)(dsc_next & 0xFFFFu), (int)(dsc_next >> 16));
-      if (tw + kWave < t1) {
-        dsc_next = glist[TR ? tl(tw + kWave, t1) : ts_next];
-        vf_next = tdst[tl(tw + kWave, t1)] * F;
-        if (!TR && tw + 2 * kWave < t1) ts_next = tslot[tl(tw + 2 * kWave, t1)];
-      }
-      const int nseg = lane < nw ? (dsc.y + kWave - 1) / kWave : 0;
-      const int incl = wave_incl_add(nseg);
-      const int excl = incl - nseg;
-      const int nseg_all = bcast(incl, kWave - 1);
-      for (int s0 = 0; s0 < nseg_all; s0 += U) {
-        const int nv = min(U, nseg_all - s0);
-        int fe[U], ne[U];
-        float de[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int t = s0 + min(u, nv - 1);
-          const int i = __popcll(__ballot(excl <= t)) - 1;
-          const int seg = t - bcast(excl, i);
-          const int base = bcast(dsc.x, i) + seg * kWave;
-          const int n = min(kWave, bcast(dsc.y, i) - seg * kWave);
-          ne[u] = n;
-          gp.get(base + min(lane, n - 1), fe[u], de[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (u < nv && lane < ne[u]) acc[fe[u]] += de[u];
-      }
-    }
-    // item it + 2S's first-window slots, for the next iteration's descriptor loads
-    const int ts_nn = TR ? 0 : tslot[tl(nn.y, nn.z)];
-    wave_lds_sync();
-    if (slot < 0) {
-      T* xr = dx + (int64_t)row * ldx;
-      const T* mr = mask ? mask + (int64_t)row * ldm : nullptr;
-      for (int f = lane; f < F; f += kWave) {
-        float a = acc[f];
-        acc[f] = 0.f;
-        if (mr && !(to_f(mr[f]) > 0.f)) a = 0.f;
-        xr[f] = from_f<T>(a);
-      }
-    } else {
-      float* wr = ws + (int64_t)slot * ldw;
-      for (int f = lane; f < F; f += kWave) {
-        wr[f] = acc[f];
-        acc[f] = 0.f;
-      }
-    }
-    wave_lds_sync();
-    it += S;
-    if (it >= n_items) break;
-    cur = nxt;
-    nxt = nn;
-    dsc_c = dsc_n;
-    vf_c = vf_n;
-    ts_n = ts_nn;
-  }
-}
-
 // Sum partial slots in order; optional relu' mask (bwd) or 1/deg (mean fwd).
 // One workgroup per split row, one thread per feature.
 template <typename T = float>
@@ -1832,14 +1723,9 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     // in the lists has a maximum X[u,f] w != 0, so X[u,f] > 0; an element with no entries
     // sums to +0, which the mask would leave +0. With fwd_out alone the mask is applied.
     if (dead_none) mask_src = nullptr;
-    if (PG_PULL_PERS && gt->nnz > 0 && blocks > PG_PULL_PERS_BLOCKS)
-      hipLaunchKernelGGL((max_bwd_pull_pers_kernel<T, R, TR>), dim3(PG_PULL_PERS_BLOCKS), dim3(kBlock), 0, st,
-                         gt->eslot, (const int4*)gt->items, (int)gt->n_items, (int)gt->nnz, gt->col, glist, gp,
-                         (int)F, mask_src, ldm, dx, ldx, w, ws_ld(F));
-    else
-      hipLaunchKernelGGL((max_bwd_pull_kernel<T, R, TR>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
-                         (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
-                         dx, ldx, w, ws_ld(F));
+    hipLaunchKernelGGL((max_bwd_pull_kernel<T, R, TR>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
+                       (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
+                       dx, ldx, w, ws_ld(F));
     if (gt->n_merges > 0)
       hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
                          (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
