@@ -651,7 +651,12 @@ def main(argv=None):
     ap.add_argument("--dump-breakdown", default="", help="write the per-launch-site breakdown (JSON)")
     ap.add_argument("--dropin-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--chunk-bwd", type=int, default=0, help=argparse.SUPPRESS)  # tuning experiments
+    ap.add_argument("--separate-l1-head", action="store_true", help=argparse.SUPPRESS)  # A/B: unfused MLP head
     args = ap.parse_args(argv)
+    if args.separate_l1_head:
+        import plagnn.engine
+
+        plagnn.engine.TrainEngine.FUSED_L1_HEAD = False
     if args.chunk_bwd:
         import plagnn.graph
 

@@ -240,6 +240,25 @@ int pg_mlp_head(const void* A4, int64_t lda, int64_t n, int32_t K, int a_dtype, 
                 float* prob, int64_t ldp, float* dz, int64_t lddz, void* dz_bf16, void* dA4,
                 int64_t ldg, float slope, float* loss2, void* ws, size_t ws_bytes,
                 pg_stream_t stream);
+/* liner1 + the head above + liner1's input gradient in one pass (ABI 12; f32; replaces the
+ * fwd.liner1 GEMM, pg_mlp_head and the dgrad.liner1 GEMM of a training step, code/model.py:
+ * 26-29 and their backward):
+ *   A4 = leaky(H3 W1^T + b1);  then pg_mlp_head's outputs on A4 (prob, dz, dA4, loss2);
+ *   dH3 = (dA4 W1) * leaky'(H3)  (liner1's input gradient through the last SAGE layer's
+ *   leaky_relu, with negative slope `slope` for both activations).
+ * H3 [n][F3], W1 [K1][F3], b1 [K1], A4 [n][K1], dA4 [n][K1], dH3 [n][F3] f32; F3 % 4 == 0,
+ * K1 <= 128, C <= 16; H3, W1, W2 16-B aligned with leading dimensions multiples of 4. The two
+ * products are computed exactly as pg_gemm_f32's three-piece kernel computes them (same
+ * split, same k order and MFMA sequence), so A4 and dH3 equal its results bitwise. prob and
+ * dz are optional (NULL). Scratch (256-B aligned): pg_mlp_l1_head_workspace(n, C, F3, K1)
+ * bytes (the head's partial sums and W1's bf16 pieces, split once per call); F3 <= 4096. */
+size_t pg_mlp_l1_head_workspace(int64_t n, int32_t C, int32_t F3, int32_t K1);
+int pg_mlp_l1_head(const float* H3, int64_t ldh, int64_t n, int32_t F3, const float* W1, int64_t ldw1,
+                   const float* b1, int32_t K1, float* A4, int64_t lda4, const float* W2, int64_t ldw,
+                   const float* b2, int32_t C, const float* labels, int64_t ldl, const float* class_w,
+                   const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob, int64_t ldp,
+                   float* dz, int64_t lddz, float* dA4, int64_t ldg, float* dH3, int64_t lddh, float slope,
+                   float* loss2, void* ws, size_t ws_bytes, pg_stream_t stream);
 size_t pg_sigmoid_multi_loss_workspace(int64_t n_index, int32_t C);
 int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C,
                           const float* labels, int64_t ldl, const float* class_w,
@@ -500,7 +519,7 @@ int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-
                          relu' mask is applied, only PG_ARG_DEAD_NONE implies it;
                          9: pg_gemm_f32_group; 10: the in-CSR's epos = transposed
                          indices (transposed max-backward descriptors), pg_gemm_f32_cat;
-                         11: pg_pad2d_group */
+                         11: pg_pad2d_group; 12: pg_mlp_l1_head */
 
 #ifdef __cplusplus
 }

@@ -29,17 +29,18 @@
 
 #include "common.hpp"
 #include "gemm_common.hpp"
+#include "x3_split.hpp"
 
 namespace {
 
 using namespace pg_gemm;
+using pg_x3::split4;
 
 constexpr int KS = 16;  // k per K step
 constexpr int NT = 256;
 
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
-using bf16x2 = __attribute__((ext_vector_type(2))) __bf16;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 using lds_bf16x4 = __attribute__((address_space(3))) bf16x4;
 
@@ -68,29 +69,6 @@ __device__ __forceinline__ bf16x8 frag(const uint16_t* __restrict__ S, int rc, i
   }
 }
 
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-  const bf16x2 v = {static_cast<__bf16>(a), static_cast<__bf16>(b)};  // v_cvt_pk_bf16_f32 (RNE)
-  return __builtin_bit_cast(uint32_t, v);
-}
-// low bf16 of a packed pair widened to f32 by v_perm_b32 (the shift form gets rewritten into
-// an extra cvt)
-__device__ __forceinline__ float lo_f(uint32_t p) { return __uint_as_float(__builtin_amdgcn_perm(0u, p, 0x01000c0cu)); }
-__device__ __forceinline__ float hi_f(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
-
-// three-piece split of 4 floats: out[piece] = 4 bf16 (8 B)
-__device__ __forceinline__ void split4(const float4 v, uint2 (&out)[3]) {
-  float r[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int piece = 0; piece < 3; ++piece) {
-    const uint32_t p0 = pk_bf16(r[0], r[1]), p1 = pk_bf16(r[2], r[3]);
-    out[piece] = make_uint2(p0, p1);
-    if (piece < 2) {
-      r[0] = r[0] - lo_f(p0); r[1] = r[1] - hi_f(p0);
-      r[2] = r[2] - lo_f(p1); r[3] = r[3] - hi_f(p1);
-    }
-  }
-}
-
 // One operand's K tile: ROWS x KS, float4 units; row image unit = (row, 4 k), k image unit
 // = (k, 4 rows).
 __device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written; read as a float4
@@ -102,12 +80,7 @@ __device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
 // One operand's buffer descriptor (wave-uniform: built from readfirstlane'd inputs, so the
 // compiler keeps it in SGPRs) covering `bytes` from P; every byte offset of the operand is
 // below 2^32 (x3_ok checks the extent on the host).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t x3_rsrc(const float* P, uint32_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(P);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  void* base = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t x3_rsrc(const float* P, uint32_t bytes) { return pg_x3::rsrc(P, bytes); }
 constexpr uint32_t kX3Oob = 0xFFFFFFF0u;  // a byte offset past every descriptor's range: reads 0
 
 template <int ROWS, bool KMAJ>

@@ -17,6 +17,7 @@
 #include <cmath>
 
 #include "common.hpp"
+#include "x3_split.hpp"
 
 namespace {
 
@@ -222,6 +223,316 @@ __global__ __launch_bounds__(64 * kMaxC) void head_final_kernel(const float* __r
   }
 }
 
+// ---- liner1 + head + liner1's input gradient, fused (f32) --------------------------------
+// The MLP on top of the last SAGE layer for one block of kL1Rows rows, in one pass:
+//   A4  = leaky(H3 W1^T + b1)                (code/model.py:26-27; written out: liner2's weight
+//                                             gradient reads it)
+//   z, prob, loss terms, dz, dA4            (head_kernel above, on A4 held in LDS)
+//   dH3 = (dA4 W1) * leaky'(H3)              (liner1's input gradient with the top SAGE layer's
+//                                             activation backward: that layer's dY)
+// Both products run as the three-piece GEMM does (gemm_x3.hip): the same split, the same
+// 16-k steps in the same order, the same six MFMAs per block, zero past K; so A4 and dH3
+// are bitwise the x3 GEMM's (and the head's outputs bitwise head_kernel's). Before, these
+// were three launches (fwd.liner1, the head, dgrad.liner1: ~60 us per cfg2 step, the two
+// GEMMs at ~60 TF/s: N = 104 columns on 64 x 64 tiles, K = 104 in 7 steps) that each
+// streamed A3 / A4 / dA4 through memory.
+// Block: 4 waves, kL1Rows = 32 rows. Phase 1: wave w owns A4 columns [32w, 32w + 32) (one
+// 32 x 32 tile); the H3 rows go through LDS as three bf16 pieces in chunks of kL1Kc columns,
+// W1's rows come straight from L2 into registers (each W1 element feeds one lane). Phase 3:
+// wave w owns dH3 columns [64w, 64w + 64) of each 256-column chunk (two tiles); dA4's pieces
+// sit in LDS, W1's columns come from L2 (8 rows x 32 consecutive columns per fragment).
+constexpr int kL1Rows = 32;
+constexpr int kL1Kc = 128;               // phase-1 K chunk staged in LDS
+constexpr int kL1SA = kL1Kc + 8;         // piece row stride (u16): ds_read_b128 rows 4 banks apart
+constexpr int kL1K1 = 128;               // liner1 width max (4 waves x 32 columns)
+constexpr int kL1PD = 4;                 // W1 fragments in flight per wave (K steps ahead)
+#ifndef PG_L1_WAVES
+#define PG_L1_WAVES 3  // waves per SIMD the registers must allow (LDS: three blocks per CU)
+#endif
+
+using pg_x3::bf16x8;
+using pg_x3::f32x16;
+
+// dynamic LDS of one block (bytes) for liner1 width K1: the region that holds phase 1's H3
+// pieces, then A4 (-> dA4) f32 [32][S] and dA4's pieces [3][32][K16 + 8]
+__host__ __device__ inline int l1_region_bytes(int K1) {
+  const int S = (K1 + 3) / 4 * 4 + 4, K16 = (K1 + 15) / 16 * 16;
+  const int p1 = 3 * kL1Rows * kL1SA * 2;
+  const int p23 = kL1Rows * S * 4 + 3 * kL1Rows * (K16 + 8) * 2;
+  return (p1 > p23 ? p1 : p23 + 15) / 16 * 16;
+}
+
+// 8 consecutive floats -> the three bf16x8 fragments (pieces)
+__device__ __forceinline__ void split8(const float4 lo, const float4 hi, bf16x8 (&f)[3]) {
+  uint2 a[3], b[3];
+  pg_x3::split4(lo, a);
+  pg_x3::split4(hi, b);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) f[p] = __builtin_bit_cast(bf16x8, make_uint4(a[p].x, a[p].y, b[p].x, b[p].y));
+}
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WAVES))) void mlp_l1_head_kernel(
+    const float* __restrict__ h3, int64_t ldh, int n, int F3, const float* __restrict__ w1, int64_t ldw1,
+    const float* __restrict__ b1, int K1, float* __restrict__ a4g, int64_t lda4,
+    const float* __restrict__ w2, int64_t ldw, const float* __restrict__ b2, int C,
+    const float* __restrict__ labels, int64_t ldl, const float* __restrict__ cw,
+    const int8_t* __restrict__ row_set, float inv_n_train, float* __restrict__ prob, int64_t ldp,
+    float* __restrict__ dz, int64_t lddz, float* __restrict__ da4g, int64_t ldg,
+    float* __restrict__ dh3, int64_t lddh, float slope, float* __restrict__ part, int nb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char region[];
+  __shared__ __attribute__((aligned(16))) float w[kMaxC * (kMaxK + 4)];
+  __shared__ float g[kRows][kMaxC];
+  __shared__ float terms[2][kRows][kMaxC];
+  static_assert(kRows == kL1Rows, "head rows");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int K4 = (K1 + 3) / 4 * 4, S = K4 + 4, K16 = (K1 + 15) / 16 * 16, SD = K16 + 8;
+  uint16_t* sp = reinterpret_cast<uint16_t*>(region);                       // phase 1: [3][32][kL1SA]
+  float* a = reinterpret_cast<float*>(region);                              // phase 2: A4 -> dA4 [32][S]
+  uint16_t* sd = reinterpret_cast<uint16_t*>(region + kL1Rows * S * 4);     // phase 3: [3][32][SD]
+  const int r0 = blockIdx.x * kL1Rows;
+  const int nr = min(kL1Rows, n - r0);
+
+  // W2 into LDS (the head's operand), issued first
+  {
+    const int uw = C * (K4 / 4);
+    for (int u = tid; u < uw; u += kBlock) {
+      const int c = u / (K4 / 4), k = (u - c * (K4 / 4)) * 4;
+      *reinterpret_cast<float4*>(w + c * S + k) = ld4(w2, (int64_t)c * ldw, k, K1);
+    }
+  }
+  for (int i = tid; i < 2 * kRows * kMaxC; i += kBlock) (&terms[0][0][0])[i] = 0.f;
+
+  // ---- phase 1: A4 = leaky(H3 W1^T + b1) ----
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int n1 = 32 * wave + l32;                       // this lane's A4 column (W1 row)
+  const bool live1 = n1 < K1;
+  // W1 through a buffer descriptor over its K1 rows: rows past K1 read 0 (the range check
+  // covers the VGPR offset, which therefore carries the whole offset); every offset fits 32
+  // bits (the host checks the extents). Each block splits the W1 fragments it reads (a
+  // version reading pieces split once per call, in these layouts, was slower: 62 vs 44 us
+  // per cfg2 call, the transposed pieces' rows being 224 B apart)
+  const __amdgpu_buffer_rsrc_t rw1 = pg_x3::rsrc(w1, (uint32_t)K1 * (uint32_t)ldw1 * 4u);
+  const int vo1 = (n1 * (int)ldw1 + 8 * h) * 4;
+  // W1 row n1 at k = 16 s + 8 h .. + 7 (zero past F3)
+  auto ldb1 = [&](int s, float4& lo, float4& hi) {
+    const int k = 16 * s + 8 * h;
+    const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw1, vo1 + 64 * s, 0, 0));
+    const float4 y = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw1, vo1 + 64 * s + 16, 0, 0));
+    lo = k < F3 ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    hi = k + 4 < F3 ? y : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const int steps1 = (F3 + 15) / 16;
+  float4 bq[kL1PD][2];
+#pragma unroll
+  for (int i = 0; i < kL1PD; ++i) ldb1(min(i, steps1 - 1), bq[i][0], bq[i][1]);
+  for (int kc = 0; kc < F3; kc += kL1Kc) {
+    const int kn = min(kL1Kc, F3 - kc);
+    // stage H3[r0 .. r0 + 31][kc .. kc + kL1Kc) as pieces (zero past kn; rows past n read a
+    // clamped valid row, never stored)
+    {
+      constexpr int kPer = kL1Rows * kL1Kc / 4 / kBlock;  // 4 float4 units per thread
+      float4 v[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int u = tid + q * kBlock, row = u / (kL1Kc / 4), k4 = (u % (kL1Kc / 4)) * 4;
+        const float4 x = *reinterpret_cast<const float4*>(h3 + (int64_t)min(r0 + row, n - 1) * ldh + kc + min(k4, kn - 4));
+        v[q] = k4 < kn ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int u = tid + q * kBlock, row = u / (kL1Kc / 4), k4 = (u % (kL1Kc / 4)) * 4;
+        uint2 pc[3];
+        pg_x3::split4(v[q], pc);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(sp + (p * kL1Rows + row) * kL1SA + k4) = pc[p];
+      }
+    }
+    __syncthreads();
+    // the chunk's K steps (kL1Kc / 16 = 8, a multiple of kL1PD); W1 fragments kL1PD steps
+    // ahead in a register ring (loads unconditional, clamped; the MFMAs of steps past F3 skipped)
+    const int sc = kc / 16;
+#pragma nounroll
+    for (int i0 = 0; i0 < kL1Kc / 16; i0 += kL1PD) {
+#pragma unroll
+      for (int j = 0; j < kL1PD; ++j) {
+        const int i = i0 + j, s = sc + i;
+        bf16x8 fb[3];
+        split8(bq[j][0], bq[j][1], fb);
+        ldb1(min(s + kL1PD, steps1 - 1), bq[j][0], bq[j][1]);
+        if (s < steps1) {
+          bf16x8 fa[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            fa[p] = *reinterpret_cast<const bf16x8*>(sp + (p * kL1Rows + l32) * kL1SA + 16 * i + 8 * h);
+          pg_x3::mfma6(acc, fa, fb);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one step's fragments live at a time
+      }
+    }
+    __syncthreads();  // the pieces are restaged (next chunk) or reused (phase 2)
+  }
+  // epilogue: + b1, leaky (as x3_store: 1 * acc, + bias, act); A4 to LDS and out
+  {
+    const float bb = live1 ? b1[n1] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      float o = 1.f * acc[r];
+      o = o + bb;
+      o = o > 0.f ? o : o * slope;
+      if (n1 < K4) a[row * S + n1] = live1 ? o : 0.f;
+      if (live1 && row < nr) a4g[(int64_t)(r0 + row) * lda4 + n1] = o;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: the head (head_kernel's arithmetic, A4 from LDS) ----
+  {
+    const int c = tid % kMaxC, rg = tid / kMaxC;
+#pragma unroll
+    for (int hh = 0; hh < kRows / (kBlock / kMaxC); ++hh) {
+      const int ri = rg + hh * (kBlock / kMaxC);
+      if (c < C && ri < nr) {
+        const int64_t r = r0 + ri;
+        const int set = row_set[r];
+        const float t = labels[r * ldl + c];
+        const float4* ar = reinterpret_cast<const float4*>(a + ri * S);
+        const float4* wr = reinterpret_cast<const float4*>(w + c * S);
+        float zz = 0.f;
+        for (int k4 = 0; k4 < K4 / 4; ++k4) {
+          const float4 x = ar[k4], y = wr[k4];
+          zz = fmaf(x.x, y.x, zz);
+          zz = fmaf(x.y, y.y, zz);
+          zz = fmaf(x.z, y.z, zz);
+          zz = fmaf(x.w, y.w, zz);
+        }
+        zz = zz + b2[c];
+        const float pr = 1.f / (1.f + expf(-zz));
+        if (prob) prob[r * ldp + c] = pr;
+        float gz = 0.f;
+        if (set != 0) {
+          const float wc = cw[2 * c];
+          const float wp1 = cw[2 * c + 1];
+          const float cp = fminf(fmaxf(pr, 1e-9f), 10.f);
+          const float q = 1.f - pr;
+          const float cq = fminf(fmaxf(q, 1e-9f), 10.f);
+          const float la = logf(cp), lb = logf(cq);
+          terms[set - 1][ri][c] = ((t * la) * wc + (1.f - t) * lb) / wp1 * 2.f;
+          if (set == 1) {
+            float gg = -inv_n_train;
+            gg = gg * 2.f;
+            gg = gg / wp1;
+            float ga = (gg * wc) * t;
+            ga = ga / cp;
+            if (!(pr >= 1e-9f && pr <= 10.f)) ga = 0.f;
+            float gb = gg * (1.f - t);
+            gb = gb / cq;
+            if (!(q >= 1e-9f && q <= 10.f)) gb = 0.f;
+            const float dp = ga + (-gb);
+            gz = (dp * (1.f - pr)) * pr;
+          }
+        }
+        g[ri][c] = gz;
+        if (dz) dz[r * lddz + c] = gz;
+      } else {
+        g[ri][c] = 0.f;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * C) {
+    const int set = tid / C, c = tid % C;
+    float s = 0.f;
+    for (int ri = 0; ri < nr; ++ri) s += terms[set][ri][c];
+    part[((int64_t)set * C + c) * nb + blockIdx.x] = s;
+  }
+  // dA4 = (dz W2) * leaky'(A4), in place of A4 (each element read and written by one thread)
+  {
+    const int j = tid % kMaxK, r2 = tid / kMaxK;
+    if (j < K4) {
+      float wj[kMaxC];
+#pragma unroll
+      for (int c = 0; c < kMaxC; ++c) wj[c] = c < C && j < K1 ? w[c * S + j] : 0.f;
+      for (int ri = r2; ri < kL1Rows; ri += kBlock / kMaxK) {
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < kMaxC; ++c) s = fmaf(g[ri][c], wj[c], s);
+        const float y = a[ri * S + j];
+        const float d = y > 0.f ? s : s * slope;
+        a[ri * S + j] = j < K1 ? d : 0.f;
+        if (j < K1 && ri < nr) da4g[(int64_t)(r0 + ri) * ldg + j] = d;
+      }
+    }
+  }
+  __syncthreads();
+  // dA4's pieces (zero past K1, up to the 16-k steps' end)
+  for (int u = tid; u < kL1Rows * (K16 / 4); u += kBlock) {
+    const int row = u / (K16 / 4), k4 = (u % (K16 / 4)) * 4;
+    const float4 x = k4 < K4 ? *reinterpret_cast<const float4*>(a + row * S + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    uint2 pc[3];
+    pg_x3::split4(x, pc);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(sd + (p * kL1Rows + row) * SD + k4) = pc[p];
+  }
+  __syncthreads();
+
+  // ---- phase 3: dH3 = (dA4 W1) * leaky'(H3), one 32-column tile per wave and pass ----
+  const int steps3 = K16 / 16;
+  for (int c0 = 32 * wave; c0 < F3; c0 += 128) {
+    const int col = c0 + l32;
+    const int colc = min(col, F3 - 1);
+    // W1[k][col], k = 16 s + 8 h + i (i < 8): one strided column piece per fragment (each load
+    // instruction: 32 consecutive floats of one W1 row per lane half); rows past K1 read 0
+    // through the descriptor
+    const int vo3 = (8 * h * (int)ldw1 + colc) * 4;
+    auto ldb3 = [&](int s, float (&v)[8]) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw1, vo3 + (16 * s + i) * (int)ldw1 * 4, 0, 0));
+    };
+    // the activation operand of the epilogue, loaded first (used last); rows past n read 0
+    float y[16];
+    {
+      const __amdgpu_buffer_rsrc_t rh = pg_x3::rsrc(h3, (uint32_t)n * (uint32_t)ldh * 4u);
+      const int voy = (4 * h * (int)ldh + colc) * 4;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = r0 + (r & 3) + 8 * (r >> 2);
+        y[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, voy + rr * (int)ldh * 4, 0, 0));
+      }
+    }
+    f32x16 acc3;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc3[r] = 0.f;
+    // every K step's W1 fragment of this tile in flight at once (K1 <= 128: at most 8 steps;
+    // steps past K16 read zeros and are not multiplied)
+    float bv[kL1K1 / 16][8];
+#pragma unroll
+    for (int s = 0; s < kL1K1 / 16; ++s) ldb3(s, bv[s]);
+#pragma unroll
+    for (int s = 0; s < kL1K1 / 16; ++s) {
+      if (s < steps3) {
+        bf16x8 fb[3], fa[3];
+        split8(make_float4(bv[s][0], bv[s][1], bv[s][2], bv[s][3]), make_float4(bv[s][4], bv[s][5], bv[s][6], bv[s][7]),
+               fb);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          fa[p] = *reinterpret_cast<const bf16x8*>(sd + (p * kL1Rows + l32) * SD + 16 * s + 8 * h);
+        pg_x3::mfma6(acc3, fa, fb);
+      }
+    }
+    // epilogue: act'(H3) (as x3_store's EPI_DLEAKY: 1 * acc, then y > 0 ? x : x slope)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float o = 1.f * acc3[r];
+      if (row < nr && col < F3) dh3[(int64_t)(r0 + row) * lddh + col] = y[r] > 0.f ? o : o * slope;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -263,6 +574,47 @@ int pg_mlp_head(const void* a4, int64_t lda, int64_t n, int32_t K, int a_dtype, 
                      n_train, n_val, loss2);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pg::set_error((int)e, "pg_mlp_head: launch failed: %s", hipGetErrorString(e));
+  return pg::ok();
+}
+
+size_t pg_mlp_l1_head_workspace(int64_t n, int32_t C, int32_t F3, int32_t K1) {
+  (void)F3;
+  (void)K1;
+  return pg_mlp_head_workspace(n, C);
+}
+
+int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const float* w1, int64_t ldw1,
+                   const float* b1, int32_t K1, float* a4, int64_t lda4, const float* w2, int64_t ldw,
+                   const float* b2, int32_t C, const float* labels, int64_t ldl, const float* class_w,
+                   const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob, int64_t ldp,
+                   float* dz, int64_t lddz, float* da4, int64_t ldg, float* dh3, int64_t lddh, float slope,
+                   float* loss2, void* ws, size_t ws_bytes, pg_stream_t stream) {
+  if (n < 0 || n > INT32_MAX || F3 <= 0 || F3 % 4 != 0 || F3 > 4096 || K1 <= 0 || K1 > kL1K1 || K1 > kMaxK ||
+      C <= 0 || C > kMaxC || ldh < F3 || ldw1 < F3 || lda4 < K1 || ldw < K1 || ldl < C || (prob && ldp < C) ||
+      (dz && lddz < C) || ldg < K1 || lddh < F3)
+    return pg::set_error(PG_ERR_INVALID, "pg_mlp_l1_head: bad shape (F3 %% 4 == 0, F3 <= 4096, K1 <= %d, C <= %d)",
+                         kL1K1, kMaxC);
+  if (n == 0) return pg::ok();
+  if (!h3 || !w1 || !b1 || !a4 || !w2 || !b2 || !labels || !class_w || !row_set || !da4 || !dh3 || !loss2 || !ws)
+    return pg::set_error(PG_ERR_INVALID, "pg_mlp_l1_head: NULL buffer");
+  if (((uintptr_t)h3 & 15) || (ldh & 3) || ((uintptr_t)w1 & 15) || (ldw1 & 3) || ((uintptr_t)w2 & 15) || (ldw & 3) ||
+      ((uintptr_t)ws & 255))
+    return pg::set_error(PG_ERR_INVALID, "pg_mlp_l1_head: H3, W1, W2 need 16-B aligned rows, ws 256-B alignment");
+  if ((double)n * (double)ldh * 4.0 >= 2147483648.0 || (double)K1 * (double)ldw1 * 4.0 >= 2147483648.0)
+    return pg::set_error(PG_ERR_UNSUPPORTED, "pg_mlp_l1_head: H3 / W1 of 2 GiB or more");
+  if (ws_bytes < pg_mlp_l1_head_workspace(n, C, F3, K1))
+    return pg::set_error(PG_ERR_WORKSPACE, "pg_mlp_l1_head: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (int)((n + kL1Rows - 1) / kL1Rows);
+  float* part = (float*)ws;
+  const float inv_n = n_train > 0 ? 1.0f / (float)n_train : 0.f;
+  hipLaunchKernelGGL(mlp_l1_head_kernel, dim3(nb), dim3(kBlock), (unsigned)l1_region_bytes(K1), st, h3, ldh, (int)n,
+                     (int)F3, w1, ldw1, b1, (int)K1, a4, lda4, w2, ldw, b2, (int)C, labels, ldl, class_w, row_set, inv_n,
+                     prob, ldp, dz, lddz, da4, ldg, dh3, lddh, slope, part, nb);
+  hipLaunchKernelGGL(head_final_kernel, dim3(2), dim3(64 * kMaxC), 0, st, (const float*)part, nb, (int)C, n_train,
+                     n_val, loss2);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pg::set_error((int)e, "pg_mlp_l1_head: launch failed: %s", hipGetErrorString(e));
   return pg::ok();
 }
 

@@ -80,6 +80,9 @@ class TrainEngine:
     # True: every weight gradient of the step in one grouped split-K launch at the end of the
     # backward (pg_gemm_f32_group); False: one split-K launch per product (A/B knob)
     GROUP_WGRAD = True
+    # liner1's forward, the head and liner1's input gradient as one launch (pg_mlp_l1_head:
+    # bitwise the separate x3 GEMMs + pg_mlp_head); False: three launches (A/B knob)
+    FUSED_L1_HEAD = True
     WIDTH_ALIGN = 4  # every padded width is a multiple of this
     _cur = ""                      # launch site being issued (_t)
     _filter: Optional[str] = None  # group_times: issue only this launch group
@@ -234,7 +237,8 @@ class TrainEngine:
             # the grouped launches' slabs, sized from the shapes alone (transposed A, plain B)
             self.gws = torch.empty(self._group_ws_bytes(L.pg_gemm_f32_group_workspace), dtype=torch.uint8,
                                    device=dev)
-        need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C))
+        need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C),
+                   L.pg_mlp_l1_head_workspace(N, C, pd[-3], pd[-2]))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
         self.ws_bytes = self.ws.numel()
 
@@ -554,9 +558,30 @@ class TrainEngine:
             out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
             self._gemm(HM, P[p + "Wcat"], out, transb=True, bias=P[p + "b"], act=LEAKY,
                        tag=f"gemm.fwd.cat.l{l + 1}")
+        if self._l1_fused():
+            self._mlp_l1_head()
+            return
         self._gemm(self.A3, P["liner1.W"], self.A4, transb=True, bias=P["liner1.b"], act=LEAKY,
                    tag="gemm.fwd.liner1")
         self._head(_lib.PG_DTYPE_F32, self.A4, self.dZ, None, self.dA4)
+
+    def _l1_fused(self) -> bool:
+        return self.FUSED_L1_HEAD and self.pd[-2] <= 128
+
+    def _mlp_l1_head(self) -> None:
+        """liner1 + liner2 + sigmoid + train/val loss + dZ + dA4 + liner1's input gradient
+        through the top SAGE layer's leaky_relu (that layer's dY) in one launch
+        (pg_mlp_l1_head; code/model.py:26-29, code/train.py:89-108, 199-207)."""
+        P, pd, C = self.P, self.pd, self.C
+        top = self.L - 1
+        dH3 = self.DYP[top][:, :pd[top + 1]]
+        with self._t("head.l1", 2.0 * 2 * self.N * pd[-3] * pd[-2]):
+            self._call("pg_mlp_l1_head", ptr(self.A3), self.A3.stride(0), self.N, pd[-3], ptr(P["liner1.W"]),
+                       P["liner1.W"].stride(0), ptr(P["liner1.b"]), pd[-2], ptr(self.A4), self.A4.stride(0),
+                       ptr(P["liner2.W"]), pd[-2], ptr(P["liner2.b"]), C, ptr(self.labels), pd[-1], ptr(self.cw),
+                       ptr(self.row_set), self.n_train, self.n_val, ptr(self.prob), pd[-1], ptr(self.dZ), pd[-1],
+                       ptr(self.dA4), self.dA4.stride(0), ptr(dH3), dH3.stride(0), LEAKY_SLOPE, ptr(self.loss),
+                       ptr(self.ws), self.ws_bytes, self._s())
 
     def _head(self, a_dtype, A4, dZ, dZb, dA4) -> None:
         """liner2 + sigmoid + train/val multi_loss + dZ + dA4 = (dZ W2) * leaky'(A4): one
@@ -579,8 +604,9 @@ class TrainEngine:
         # liner1
         self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
         top = self.L - 1
-        self._gemm(self.dA4, P["liner1.W"], self.DYP[top][:, :pd[top + 1]], act=LEAKY, dact=self.A3,
-                   tag="gemm.dgrad.liner1")
+        if not self._l1_fused():  # (fused: the head wrote the top layer's dY already)
+            self._gemm(self.dA4, P["liner1.W"], self.DYP[top][:, :pd[top + 1]], act=LEAKY, dact=self.A3,
+                       tag="gemm.dgrad.liner1")
         for l in reversed(range(self.L)):
             p = f"conv{l + 1}."
             Fi, Fo = pd[l], pd[l + 1]
@@ -779,6 +805,14 @@ class TrainEngine:
             wgrad = fwd
             igrad = 2 * N * fo * fi + (2 * N * fo * fi + 2 * N * fi * fi if l > 0 else 0)
             f += fwd + wgrad + igrad
-        f += 3 * 2 * N * d[-3] * d[-2]   # liner1: forward, weight and input gradients
+        # liner1: forward, weight and input gradients (the forward and the input gradient run
+        # inside the fused head when FUSED_L1_HEAD: head_flops_per_step)
+        f += (1 if self._l1_fused() else 3) * 2 * N * d[-3] * d[-2]
         f += 2 * N * d[-2] * d[-1]       # liner2: weight gradient
         return f
+
+    def head_flops_per_step(self) -> int:
+        """Flops of the liner1 products inside the fused head (forward + input gradient, true
+        dims), 0 when they run as GEMMs."""
+        d = self.dims
+        return 2 * 2 * self.N * d[-3] * d[-2] if self._l1_fused() else 0

@@ -35,6 +35,8 @@ class TrainEngineBF16(TrainEngine):
     # the stacked input-gradient weights as [Fi][Fo + Fi] (B^T, a row image: the A B^T
     # ping-pong kernel of pg_gemm_bf16 takes the product) instead of [Fo + Fi][Fi] (a k image)
     STACK_T = True
+    # the fused liner1 + head kernel is f32 only: bf16 storage keeps liner1 as bf16 GEMMs
+    FUSED_L1_HEAD = False
 
     # ------------------------------------------------------------------ buffers
     def _alloc_buffers(self, features: torch.Tensor) -> None:
