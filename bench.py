@@ -315,7 +315,8 @@ def _roofline(engine, gt, bf16):
     work = {"gemm": float(engine.flops_per_step()),
             "spmm_max_fwd": float(sum(engine.spmm_bytes(l) for l in range(L))),
             "spmm_max_bwd": float(sum(engine.spmm_bwd_bytes(l) for l in range(L))),
-            "adam": 16.0 * engine.flat.numel()}
+            "adam": 16.0 * engine.flat.numel(),
+            "head": float(engine.head_flops_per_step())}
     gemm_group = "gemm_bf16" if bf16 else "gemm_f32"
     groups = {}
     for gname, r in gt.items():
@@ -341,6 +342,15 @@ def _roofline(engine, gt, bf16):
                          peak_is="bf16 MFMA peak / 6 (three-piece f32 split, gemm_x3.hip)",
                          peak_f32_mfma=PEAK_F32_TFLOPS, frac_vs_f32_mfma=round(ach / PEAK_F32_TFLOPS, 4))
             return r
+        if gname == "head":
+            # the fused MLP head (pg_mlp_l1_head): liner1's forward and input-gradient products
+            # (three-piece MFMA) with the loss in between; its flops against the same ceiling
+            ach = g["work"] / sec / 1e12
+            return {"bound": "mfma", "achieved": round(ach, 2), "unit": "TFLOP/s", **base,
+                    "flops_per_step": int(g["work"]), "peak": round(X3_CEILING_TFLOPS, 1),
+                    "frac": round(ach / X3_CEILING_TFLOPS, 4),
+                    "what": "liner1 forward + liner2/sigmoid/multi_loss/dZ/dA4 + liner1 input gradient, one launch "
+                            "(+ the loss reduction); flops of the two liner1 products"}
         ach = g["work"] / sec / 1e9
         if gname == "spmm_max_fwd":
             # per-edge row gathers (SURVEY.md §8d bytes) are served mostly by the L2s and the
@@ -562,6 +572,7 @@ def run(args, rank, world, dev, dist, mode, breakdown=True):
         "spmm_roofline": {k: roof(k) for k in ("spmm_max_fwd", "spmm_max_bwd") if k in groups},
         # the GEMM group's own roofline when another group dominates (cfg5)
         "gemm_roofline": roof(gemm_name) if gemm_name in groups and gemm_name != dom else None,
+        "head_roofline": roof("head") if groups.get("head", {}).get("work") else None,
         "kernels_ms_per_step": {k: round(v["ms"], 4) for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])},
         "allreduce": ar_info,
         "loss": {"train": loss_tr, "val": loss_va},
@@ -591,7 +602,7 @@ def sub_configs(args):
         t0 = time.perf_counter()
         res = _child(args, ["--config", name])
         keep = ("value", "unit", "ms_per_step", "step_distribution", "dtype", "config", "roofline", "spmm_roofline",
-                "gemm_roofline", "kernels_ms_per_step", "loss")
+                "gemm_roofline", "head_roofline", "kernels_ms_per_step", "loss")
         out[name] = {k: res[k] for k in keep}
         out[name]["child_wall_s"] = round(time.perf_counter() - t0, 1)
         print(f"sub-config {name}: {res['ms_per_step']} ms/step", file=sys.stderr, flush=True)
