@@ -635,7 +635,9 @@ def guarded_dp_leg(args, rank, world, dev, dist, ctrl):
     except (Exception, SystemExit) as e:  # run() raises SystemExit on diverged replicas
         err = f"rank {rank}: {type(e).__name__}: {e}"[-500:]
         print(f"dp leg failed on {err}", file=sys.stderr, flush=True)
-    flag = torch.tensor([1 if err else 0], dtype=torch.int32)
+    # (without a gloo group the default one carries it: a device tensor for RCCL)
+    on_dev = ctrl is None and dist.get_backend() == "nccl"
+    flag = torch.tensor([1 if err else 0], dtype=torch.int32, device=dev if on_dev else "cpu")
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=ctrl)
     if flag.item():
         return {"error": err or "failed on another rank (see its stderr)"} if rank == 0 else None
@@ -703,7 +705,10 @@ def main(argv=None):
         backend = os.environ.get("PLAGNN_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
-            ctrl = dist.new_group(backend="gloo")
+            try:
+                ctrl = dist.new_group(backend="gloo")
+            except Exception as e:  # noqa: BLE001 — the dp leg's flag then goes over RCCL itself
+                print(f"gloo control group unavailable ({e}); dp-leg status over {backend}", file=sys.stderr)
         else:
             dist.init_process_group(backend)
 

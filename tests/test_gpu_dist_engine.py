@@ -283,3 +283,45 @@ def test_engine_rejects_buckets_it_does_not_launch():
     with pytest.raises(RuntimeError, match="liner1.W"):
         eng._check_bucket_pending(0)
     eng._parts = []
+
+
+def _worker_guard_nccl(rank, world, port, outdir):
+    """bench.py's N > 1 dp-leg guard over a real RCCL default group (one rank: a one-GPU box
+    holds one RCCL rank) with its gloo control group, as the driver's 8-GPU runs set it up."""
+    import json
+    import sys
+
+    sys.path[:0] = [PKG, ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import torch.distributed as dist
+
+    import bench
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    ctrl = dist.new_group(backend="gloo")
+
+    def boom(*a, **k):
+        raise RuntimeError("injected dp-leg failure")
+
+    bench.run = boom
+    out = {"with_gloo": bench.guarded_dp_leg(None, 0, 1, dev, dist, ctrl),
+           "rccl_only": bench.guarded_dp_leg(None, 0, 1, dev, dist, None)}
+    bench.run = lambda *a, **k: {"value": 1.0}
+    out["ok"] = bench.guarded_dp_leg(None, 0, 1, dev, dist, ctrl)
+    with open(os.path.join(outdir, "guard.json"), "w") as f:
+        json.dump(out, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_bench_dp_guard_over_rccl_one_rank(tmp_path):
+    import json
+
+    mp.start_processes(_worker_guard_nccl, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+                       start_method="spawn")
+    got = json.load(open(tmp_path / "guard.json"))
+    assert "injected dp-leg failure" in got["with_gloo"]["error"]
+    assert "injected dp-leg failure" in got["rccl_only"]["error"]
+    assert got["ok"] == {"value": 1.0}
