@@ -665,11 +665,16 @@ def main(argv=None):
     ap.add_argument("--dropin-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--chunk-bwd", type=int, default=0, help=argparse.SUPPRESS)  # tuning experiments
     ap.add_argument("--separate-l1-head", action="store_true", help=argparse.SUPPRESS)  # A/B: unfused MLP head
+    ap.add_argument("--separate-adam-prep", action="store_true", help=argparse.SUPPRESS)  # A/B: own prepare launch
     args = ap.parse_args(argv)
     if args.separate_l1_head:
         import plagnn.engine
 
         plagnn.engine.TrainEngine.FUSED_L1_HEAD = False
+    if args.separate_adam_prep:
+        import plagnn.engine
+
+        plagnn.engine.TrainEngine.FOLD_ADAM_PREP = False
     if args.chunk_bwd:
         import plagnn.graph
 

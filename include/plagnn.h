@@ -251,14 +251,17 @@ int pg_mlp_head(const void* A4, int64_t lda, int64_t n, int32_t K, int a_dtype, 
  * products are computed exactly as pg_gemm_f32's three-piece kernel computes them (same
  * split, same k order and MFMA sequence), so A4 and dH3 equal its results bitwise. prob and
  * dz are optional (NULL). Scratch (256-B aligned): pg_mlp_l1_head_workspace(n, C, F3, K1)
- * bytes (the head's partial sums and W1's bf16 pieces, split once per call); F3 <= 4096. */
+ * bytes; F3 <= 4096. adam_state (optional, NULL = none): the launch also does
+ * pg_adam_prepare(adam_state, lr, beta1, beta2)'s work (one per step, before pg_adam_apply),
+ * so a training step needs one launch fewer. */
 size_t pg_mlp_l1_head_workspace(int64_t n, int32_t C, int32_t F3, int32_t K1);
 int pg_mlp_l1_head(const float* H3, int64_t ldh, int64_t n, int32_t F3, const float* W1, int64_t ldw1,
                    const float* b1, int32_t K1, float* A4, int64_t lda4, const float* W2, int64_t ldw,
                    const float* b2, int32_t C, const float* labels, int64_t ldl, const float* class_w,
                    const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob, int64_t ldp,
                    float* dz, int64_t lddz, float* dA4, int64_t ldg, float* dH3, int64_t lddh, float slope,
-                   float* loss2, void* ws, size_t ws_bytes, pg_stream_t stream);
+                   float* loss2, void* ws, size_t ws_bytes, float* adam_state, double lr, double beta1,
+                   double beta2, pg_stream_t stream);
 size_t pg_sigmoid_multi_loss_workspace(int64_t n_index, int32_t C);
 int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C,
                           const float* labels, int64_t ldl, const float* class_w,

@@ -9,6 +9,7 @@
 
 #include <cmath>
 
+#include "adam_step.hpp"
 #include "common.hpp"
 
 namespace {
@@ -218,12 +219,7 @@ __global__ __launch_bounds__(kBlock) void multi_loss_final_kernel(const float* _
 // ---- Adam ---------------------------------------------------------------------------
 __global__ void adam_prepare_kernel(float* state, double lr, double beta1, double beta2) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const float step = state[0] + 1.f;
-  state[0] = step;
-  const double bc1 = 1.0 - pow(beta1, (double)step);
-  const double bc2 = 1.0 - pow(beta2, (double)step);
-  state[1] = (float)(lr / bc1);  // step_size
-  state[2] = (float)sqrt(bc2);   // sqrt(bias_correction2)
+  pg_adam::step_scalars(state, lr, beta1, beta2);
 }
 
 __global__ __launch_bounds__(kBlock) void adam_apply_kernel(

@@ -16,6 +16,7 @@
 
 #include <cmath>
 
+#include "adam_step.hpp"
 #include "common.hpp"
 #include "x3_split.hpp"
 
@@ -196,7 +197,12 @@ __global__ __launch_bounds__(kBlock) void head_kernel(
 // lanes in a fixed butterfly, and thread 0 adds the classes in order: deterministic.
 __global__ __launch_bounds__(64 * kMaxC) void head_final_kernel(const float* __restrict__ part, int nb,
                                                                 int C, int64_t n_train, int64_t n_val,
-                                                                float* __restrict__ loss) {
+                                                                float* __restrict__ loss, float* adam_state = nullptr,
+                                                                double lr = 0.0, double beta1 = 0.0,
+                                                                double beta2 = 0.0) {
+  // (optional) the step's Adam scalars, pg_adam_prepare's work, so the step has one tiny
+  // launch fewer: it runs once per step here as there, before pg_adam_apply
+  if (adam_state && blockIdx.x == 1 && threadIdx.x == 0) pg_adam::step_scalars(adam_state, lr, beta1, beta2);
   __shared__ float cls[kMaxC];
   const int set = blockIdx.x, c = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t ns = set == 0 ? n_train : n_val;
@@ -588,7 +594,8 @@ int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const fl
                    const float* b2, int32_t C, const float* labels, int64_t ldl, const float* class_w,
                    const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob, int64_t ldp,
                    float* dz, int64_t lddz, float* da4, int64_t ldg, float* dh3, int64_t lddh, float slope,
-                   float* loss2, void* ws, size_t ws_bytes, pg_stream_t stream) {
+                   float* loss2, void* ws, size_t ws_bytes, float* adam_state, double lr, double beta1,
+                   double beta2, pg_stream_t stream) {
   if (n < 0 || n > INT32_MAX || F3 <= 0 || F3 % 4 != 0 || F3 > 4096 || K1 <= 0 || K1 > kL1K1 || K1 > kMaxK ||
       C <= 0 || C > kMaxC || ldh < F3 || ldw1 < F3 || lda4 < K1 || ldw < K1 || ldl < C || (prob && ldp < C) ||
       (dz && lddz < C) || ldg < K1 || lddh < F3)
@@ -612,7 +619,7 @@ int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const fl
                      (int)F3, w1, ldw1, b1, (int)K1, a4, lda4, w2, ldw, b2, (int)C, labels, ldl, class_w, row_set, inv_n,
                      prob, ldp, dz, lddz, da4, ldg, dh3, lddh, slope, part, nb);
   hipLaunchKernelGGL(head_final_kernel, dim3(2), dim3(64 * kMaxC), 0, st, (const float*)part, nb, (int)C, n_train,
-                     n_val, loss2);
+                     n_val, loss2, adam_state, lr, beta1, beta2);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pg::set_error((int)e, "pg_mlp_l1_head: launch failed: %s", hipGetErrorString(e));
   return pg::ok();

@@ -161,7 +161,7 @@ SIGNATURES = {
     "pg_mlp_l1_head_workspace": (_sz, [_i64, _i32, _i32, _i32]),
     "pg_mlp_l1_head": (_i, [_vp, _i64, _i64, _i32, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _i64, _vp, _i32, _vp,
                             _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _f, _vp,
-                            _vp, _sz, _vp]),
+                            _vp, _sz, _vp, _d, _d, _d, _vp]),
     "pg_adam_prepare": (_i, [_vp, _d, _d, _d, _vp]),
     "pg_adam_apply": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _d, _d, _d, _d, _vp]),
     "pg_gemm_f32_split_k": (_i, [_i64, _i64, _i64]),

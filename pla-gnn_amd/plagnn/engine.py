@@ -83,6 +83,11 @@ class TrainEngine:
     # liner1's forward, the head and liner1's input gradient as one launch (pg_mlp_l1_head:
     # bitwise the separate x3 GEMMs + pg_mlp_head); False: three launches (A/B knob)
     FUSED_L1_HEAD = True
+    # with it, the fused head's final kernel also forms the step's Adam scalars (pg_adam_prepare's
+    # work): one launch fewer per step (A/B knob)
+    FOLD_ADAM_PREP = True
+    _fold_prep = False             # set by the step paths (step_eager, capture, group_times)
+    _prepped = False               # the head of this step formed the Adam scalars
     WIDTH_ALIGN = 4  # every padded width is a multiple of this
     _cur = ""                      # launch site being issued (_t)
     _filter: Optional[str] = None  # group_times: issue only this launch group
@@ -408,11 +413,16 @@ class TrainEngine:
             try:
                 with torch.cuda.graph(g, stream=s):
                     for _ in range(copies):
-                        self.forward()
-                        self.backward()
+                        self._fold_prep = True  # as the step runs it
+                        try:
+                            self.forward()
+                            self.backward()
+                        finally:
+                            self._fold_prep = False
                         self.adam()
             finally:
                 self._filter = None
+                self._prepped = False
             launches = self._issued // copies
             if launches == 0:
                 continue
@@ -575,13 +585,17 @@ class TrainEngine:
         P, pd, C = self.P, self.pd, self.C
         top = self.L - 1
         dH3 = self.DYP[top][:, :pd[top + 1]]
+        # inside a training step (not a bare forward()): the Adam scalars too
+        fold = self._fold_prep and self.FOLD_ADAM_PREP
+        self._prepped = fold
         with self._t("head.l1", 2.0 * 2 * self.N * pd[-3] * pd[-2]):
             self._call("pg_mlp_l1_head", ptr(self.A3), self.A3.stride(0), self.N, pd[-3], ptr(P["liner1.W"]),
                        P["liner1.W"].stride(0), ptr(P["liner1.b"]), pd[-2], ptr(self.A4), self.A4.stride(0),
                        ptr(P["liner2.W"]), pd[-2], ptr(P["liner2.b"]), C, ptr(self.labels), pd[-1], ptr(self.cw),
                        ptr(self.row_set), self.n_train, self.n_val, ptr(self.prob), pd[-1], ptr(self.dZ), pd[-1],
                        ptr(self.dA4), self.dA4.stride(0), ptr(dH3), dH3.stride(0), LEAKY_SLOPE, ptr(self.loss),
-                       ptr(self.ws), self.ws_bytes, self._s())
+                       ptr(self.ws), self.ws_bytes, ptr(self.adam_state) if fold else None, self.lr, self.betas[0],
+                       self.betas[1], self._s())
 
     def _head(self, a_dtype, A4, dZ, dZb, dA4) -> None:
         """liner2 + sigmoid + train/val multi_loss + dZ + dA4 = (dZ W2) * leaky'(A4): one
@@ -671,8 +685,10 @@ class TrainEngine:
 
     def adam(self) -> None:
         st = self._s()
+        prepped, self._prepped = self._prepped, False
         with self._t("adam", 16.0 * self.flat.numel()):
-            self._call("pg_adam_prepare", ptr(self.adam_state), self.lr, self.betas[0], self.betas[1], st)
+            if not prepped:  # (else this step's head formed the scalars)
+                self._call("pg_adam_prepare", ptr(self.adam_state), self.lr, self.betas[0], self.betas[1], st)
             self._call("pg_adam_apply", ptr(self.flat), ptr(self.gflat), ptr(self.m), ptr(self.v),
                  self.flat.numel(), ptr(self.adam_state), self.betas[0], self.betas[1], self.eps, 0.0, st)
 
@@ -692,11 +708,13 @@ class TrainEngine:
         self._uses_buckets(allreduce)
         inline = allreduce is not None and getattr(allreduce, "capturable", False)
         self._ar_inline = allreduce if inline else None
+        self._fold_prep = True
         try:
             self.forward()
             self.backward()
         finally:
             self._ar_inline = None
+            self._fold_prep = False
         if inline:
             allreduce.join()
         elif allreduce is not None:
@@ -726,18 +744,24 @@ class TrainEngine:
         if allreduce is None or inline:
             with torch.cuda.graph(self.graph):
                 self._ar_inline = allreduce if inline else None
+                self._fold_prep = True
                 try:
                     self.forward()
                     self.backward()
                 finally:
                     self._ar_inline = None
+                    self._fold_prep = False
                 if inline:
                     allreduce.join()
                 self.adam()
         else:
             with torch.cuda.graph(self.graph):
-                self.forward()
-                self.backward()
+                self._fold_prep = True
+                try:
+                    self.forward()
+                    self.backward()
+                finally:
+                    self._fold_prep = False
             self.graph_adam = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_adam):
                 self.adam()

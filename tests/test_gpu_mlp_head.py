@@ -116,7 +116,7 @@ def test_mlp_l1_head_rejects_bad_shapes():
     def args(F3, K1, C):
         return (p, 256, 64, F3, p, 256, p, K1, outs[0].data_ptr(), 256, p, 256, p, C, p, 256, p, rs.data_ptr(), 0, 0,
                 None, 0, None, 0, outs[1].data_ptr(), 256, outs[2].data_ptr(), 256, 0.01, loss.data_ptr(),
-                ws.data_ptr(), ws.numel(), None)
+                ws.data_ptr(), ws.numel(), None, 0.0, 0.0, 0.0, None)
 
     assert L.pg_mlp_l1_head(*args(256, 104, 12)) == 0
     torch.cuda.synchronize()
@@ -124,5 +124,35 @@ def test_mlp_l1_head_rejects_bad_shapes():
     for bad in ((254, 104, 12), (256, 129, 12), (256, 104, 17)):
         assert L.pg_mlp_l1_head(*args(*bad)) != 0
     short = list(args(256, 104, 12))
-    short[-2] = ws.numel() - 1  # workspace one byte short
+    short[-6] = ws.numel() - 1  # workspace one byte short
     assert L.pg_mlp_l1_head(*short) != 0
+
+
+def test_adam_scalars_folded_into_head_equal_separate_prepare():
+    """FOLD_ADAM_PREP: inside a training step the fused head's final kernel forms the Adam
+    scalars (pg_adam_prepare's work). Three steps (eager, then captured replays) must leave
+    the parameters, moments and step count bitwise where the separate prepare launch leaves
+    them; a bare forward() must not advance the step count."""
+    import plagnn
+
+    dims = (31, 24, 20, 16, 10, 12)
+    engs = []
+    for fold in (True, False):
+        e, _ = _engine_pair(dims, 600, 6000, seed=5)
+        e.FOLD_ADAM_PREP = fold
+        engs.append(e)
+    for e in engs:
+        e.step_eager()
+        e.capture(warmup=1)
+        e.step()
+        e.step()
+    torch.cuda.synchronize()
+    a, b = engs
+    for name in ("flat", "m", "v", "adam_state"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert a.adam_state[0].item() == 4.0  # 1 eager + 1 capture warm-up + 2 replays
+    before = a.adam_state.clone()
+    a.forward()
+    torch.cuda.synchronize()
+    assert torch.equal(a.adam_state, before)
+    assert isinstance(a, plagnn.TrainEngine)
