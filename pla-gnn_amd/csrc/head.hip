@@ -277,6 +277,55 @@ __device__ __forceinline__ void split8(const float4 lo, const float4 hi, bf16x8 
   for (int p = 0; p < 3; ++p) f[p] = __builtin_bit_cast(bf16x8, make_uint4(a[p].x, a[p].y, b[p].x, b[p].y));
 }
 
+#ifndef PG_L1_SKIP
+#define PG_L1_SKIP 0  // probe builds only (timing, wrong results): 1 / 2 / 3 skip that phase's products
+#endif
+#ifndef PG_L1_PRESPLIT
+#define PG_L1_PRESPLIT 1  // W1's pieces split once per call in the fragments' own layout
+#endif
+// W1 [K1][F3] split once per call into its three bf16 pieces, stored fragment-native: for
+// each piece, blocks of 32 rows x 8 k of 512 B, lane l of a fragment read owning the 16 B
+// of row l (so a fragment read is one 512-B run per lane half):
+//   p1: rows n < 128 (W1 rows, zero past K1), k < F16 (W1 columns, zero past F3): phase 1
+//   p3: rows c < F32 (W1 columns, F3 rounded up to 32), k < K16 (W1 rows, zero past K1):
+//       W1^T for phase 3
+// (the same split4 as every other split: bitwise the pieces each block formed itself)
+__host__ __device__ inline int64_t l1_p1_plane(int F3) { return (int64_t)kL1K1 * ((F3 + 15) / 16 * 16); }
+__host__ __device__ inline int64_t l1_p3_plane(int F3, int K1) {
+  return (int64_t)((F3 + 31) / 32 * 32) * ((K1 + 15) / 16 * 16);
+}
+__global__ __launch_bounds__(kBlock) void l1_split_kernel(const float* __restrict__ w1, int64_t ldw1, int K1, int F3,
+                                                          uint16_t* __restrict__ p1, uint16_t* __restrict__ p3) {
+  const int F16 = (F3 + 15) / 16 * 16, K16 = (K1 + 15) / 16 * 16, F32 = (F3 + 31) / 32 * 32;
+  const int n1u = kL1K1 * (F16 / 8), n3u = F32 * (K16 / 8);
+  const int u = blockIdx.x * kBlock + threadIdx.x;
+  if (u >= n1u + n3u) return;
+  float v[8];
+  uint16_t* dst;
+  int64_t plane;
+  if (u < n1u) {  // unit (row block, k block, lane) -> W1[n][k0 .. k0 + 7]
+    const int l = u & 31, kb = (u >> 5) % (F16 / 8), nb = (u >> 5) / (F16 / 8);
+    const int n = 32 * nb + l, k0 = 8 * kb;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = n < K1 && k0 + i < F3 ? w1[(int64_t)n * ldw1 + k0 + i] : 0.f;
+    dst = p1 + (int64_t)u * 8;
+    plane = l1_p1_plane(F3);
+  } else {        // -> W1[j0 .. j0 + 7][c]
+    const int w = u - n1u;
+    const int l = w & 31, kb = (w >> 5) % (K16 / 8), cb = (w >> 5) / (K16 / 8);
+    const int c = 32 * cb + l, j0 = 8 * kb;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = c < F3 && j0 + i < K1 ? w1[(int64_t)(j0 + i) * ldw1 + c] : 0.f;
+    dst = p3 + (int64_t)w * 8;
+    plane = l1_p3_plane(F3, K1);
+  }
+  uint2 a[3], b[3];
+  pg_x3::split4(make_float4(v[0], v[1], v[2], v[3]), a);
+  pg_x3::split4(make_float4(v[4], v[5], v[6], v[7]), b);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) *reinterpret_cast<uint4*>(dst + p * plane) = make_uint4(a[p].x, a[p].y, b[p].x, b[p].y);
+}
+
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WAVES))) void mlp_l1_head_kernel(
     const float* __restrict__ h3, int64_t ldh, int n, int F3, const float* __restrict__ w1, int64_t ldw1,
     const float* __restrict__ b1, int K1, float* __restrict__ a4g, int64_t lda4,
@@ -284,7 +333,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
     const float* __restrict__ labels, int64_t ldl, const float* __restrict__ cw,
     const int8_t* __restrict__ row_set, float inv_n_train, float* __restrict__ prob, int64_t ldp,
     float* __restrict__ dz, int64_t lddz, float* __restrict__ da4g, int64_t ldg,
-    float* __restrict__ dh3, int64_t lddh, float slope, float* __restrict__ part, int nb) {
+    float* __restrict__ dh3, int64_t lddh, float slope, float* __restrict__ part, int nb,
+    const uint16_t* __restrict__ p1, const uint16_t* __restrict__ p3) {
   extern __shared__ __attribute__((aligned(16))) unsigned char region[];
   __shared__ __attribute__((aligned(16))) float w[kMaxC * (kMaxK + 4)];
   __shared__ float g[kRows][kMaxC];
@@ -307,6 +357,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
     }
   }
   for (int i = tid; i < 2 * kRows * kMaxC; i += kBlock) (&terms[0][0][0])[i] = 0.f;
+  // the head's per-thread inputs (class c = tid % 16 of rows tid / 16 and tid / 16 + 16),
+  // loaded now so that phase 2 does not wait on them
+  constexpr int kHH = kRows / (kBlock / kMaxC);
+  int hset[kHH];
+  float hlab[kHH];
+  const int hc = min(tid % kMaxC, C - 1);
+  const float hwc = cw[2 * hc], hwp1 = cw[2 * hc + 1], hb2 = b2[hc];
+#pragma unroll
+  for (int hh = 0; hh < kHH; ++hh) {
+    const int64_t r = min(r0 + tid / kMaxC + hh * (kBlock / kMaxC), n - 1);
+    hset[hh] = row_set[r];
+    hlab[hh] = labels[r * ldl + hc];
+  }
 
   // ---- phase 1: A4 = leaky(H3 W1^T + b1) ----
   f32x16 acc;
@@ -314,6 +377,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const int n1 = 32 * wave + l32;                       // this lane's A4 column (W1 row)
   const bool live1 = n1 < K1;
+#if !PG_L1_PRESPLIT
   // W1 through a buffer descriptor over its K1 rows: rows past K1 read 0 (the range check
   // covers the VGPR offset, which therefore carries the whole offset); every offset fits 32
   // bits (the host checks the extents). Each block splits the W1 fragments it reads (a
@@ -329,23 +393,44 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
     lo = k < F3 ? x : make_float4(0.f, 0.f, 0.f, 0.f);
     hi = k + 4 < F3 ? y : make_float4(0.f, 0.f, 0.f, 0.f);
   };
+#endif
   const int steps1 = (F3 + 15) / 16;
+#if PG_L1_PRESPLIT
+  // p1's fragment of step s: block (wave, 2 s + h), this lane's 16 B, per piece
+  const __amdgpu_buffer_rsrc_t rp1 = pg_x3::rsrc(p1, (uint32_t)(3 * l1_p1_plane(F3) * 2));
+  const int pl1 = (int)(l1_p1_plane(F3) * 2), kb1 = (F3 + 15) / 16 * 2;
+  auto ldf1 = [&](int s, bf16x8 (&f)[3]) {
+    const int off = ((wave * kb1 + 2 * s + h) * 32 + l32) * 16;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      f[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rp1, off + p * pl1, 0, 0));
+  };
+  bf16x8 bq[kL1PD][3];
+#pragma unroll
+  for (int i = 0; i < kL1PD; ++i) ldf1(min(i, steps1 - 1), bq[i]);
+#else
   float4 bq[kL1PD][2];
 #pragma unroll
   for (int i = 0; i < kL1PD; ++i) ldb1(min(i, steps1 - 1), bq[i][0], bq[i][1]);
-  for (int kc = 0; kc < F3; kc += kL1Kc) {
-    const int kn = min(kL1Kc, F3 - kc);
-    // stage H3[r0 .. r0 + 31][kc .. kc + kL1Kc) as pieces (zero past kn; rows past n read a
-    // clamped valid row, never stored)
-    {
-      constexpr int kPer = kL1Rows * kL1Kc / 4 / kBlock;  // 4 float4 units per thread
-      float4 v[kPer];
+#endif
+  // H3[r0 .. r0 + 31][kc .. kc + kL1Kc) in registers, one chunk ahead (the next chunk's
+  // loads are in flight during this chunk's MFMAs); zero past F3, rows past n read a clamped
+  // valid row (never stored)
+  constexpr int kPer = kL1Rows * kL1Kc / 4 / kBlock;  // 4 float4 units per thread
+  float4 hv[kPer];
+  auto ldh3 = [&](int kc) {
 #pragma unroll
-      for (int q = 0; q < kPer; ++q) {
-        const int u = tid + q * kBlock, row = u / (kL1Kc / 4), k4 = (u % (kL1Kc / 4)) * 4;
-        const float4 x = *reinterpret_cast<const float4*>(h3 + (int64_t)min(r0 + row, n - 1) * ldh + kc + min(k4, kn - 4));
-        v[q] = k4 < kn ? x : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+    for (int q = 0; q < kPer; ++q) {
+      const int u = tid + q * kBlock, row = u / (kL1Kc / 4), k4 = (u % (kL1Kc / 4)) * 4;
+      const float4 x = *reinterpret_cast<const float4*>(h3 + (int64_t)min(r0 + row, n - 1) * ldh + min(kc + k4, F3 - 4));
+      hv[q] = kc + k4 < F3 ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  ldh3(0);
+  for (int kc = 0; kc < F3; kc += kL1Kc) {
+    // stage the chunk as pieces, then start the next chunk's loads
+    {
+      float4* v = hv;
 #pragma unroll
       for (int q = 0; q < kPer; ++q) {
         const int u = tid + q * kBlock, row = u / (kL1Kc / 4), k4 = (u % (kL1Kc / 4)) * 4;
@@ -356,6 +441,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
       }
     }
     __syncthreads();
+    if (kc + kL1Kc < F3) ldh3(kc + kL1Kc);
     // the chunk's K steps (kL1Kc / 16 = 8, a multiple of kL1PD); W1 fragments kL1PD steps
     // ahead in a register ring (loads unconditional, clamped; the MFMAs of steps past F3 skipped)
     const int sc = kc / 16;
@@ -364,6 +450,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
 #pragma unroll
       for (int j = 0; j < kL1PD; ++j) {
         const int i = i0 + j, s = sc + i;
+#if PG_L1_PRESPLIT
+        if (s < steps1 && PG_L1_SKIP != 1) {
+          bf16x8 fa[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            fa[p] = *reinterpret_cast<const bf16x8*>(sp + (p * kL1Rows + l32) * kL1SA + 16 * i + 8 * h);
+          pg_x3::mfma6(acc, fa, bq[j]);
+        }
+        if (PG_L1_SKIP != 1) ldf1(min(s + kL1PD, steps1 - 1), bq[j]);
+#else
         bf16x8 fb[3];
         split8(bq[j][0], bq[j][1], fb);
         ldb1(min(s + kL1PD, steps1 - 1), bq[j][0], bq[j][1]);
@@ -374,6 +470,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
             fa[p] = *reinterpret_cast<const bf16x8*>(sp + (p * kL1Rows + l32) * kL1SA + 16 * i + 8 * h);
           pg_x3::mfma6(acc, fa, fb);
         }
+#endif
         __builtin_amdgcn_sched_barrier(0);  // one step's fragments live at a time
       }
     }
@@ -402,8 +499,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
       const int ri = rg + hh * (kBlock / kMaxC);
       if (c < C && ri < nr) {
         const int64_t r = r0 + ri;
-        const int set = row_set[r];
-        const float t = labels[r * ldl + c];
+        const int set = hset[hh];
+        const float t = hlab[hh];
         const float4* ar = reinterpret_cast<const float4*>(a + ri * S);
         const float4* wr = reinterpret_cast<const float4*>(w + c * S);
         float zz = 0.f;
@@ -414,13 +511,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
           zz = fmaf(x.z, y.z, zz);
           zz = fmaf(x.w, y.w, zz);
         }
-        zz = zz + b2[c];
+        zz = zz + hb2;
         const float pr = 1.f / (1.f + expf(-zz));
         if (prob) prob[r * ldp + c] = pr;
         float gz = 0.f;
         if (set != 0) {
-          const float wc = cw[2 * c];
-          const float wp1 = cw[2 * c + 1];
+          const float wc = hwc;
+          const float wp1 = hwp1;
           const float cp = fminf(fmaxf(pr, 1e-9f), 10.f);
           const float q = 1.f - pr;
           const float cq = fminf(fmaxf(q, 1e-9f), 10.f);
@@ -486,9 +583,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
 
   // ---- phase 3: dH3 = (dA4 W1) * leaky'(H3), one 32-column tile per wave and pass ----
   const int steps3 = K16 / 16;
-  for (int c0 = 32 * wave; c0 < F3; c0 += 128) {
+  for (int c0 = 32 * wave; c0 < (PG_L1_SKIP == 3 ? 0 : F3); c0 += 128) {
     const int col = c0 + l32;
     const int colc = min(col, F3 - 1);
+#if !PG_L1_PRESPLIT
     // W1[k][col], k = 16 s + 8 h + i (i < 8): one strided column piece per fragment (each load
     // instruction: 32 consecutive floats of one W1 row per lane half); rows past K1 read 0
     // through the descriptor
@@ -498,6 +596,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
       for (int i = 0; i < 8; ++i)
         v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw1, vo3 + (16 * s + i) * (int)ldw1 * 4, 0, 0));
     };
+#endif
     // the activation operand of the epilogue, loaded first (used last); rows past n read 0
     float y[16];
     {
@@ -514,6 +613,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
     for (int r = 0; r < 16; ++r) acc3[r] = 0.f;
     // every K step's W1 fragment of this tile in flight at once (K1 <= 128: at most 8 steps;
     // steps past K16 read zeros and are not multiplied)
+#if PG_L1_PRESPLIT
+    // p3's fragment of step s: block (c0 / 32, 2 s + h), this lane's 16 B, per piece;
+    // kL1PD steps ahead in a register ring
+    const __amdgpu_buffer_rsrc_t rp3 = pg_x3::rsrc(p3, (uint32_t)(3 * l1_p3_plane(F3, K1) * 2));
+    const int pl3 = (int)(l1_p3_plane(F3, K1) * 2), kb3 = K16 / 8;
+    auto ldf3 = [&](int s, bf16x8 (&f)[3]) {
+      const int off = (((c0 >> 5) * kb3 + 2 * s + h) * 32 + l32) * 16;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        f[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rp3, off + p * pl3, 0, 0));
+    };
+    bf16x8 bv[kL1PD][3];
+#pragma unroll
+    for (int i = 0; i < kL1PD; ++i) ldf3(min(i, steps3 - 1), bv[i]);
+#pragma nounroll
+    for (int s0 = 0; s0 < steps3; s0 += kL1PD) {
+#pragma unroll
+      for (int i = 0; i < kL1PD; ++i) {
+        const int s = s0 + i;
+        if (s < steps3) {
+          bf16x8 fa[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            fa[p] = *reinterpret_cast<const bf16x8*>(sd + (p * kL1Rows + l32) * SD + 16 * s + 8 * h);
+          pg_x3::mfma6(acc3, fa, bv[i]);
+        }
+        ldf3(min(s + kL1PD, steps3 - 1), bv[i]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#else
     float bv[kL1K1 / 16][8];
 #pragma unroll
     for (int s = 0; s < kL1K1 / 16; ++s) ldb3(s, bv[s]);
@@ -529,6 +659,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
         pg_x3::mfma6(acc3, fa, fb);
       }
     }
+#endif
     // epilogue: act'(H3) (as x3_store's EPI_DLEAKY: 1 * acc, then y > 0 ? x : x slope)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -584,9 +715,10 @@ int pg_mlp_head(const void* a4, int64_t lda, int64_t n, int32_t K, int a_dtype, 
 }
 
 size_t pg_mlp_l1_head_workspace(int64_t n, int32_t C, int32_t F3, int32_t K1) {
-  (void)F3;
-  (void)K1;
-  return pg_mlp_head_workspace(n, C);
+  const size_t head = (pg_mlp_head_workspace(n, C) + 255) / 256 * 256;
+  if (!PG_L1_PRESPLIT || F3 <= 0 || K1 <= 0) return head;
+  const size_t p1 = (size_t)(3 * l1_p1_plane(F3) * 2 + 255) / 256 * 256;
+  return head + p1 + (size_t)(3 * l1_p3_plane(F3, K1) * 2);
 }
 
 int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const float* w1, int64_t ldw1,
@@ -614,10 +746,20 @@ int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const fl
   hipStream_t st = (hipStream_t)stream;
   const int nb = (int)((n + kL1Rows - 1) / kL1Rows);
   float* part = (float*)ws;
+  uint16_t* p1 = nullptr;
+  uint16_t* p3 = nullptr;
+  if (PG_L1_PRESPLIT) {
+    p1 = (uint16_t*)((char*)ws + (pg_mlp_head_workspace(n, C) + 255) / 256 * 256);
+    p3 = p1 + ((size_t)(3 * l1_p1_plane(F3) * 2 + 255) / 256 * 256) / 2;
+    const int units = (int)(kL1K1 * ((F3 + 15) / 16 * 2) + ((F3 + 31) / 32 * 32) * ((K1 + 15) / 16 * 2));
+    hipLaunchKernelGGL(l1_split_kernel, dim3((units + kBlock - 1) / kBlock), dim3(kBlock), 0, st, w1, ldw1, (int)K1,
+                       (int)F3, p1, p3);
+  }
   const float inv_n = n_train > 0 ? 1.0f / (float)n_train : 0.f;
   hipLaunchKernelGGL(mlp_l1_head_kernel, dim3(nb), dim3(kBlock), (unsigned)l1_region_bytes(K1), st, h3, ldh, (int)n,
                      (int)F3, w1, ldw1, b1, (int)K1, a4, lda4, w2, ldw, b2, (int)C, labels, ldl, class_w, row_set, inv_n,
-                     prob, ldp, dz, lddz, da4, ldg, dh3, lddh, slope, part, nb);
+                     prob, ldp, dz, lddz, da4, ldg, dh3, lddh, slope, part, nb, (const uint16_t*)p1,
+                     (const uint16_t*)p3);
   hipLaunchKernelGGL(head_final_kernel, dim3(2), dim3(64 * kMaxC), 0, st, (const float*)part, nb, (int)C, n_train,
                      n_val, loss2, adam_state, lr, beta1, beta2);
   const hipError_t e = hipGetLastError();
