@@ -83,11 +83,11 @@ __device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t x3_rsrc(const float* P, uint32_t bytes) { return pg_x3::rsrc(P, bytes); }
 constexpr uint32_t kX3Oob = 0xFFFFFFF0u;  // a byte offset past every descriptor's range: reads 0
 
-template <int ROWS, bool KMAJ>
+template <int ROWS, bool KMAJ, int NTH = NT>
 struct Stage {
   static constexpr int UNITS = ROWS * KS / 4;
-  static constexpr int PER = UNITS / NT;
-  static_assert(PER >= 1 && UNITS % NT == 0, "units per thread");
+  static constexpr int PER = UNITS / NTH;
+  static_assert(PER >= 1 && UNITS % NTH == 0, "units per thread");
   float4 v[PER];
 
   __device__ __forceinline__ static void unit_pos(int q, int& row, int& k) {
@@ -133,7 +133,7 @@ struct Stage {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int row, k;
-      unit_pos(tid + i * NT, row, k);
+      unit_pos(tid + i * NTH, row, k);
       const int gk = k0 + k;
       // straight-line: a unit past kz1 reads a 16-B zero word in global memory instead of
       // being zeroed behind a branch, so every load is unconditional and the compiler
@@ -150,7 +150,7 @@ struct Stage {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int row, k;
-      unit_pos(tid + i * NT, row, k);
+      unit_pos(tid + i * NTH, row, k);
       uint2 pc[3];
       split4(v[i], pc);
       const int off = img_off<ROWS, KMAJ>(row, k);
@@ -179,20 +179,20 @@ struct Stage {
 // valid row, never stored) and its k within a K step. A step then costs one add, one
 // compare and one select per unit (a unit at or past kz1 reads through an out-of-range
 // offset: zeros), no 64-bit address arithmetic.
-template <int ROWS, bool KMAJ>
+template <int ROWS, bool KMAJ, int NTH = NT>
 struct StageAddr {
-  static constexpr int PER = Stage<ROWS, KMAJ>::PER;
+  static constexpr int PER = Stage<ROWS, KMAJ, NTH>::PER;
   // k image: unit i of a thread sits KQS k-rows below unit 0 in the same 4 rows, so one
   // offset and a wave-uniform stride describe them all; row image: every unit its own row
   // (clamped), one k
-  static constexpr int KQS = KMAJ ? NT / (ROWS / 4) : 0;
+  static constexpr int KQS = KMAJ ? NTH / (ROWS / 4) : 0;
   static constexpr int NOFF = KMAJ ? 1 : PER;
   uint32_t off_[NOFF];
   uint32_t ustride;  // KMAJ: bytes between consecutive units (wave-uniform)
   int kq0;
   __device__ __forceinline__ void setup(int64_t ld, int r0, int R, int k0, int tid) {
     int row, k;
-    Stage<ROWS, KMAJ>::unit_pos(tid, row, k);
+    Stage<ROWS, KMAJ, NTH>::unit_pos(tid, row, k);
     kq0 = k;
     if constexpr (KMAJ) {
       off_[0] = ((uint32_t)(k0 + k) * (uint32_t)ld + (uint32_t)min(r0 + row, R - 4)) * 4u;
@@ -200,7 +200,7 @@ struct StageAddr {
     } else {
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
-        Stage<ROWS, KMAJ>::unit_pos(tid + i * NT, row, k);
+        Stage<ROWS, KMAJ, NTH>::unit_pos(tid + i * NTH, row, k);
         off_[i] = ((uint32_t)min(r0 + row, R - 1) * (uint32_t)ld + (uint32_t)(k0 + k)) * 4u;
       }
       ustride = 0;
@@ -216,21 +216,22 @@ struct StageAddr {
 
 // The accumulator tile leaves through LDS in PASSES row bands (16-B stores), with the
 // epilogue (alpha, beta C, bias, act / act', or the split-K partial slab).
-template <int BM, int BN, int EPI, int PASSES>
-__device__ __forceinline__ void x3_store(const f32x16 (&acc)[BM / 64][BN / 64], float* __restrict__ img, int tid,
+template <int BM, int BN, int EPI, int PASSES, int NTH = NT>
+__device__ __forceinline__ void x3_store(const f32x16 (&acc)[BM / 64][BN / (32 * (NTH / 128))], float* __restrict__ img, int tid,
                                          int m0, int n0, int M, int N, int kz, float alpha, float beta,
                                          float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
                                          float slope, const float* __restrict__ dact, int64_t lddact,
                                          float* __restrict__ ws) {
   constexpr bool SPLIT = EPI == EPI_SPLIT;
-  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int WN = NTH / 128;  // waves along N (2 x WN waves)
+  constexpr int TM = BM / 64, TN = BN / (32 * WN);
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
+  const int wm = wave / WN, wn = wave % WN, h = lane >> 5, l32 = lane & 31;
   constexpr int BAND = BM / PASSES;
-  constexpr int IT = BAND * BN / 4 / NT;  // output quads per thread and pass
+  constexpr int IT = BAND * BN / 4 / NTH;  // output quads per thread and pass
   constexpr int CH = IT < 8 ? IT : 8;     // quads whose operand loads are in flight together
   constexpr bool DACT = EPI == EPI_DRELU || EPI == EPI_DLEAKY;
-  static_assert(NT % (BN / 4) == 0 && IT % CH == 0, "one column quad per thread");
+  static_assert(NTH % (BN / 4) == 0 && IT % CH == 0, "one column quad per thread");
   // this thread's column quad is the same in every iteration: its bias is loaded once, and
   // the activation operand's quads are loaded CH at a time ahead of their use (clamped
   // addresses, no branch: behind the store loop's bounds test the loads would run one at a
@@ -244,7 +245,7 @@ __device__ __forceinline__ void x3_store(const f32x16 (&acc)[BM / 64][BN / 64], 
     if constexpr (DACT) {
 #pragma unroll
       for (int q = 0; q < CH; ++q) {
-        const int row = ((c0 + q) * NT + tid) / (BN / 4);
+        const int row = ((c0 + q) * NTH + tid) / (BN / 4);
         const int gr = min(m0 + pass * BAND + row, M - 1);
         y4[q] = *reinterpret_cast<const float4*>(dact + (int64_t)gr * lddact + gcl);
       }
@@ -261,7 +262,7 @@ __device__ __forceinline__ void x3_store(const f32x16 (&acc)[BM / 64][BN / 64], 
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h - pass * BAND;
-            img[row * BN + wn * (BN / 2) + j * 32 + l32] = acc[i][j][r];
+            img[row * BN + wn * (BN / WN) + j * 32 + l32] = acc[i][j][r];
           }
     }
     __syncthreads();
@@ -270,7 +271,7 @@ __device__ __forceinline__ void x3_store(const f32x16 (&acc)[BM / 64][BN / 64], 
       if (c0 > 0) prefetch(pass, c0);
 #pragma unroll
       for (int q = 0; q < CH; ++q) {
-        const int u = (c0 + q) * NT + tid;
+        const int u = (c0 + q) * NTH + tid;
         const int row = u / (BN / 4), c = cq;
         const int gr = m0 + pass * BAND + row, gc = n0 + c;
         if (gr >= M || gc >= N) continue;
@@ -354,7 +355,7 @@ struct X3Cat {
   int64_t ldb2;
   int kcat;
 };
-template <int BM, int BN, bool TA, bool TB, int EPI, bool KCAT = false>
+template <int BM, int BN, bool TA, bool TB, int EPI, bool KCAT = false, int NTH = NT>
 __device__ __forceinline__ void x3_tile(
     uint16_t* __restrict__ lds, int M, int N, int K, int k_per_split, int kz, int tm, int tn, float alpha,
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, float beta,
@@ -363,15 +364,16 @@ __device__ __forceinline__ void x3_tile(
     float* __restrict__ ws, float* __restrict__ ws_rowsum, X3Cat cat = {}) {
   constexpr bool AK = TA, BKM = !TB;
   constexpr bool SPLIT = EPI == EPI_SPLIT;
-  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int WN = NTH / 128;  // waves along N (2 x WN waves)
+  constexpr int TM = BM / 64, TN = BN / (32 * WN);
   constexpr int IA = BM * KS, IB = BN * KS;  // one piece's image (u16)
   constexpr int BUF = 3 * (IA + IB);         // one buffer: [A_h A_m A_l | B_h B_m B_l]
   constexpr int STAGE_U16 = 2 * BUF;
   constexpr int PASSES = 2 * BM * BN > STAGE_U16 ? 2 : 1;  // f32 epilogue image in row bands
-  static_assert(x3_lds_u16<BM, BN>() * 2 >= NT * 4 * 8, "row-sum scratch");
+  static_assert(x3_lds_u16<BM, BN>() * 2 >= NTH * 4 * 8, "row-sum scratch");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, l32 = lane & 31;
+  const int wm = wave / WN, wn = wave % WN, l32 = lane & 31;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kz0 = kz * k_per_split;
   const int kz1 = min(K, kz0 + k_per_split);
@@ -385,8 +387,8 @@ __device__ __forceinline__ void x3_tile(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  Stage<BM, AK> sa;
-  Stage<BN, BKM> sb;
+  Stage<BM, AK, NTH> sa;
+  Stage<BN, BKM, NTH> sb;
   static_assert(!KCAT || PG_X3_BUFLOAD, "K-concatenated operands need the buffer-load addressing");
 #if PG_X3_BUFLOAD
   // operand extents in bytes (row image: R rows of ld; k image: K rows of ld); with KCAT the
@@ -396,13 +398,13 @@ __device__ __forceinline__ void x3_tile(
   const uint32_t b_bytes = (uint32_t)(BKM ? ((int64_t)(K1 - 1) * ldb + N) * 4 : ((int64_t)(N - 1) * ldb + K1) * 4);
   const __amdgpu_buffer_rsrc_t rsa = x3_rsrc(A, a_bytes), rsb = x3_rsrc(B, b_bytes);
   const uint32_t a_kstride = AK ? (uint32_t)lda * 4u : 4u, b_kstride = BKM ? (uint32_t)ldb * 4u : 4u;
-  StageAddr<BM, AK> aa;
-  StageAddr<BN, BKM> ab;
+  StageAddr<BM, AK, NTH> aa;
+  StageAddr<BN, BKM, NTH> ab;
   aa.setup(lda, m0, M, kz0, tid);
   ab.setup(ldb, n0, N, kz0, tid);
   // KCAT: the second operands' addressing (their own k starts at 0 where the first ends)
-  StageAddr<BM, AK> aa2;
-  StageAddr<BN, BKM> ab2;
+  StageAddr<BM, AK, NTH> aa2;
+  StageAddr<BN, BKM, NTH> ab2;
   __amdgpu_buffer_rsrc_t rsa2 = rsa, rsb2 = rsb;
   uint32_t a2_kstride = 0, b2_kstride = 0;
   if constexpr (KCAT) {
@@ -418,7 +420,7 @@ __device__ __forceinline__ void x3_tile(
     aa2.setup(cat.lda2, m0, M, 0, tid);
     ab2.setup(cat.ldb2, n0, N, 0, tid);
   }
-  auto load_a = [&](Stage<BM, AK>& st, int kt) {
+  auto load_a = [&](Stage<BM, AK, NTH>& st, int kt) {
     if constexpr (KCAT) {
       st.load_cat(aa, aa2, rsa, rsa2, (uint32_t)(kt - kz0) * a_kstride, (uint32_t)(kt - cat.kcat) * a2_kstride,
                   cat.kcat, kt, kz1);
@@ -426,7 +428,7 @@ __device__ __forceinline__ void x3_tile(
       st.load(aa, rsa, (uint32_t)(kt - kz0) * a_kstride, kt, kz1);
     }
   };
-  auto load_b = [&](Stage<BN, BKM>& st, int kt) {
+  auto load_b = [&](Stage<BN, BKM, NTH>& st, int kt) {
     if constexpr (KCAT) {
       st.load_cat(ab, ab2, rsb, rsb2, (uint32_t)(kt - kz0) * b_kstride, (uint32_t)(kt - cat.kcat) * b2_kstride,
                   cat.kcat, kt, kz1);
@@ -435,15 +437,15 @@ __device__ __forceinline__ void x3_tile(
     }
   };
 #else
-  auto load_a = [&](Stage<BM, AK>& st, int kt) { st.load(A, lda, m0, M, kt, kz1, tid); };
-  auto load_b = [&](Stage<BN, BKM>& st, int kt) { st.load(B, ldb, n0, N, kt, kz1, tid); };
+  auto load_a = [&](Stage<BM, AK, NTH>& st, int kt) { st.load(A, lda, m0, M, kt, kz1, tid); };
+  auto load_b = [&](Stage<BN, BKM, NTH>& st, int kt) { st.load(B, ldb, n0, N, kt, kz1, tid); };
 #endif
-  double rs[Stage<BM, AK>::RSN];
+  double rs[Stage<BM, AK, NTH>::RSN];
 #pragma unroll
-  for (int i = 0; i < Stage<BM, AK>::RSN; ++i) rs[i] = 0.0;
+  for (int i = 0; i < Stage<BM, AK, NTH>::RSN; ++i) rs[i] = 0.0;
 
   const int nk = kz1 > kz0 ? (kz1 - kz0 + KS - 1) / KS : 0;
-  const int ra = wm * (BM / 2) + l32, rb = wn * (BN / 2) + l32;
+  const int ra = wm * (BM / 2) + l32, rb = wn * (BN / WN) + l32;
   auto mfmas = [&](const uint16_t* As, const uint16_t* Bs) {
     bf16x8 fa[3][TM], fb[3][TN];
 #pragma unroll
@@ -472,8 +474,8 @@ __device__ __forceinline__ void x3_tile(
     // loads are unconditional) into the slot tile t left, and stores tile t + 1. Measured
     // on the cfg2 step: GEMM 916 -> 902 us (the split waits for a tile issued a step
     // earlier instead of during the same step's MFMAs)
-    Stage<BM, AK> sa2;
-    Stage<BN, BKM> sb2;
+    Stage<BM, AK, NTH> sa2;
+    Stage<BN, BKM, NTH> sb2;
     load_a(sa, kz0);
     load_b(sb, kz0);
     const int k1c = kz0 + min(1, nk - 1) * KS;
@@ -485,7 +487,7 @@ __device__ __forceinline__ void x3_tile(
     __syncthreads();
     // loads sit outside every branch (only MFMAs and stores are conditional), so the
     // compiler's wait counts stay exact across the loop
-    auto kstep = [&](int t, Stage<BM, AK>& la, Stage<BN, BKM>& lb, Stage<BM, AK>& na, Stage<BN, BKM>& nb) {
+    auto kstep = [&](int t, Stage<BM, AK, NTH>& la, Stage<BN, BKM, NTH>& lb, Stage<BM, AK, NTH>& na, Stage<BN, BKM, NTH>& nb) {
       const int cur = t & 1;
       const int kl = kz0 + min(t + 2, nk - 1) * KS;
       load_a(la, kl);
@@ -544,9 +546,9 @@ __device__ __forceinline__ void x3_tile(
   if (do_rs) {
     double* red = reinterpret_cast<double*>(lds);
     if constexpr (!AK) {
-      // row image: unit i of thread tid is row (tid + i NT) / 4, k-quarter tid % 4
+      // row image: unit i of thread tid is row (tid + i NTH) / 4, k-quarter tid % 4
 #pragma unroll
-      for (int i = 0; i < Stage<BM, AK>::RSN; ++i) red[tid + i * NT] = rs[i];  // = 4 row + k-quarter
+      for (int i = 0; i < Stage<BM, AK, NTH>::RSN; ++i) red[tid + i * NTH] = rs[i];  // = 4 row + k-quarter
       __syncthreads();
       if (tid < BM && m0 + tid < M) {
         const double t = (red[4 * tid] + red[4 * tid + 1]) + (red[4 * tid + 2] + red[4 * tid + 3]);
@@ -555,7 +557,7 @@ __device__ __forceinline__ void x3_tile(
       }
     } else {
       // k image: thread tid holds rows 4 (tid % (BM / 4)) .. + 3 for the k-rows tid / (BM / 4)
-      constexpr int G = NT / (BM / 4);
+      constexpr int G = NTH / (BM / 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[(tid / (BM / 4)) * BM + 4 * (tid % (BM / 4)) + e] = rs[e];
       __syncthreads();
@@ -570,7 +572,7 @@ __device__ __forceinline__ void x3_tile(
   }
 
   X3_STAMP(65, 0);
-  x3_store<BM, BN, EPI, PASSES>(acc, reinterpret_cast<float*>(lds), tid, m0, n0, M, N, kz, alpha, beta, C, ldc,
+  x3_store<BM, BN, EPI, PASSES, NTH>(acc, reinterpret_cast<float*>(lds), tid, m0, n0, M, N, kz, alpha, beta, C, ldc,
                                 bias, slope, dact, lddact, ws);
   X3_STAMP(65, 1);
 }
@@ -616,8 +618,14 @@ void gemm_x3_cat_kernel(
 // Grouped split-K partials: the items of every part (its tiles x its K slices, slice-major)
 // laid end to end, one launch for all of them (the step's weight gradients: the slab bytes
 // then scale with the group's workgroups, not with each product's).
+#ifndef PG_X3_GROUP_THREADS
+#define PG_X3_GROUP_THREADS 256  // variant builds: 512 = 2 x 4 waves of 64 x 64 per 128 x 256 tile
+#endif
+#ifndef PG_X3_GROUP_WAVES
+#define PG_X3_GROUP_WAVES (PG_X3_GROUP_THREADS == 512 ? 4 : x3_waves<BM, BN>())
+#endif
 template <int BM, int BN, bool TA, bool TB>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(x3_waves<BM, BN>())))
+__global__ __launch_bounds__(PG_X3_GROUP_THREADS) __attribute__((amdgpu_waves_per_eu(PG_X3_GROUP_WAVES)))
 void gemm_x3_group_kernel(X3Group g) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[x3_lds_u16<BM, BN>()];
   const int item = x3_item(g.items);
@@ -626,7 +634,8 @@ void gemm_x3_group_kernel(X3Group g) {
   const X3Part& p = g.p[k];
   const int local = item - p.first_item;
   const int kz = local / p.tiles, tile = local % p.tiles;
-  x3_tile<BM, BN, TA, TB, EPI_SPLIT>(lds, p.M, p.N, p.K, p.kps, kz, tile / p.tiles_n, tile % p.tiles_n, 1.f, p.A,
+  x3_tile<BM, BN, TA, TB, EPI_SPLIT, false, PG_X3_GROUP_THREADS>(lds, p.M, p.N, p.K, p.kps, kz, tile / p.tiles_n,
+                                                                 tile % p.tiles_n, 1.f, p.A,
                                      p.lda, p.B, p.ldb, 0.f, nullptr, 0, nullptr, 0.f, nullptr, 0, p.rowsum, p.ws,
                                      p.ws_rowsum);
 }
@@ -666,7 +675,7 @@ int launch_trans(const X3Args& a, hipStream_t st) {
 namespace pg_gemm {
 
 int gemm_x3_group_launch(const X3Group& g, bool ta, bool tb, hipStream_t st) {
-  const dim3 grid((unsigned)g.items), block(NT);
+  const dim3 grid((unsigned)g.items), block(PG_X3_GROUP_THREADS);
 #define PG_G(TA_, TB_) \
   hipLaunchKernelGGL((gemm_x3_group_kernel<kX3GroupBM, kX3GroupBN, TA_, TB_>), grid, block, 0, st, g)
   if (ta && !tb) PG_G(true, false);
