@@ -23,6 +23,7 @@
 #include <limits>
 
 #include "common.hpp"
+#include "x3_split.hpp"
 
 namespace {
 
@@ -1044,7 +1045,10 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
     const int4* __restrict__ rows, int n_long, int n_rows, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F,
     const T* __restrict__ dout, int64_t ldd, const T* __restrict__ fout, int64_t ldf,
-    const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist, const int32_t* __restrict__ einv) {
+    const float* __restrict__ ew, R gp, uint32_t* __restrict__ glist, const int32_t* __restrict__ einv,
+    uint32_t* __restrict__ tickets, int n_tickets) {
+  // the pull's split-row ticket counters start every call at zero (this launch precedes it)
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n_tickets; i += gridDim.x * kBlock) tickets[i] = 0u;
   const DescOut<TR> dsc{glist, einv};
   constexpr int kLds = NV > 0 && kWavesPerBlock * pack_wave_ints<NV>() > kPackLds
                            ? kWavesPerBlock * pack_wave_ints<NV>() : kPackLds;
@@ -1065,6 +1069,10 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
   }
 }
 
+#ifndef PG_PULL_MERGE
+#define PG_PULL_MERGE 1  // split rows combined inside the pull (0: the sum_merge_kernel launch)
+#endif
+
 #ifndef PG_PULL_U
 #define PG_PULL_U 8  // list segments in flight per wave (4-8 best on S0, 16 +6 %, 32 +25 %)
 #endif
@@ -1080,12 +1088,28 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
 // rate on gfx950: scripts/probes/lds_rmw_probe.hip), measured slower on the engine's data:
 // a source that wins a feature at many destinations puts it many times into one segment,
 // and the swaps serialise.
-template <typename T, typename R, bool TR>
+// In-launch combine of split rows (MERGE; replaces sum_merge_kernel's launch): the pieces of a
+// row longer than the schedule's chunk store their partial rows write-through (sc1), drain
+// them, and draw a ticket from the row's counter (one per first slot, zeroed by the pack);
+// the piece that draws the last ticket reads every slot of the row with sc1 loads (no stale
+// L1 or other-XCD L2 line can serve them, so no acquire fence) and sums them in slot order
+// from +0, exactly sum_merge_kernel's order: the same bits whichever piece arrives last.
+struct PullMerge {
+  const int32_t* ptr;  // the transposed CSR's row pointers (piece index = (t0 - ptr[row]) / chunk)
+  int chunk;           // the schedule's chunk (pg_schedule_build)
+  uint32_t* tickets;   // [n_slots]
+  uint32_t ws_bytes;   // the slot region (< 2 GiB, checked on the host)
+};
+
+typedef __attribute__((address_space(1))) uint32_t pg_gu32;
+typedef uint32_t pg_u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T, typename R, bool TR, bool MERGE>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
     const int32_t* __restrict__ tdst, const uint32_t* __restrict__ glist, R gp, int F,
     const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx, float* __restrict__ ws,
-    int64_t ldw) {
+    int64_t ldw, PullMerge pm) {
   constexpr int U = PG_PULL_U;
   __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
   const int wave = wave_id_uniform();
@@ -1095,7 +1119,8 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   const int4 item = items[it];
   const int row = item.x, t0 = item.y, t1 = item.z, slot = item.w;
   const int lane = lane_id();
-  for (int f = lane; f < F; f += kWave) acc[f] = 0.f;
+  // (MERGE: the 16-B slot stores cover ldw = round_up(F, 4) columns)
+  for (int f = lane; f < (MERGE ? (int)ldw : F); f += kWave) acc[f] = 0.f;
   // descriptors (and the destinations' record bases v F) one window ahead, their in-CSR
   // slots two windows ahead (an item with no out-edges reads nothing)
   auto tl_of = [&](int tw) { return tw + min(lane, t1 - tw - 1); };
@@ -1154,6 +1179,47 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
       float a = acc[f];
       if (mr && !(to_f(mr[f]) > 0.f)) a = 0.f;
       xr[f] = from_f<T>(a);
+    }
+  } else if constexpr (MERGE) {
+    const __amdgpu_buffer_rsrc_t rs = pg_x3::rsrc(ws, pm.ws_bytes);
+    const uint32_t sbase = (uint32_t)slot * (uint32_t)ldw * 4u;
+    for (int f = lane * 4; f < F; f += kWave * 4)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pg_u32x4, *reinterpret_cast<const float4*>(acc + f)), rs, sbase + (uint32_t)f * 4u,
+                                             0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every payload store drained before the ticket
+    const int rb = pm.ptr[row], re = pm.ptr[row + 1];
+    const int s0 = slot - (t0 - rb) / pm.chunk;
+    const int ns = (re - rb + pm.chunk - 1) / pm.chunk;
+    uint32_t ticket = 0;
+    if (lane == 0)
+      ticket = __hip_atomic_fetch_add((pg_gu32*)(pm.tickets + s0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __builtin_amdgcn_readfirstlane(ticket);
+    if ((int)ticket != ns - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the ticket
+    T* xr = dx + (int64_t)row * ldx;
+    const T* mr = mask ? mask + (int64_t)row * ldm : nullptr;
+    for (int f = lane * 4; f < F; f += kWave * 4) {
+      float a[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int s = s0; s < s0 + ns; s += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[e] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+              rs, (uint32_t)min(s + e, s0 + ns - 1) * (uint32_t)ldw * 4u + (uint32_t)f * 4u, 0, 16));
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (s + e < s0 + ns) {
+            a[0] += v[e].x; a[1] += v[e].y; a[2] += v[e].z; a[3] += v[e].w;
+          }
+      }
+      if (mr) {
+        float mk[4];
+        load_tile<4, T>(mr, f, F, mk, 0.f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (!(mk[i] > 0.f)) a[i] = 0.f;
+      }
+      store_tile<4, T>(xr, f, F, a);
     }
   } else {
     float* wr = ws + (int64_t)slot * ldw;
@@ -1627,7 +1693,7 @@ int pg_spmm_max_fwd_bf16(const pg_csr_t* g, const void* X, int64_t ldx, int64_t 
                                  arg_kind, ws, ws_bytes, stream);
 }
 
-// [split-row partials][grouped path: list records N x F x 8 B | glist nnz x int2]
+// [split-row partials][grouped path: list records N x F x 8 B | glist nnz x 4 B | tickets n_slots x 4 B]
 static size_t bwd_partials_bytes(const pg_csr_t* gt, int64_t F) {
   return gt->n_slots > 0 ? round_up(gt->n_slots * ws_ld(F) * 4, 256) : 0;
 }
@@ -1638,6 +1704,7 @@ size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F) {
   if (F <= kGroupMaxF) {
     const int64_t N = gt->n_cols;
     b += round_up(N * F * 8, 256) + round_up(gt->nnz * 4, 256);
+    if (gt->n_slots > 0) b += round_up(gt->n_slots * 4, 256);  // the pull's split-row tickets
   }
   return b;
 }
@@ -1685,6 +1752,14 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     p += round_up(N * F * 8, 256);
     uint32_t* glist = (uint32_t*)p;
     p += round_up(g->nnz * 4, 256);
+    uint32_t* tickets = (uint32_t*)p;
+    // split rows combined inside the pull (sum_merge_kernel's launch otherwise): vector rows,
+    // the schedule's chunk known, a slot region a 32-bit buffer offset covers
+    constexpr uintptr_t kTm = 4 * sizeof(T) - 1;
+    const bool merge_in = PG_PULL_MERGE && gt->n_merges > 0 && gt->chunk > 0 && F % 4 == 0 && ldx % 4 == 0 &&
+                          ((uintptr_t)dx & kTm) == 0 && ((uintptr_t)w & 15) == 0 && pbytes < ((size_t)1 << 31) &&
+                          (!mask_src || dead_none || (ldm % 4 == 0 && ((uintptr_t)mask_src & kTm) == 0));
+    const int n_tickets = merge_in ? (int)gt->n_slots : 0;
     const auto* arg16 = (const uint16_t*)argpos;
     // rows past kPackWaveMax: the schedule's split rows when its chunk guarantees they are
     // a superset, else every row
@@ -1713,7 +1788,8 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     auto pack = [&](auto nv_c) {
       constexpr int NV = decltype(nv_c)::value;
       hipLaunchKernelGGL((group_pack_kernel<uint16_t, T, NV, R, TR>), pgrid, dim3(kBlock), 0, st, prow, n_long,
-                         (int)N, g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, g->ew, gp, glist, g->epos);
+                         (int)N, g->ptr, arg16, lda, (int)F, dout, ldd, fwd_out, ldf, g->ew, gp, glist, g->epos,
+                         tickets, n_tickets);
       return PG_OK;
     };
     if (vec) dispatch_nc_vec((int)((F + 255) / 256), pack);
@@ -1723,10 +1799,16 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     // in the lists has a maximum X[u,f] w != 0, so X[u,f] > 0; an element with no entries
     // sums to +0, which the mask would leave +0. With fwd_out alone the mask is applied.
     if (dead_none) mask_src = nullptr;
-    hipLaunchKernelGGL((max_bwd_pull_kernel<T, R, TR>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
-                       (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
-                       dx, ldx, w, ws_ld(F));
-    if (gt->n_merges > 0)
+    const PullMerge pm{gt->ptr, gt->chunk, tickets, (uint32_t)pbytes};
+    if (merge_in)
+      hipLaunchKernelGGL((max_bwd_pull_kernel<T, R, TR, true>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
+                         (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
+                         dx, ldx, w, ws_ld(F), pm);
+    else
+      hipLaunchKernelGGL((max_bwd_pull_kernel<T, R, TR, false>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
+                         (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
+                         dx, ldx, w, ws_ld(F), pm);
+    if (gt->n_merges > 0 && !merge_in)
       hipLaunchKernelGGL(sum_merge_kernel<T>, dim3((unsigned)gt->n_merges), dim3(kBlock), 0, st,
                          (const int4*)gt->merges, (int)gt->n_merges, (int)F, w, ws_ld(F), gt->ptr, 0,
                          mask_src, ldm, dx, ldx);

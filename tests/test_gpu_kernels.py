@@ -3,7 +3,8 @@
 Bars: the max aggregation and its argmax are bit-exact (selection, integer positions);
 the max backward is bit-exact on rows that are not split across work items (same
 ascending-destination summation order as the oracle's sequential scatter_add_) and
-within 1e-6 relative on split rows; sums / GEMMs within the fp32 tolerances stated per
+within 1e-6 relative of it on split rows, which are bit-exact against the schedule's own
+piecewise order (`_piecewise_max_bwd`); sums / GEMMs within the fp32 tolerances stated per
 test.
 """
 import numpy as np
@@ -138,6 +139,70 @@ def test_spmm_max_bwd(oracle_mod, F, weighted, trans):
     # DGL scatter form (atomics: the fp32 summation order varies run to run, as in DGL)
     dXs = ops.spmm_max_backward_scatter(dg, argpos, torch.from_numpy(dZ).to(DEV), ews).cpu().numpy()
     np.testing.assert_allclose(dXs, dX_ref, rtol=1e-4, atol=1e-4)
+
+
+def _piecewise_max_bwd(g, argpos, dZ, ew_slots):
+    """dX of the max backward exactly as its schedule sums it: every out-CSR row longer than
+    the schedule's chunk is cut into pieces of `chunk` edges, each piece summed in
+    ascending destination order in f32 from +0, and the pieces' sums added in piece order
+    from +0 (sum_merge_kernel's order, and the in-pull combine's); a shorter row is one
+    piece. The contributions are the pack's records: w * dZ[v, f] (f32 product) where the
+    argmax position of (v, f) is the edge's in-CSR position."""
+    fptr, bptr, bcol, bslot, c = g.fwd.ptr, g.bwd.ptr, g.bwd.col, g.bwd.eslot, g.bwd.chunk
+    n, F = dZ.shape
+    ap = argpos.astype(np.int64)
+    if argpos.dtype == np.int16:  # u16 records ("none" = 0xFFFF matches no position)
+        ap &= 0xFFFF
+    dX = np.zeros((n, F), np.float32)
+    for u in range(len(bptr) - 1):
+        b, e = int(bptr[u]), int(bptr[u + 1])
+        pieces = [(b, e)] if e - b <= c else [(k, min(e, k + c)) for k in range(b, e, c)]
+        tot = np.zeros(F, np.float32)
+        for k0, k1 in pieces:
+            acc = np.zeros(F, np.float32)
+            for t in range(k0, k1):
+                v, s = int(bcol[t]), int(bslot[t])
+                hit = ap[v] == s - int(fptr[v])
+                val = dZ[v] if ew_slots is None else np.float32(ew_slots[s]) * dZ[v]
+                acc[hit] += val[hit]
+            tot = acc if len(pieces) == 1 else tot + acc
+        dX[u] = tot
+    return dX
+
+
+@pytest.mark.parametrize("F", [4, 64, 256, 503, 504])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("chunk_bwd,trans", [(4, False), (4, True), (64, False), (512, True)])
+def test_spmm_max_bwd_split_rows_bitexact(oracle_mod, F, weighted, chunk_bwd, trans):
+    """Every row bit-exact, split rows included, against the schedule's own summation order
+    (`_piecewise_max_bwd`). chunk_bwd = 4 splits almost every source row, so thousands of
+    pieces race for the in-pull combine's tickets (F % 4 == 0; F = 503 takes the separate
+    merge launch); two calls in a row must agree (the tickets restart at zero every call)."""
+    import plagnn
+    from plagnn import ops
+
+    n = 700
+    src, dst = hub_graph(n, 1500, seed=F + chunk_bwd)
+    rng = np.random.default_rng(F + 3)
+    w = rng.uniform(-1, 2, len(src)).astype(np.float32) if weighted else None
+    g = plagnn.CSRGraph(src, dst, n, chunk=256, chunk_bwd=chunk_bwd, bwd_trans=trans)
+    assert g.bwd.n_merges >= (300 if chunk_bwd == 4 else 1)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    X[rng.random((n, F)) < 0.4] = 0.0
+    dZ = rng.standard_normal((n, F)).astype(np.float32)
+    dg = g.on(DEV)
+    ews = dg.edge_weight_slots(None if w is None else torch.from_numpy(w))
+    out, argpos = ops.spmm_max(dg, torch.from_numpy(X).to(DEV), ews)
+    dZd = torch.from_numpy(dZ).to(DEV)
+    dX = ops.spmm_max_backward(dg, argpos, dZd, ews)
+    dX2 = ops.spmm_max_backward(dg, argpos, dZd, ews)
+    torch.cuda.synchronize()
+    assert torch.equal(dX, dX2)
+    ref = _piecewise_max_bwd(g, argpos.cpu().numpy(), dZ, None if ews is None else ews.cpu().numpy())
+    np.testing.assert_array_equal(dX.cpu().numpy(), ref)
+    # the fused relu' mask on the combined rows
+    dXm = ops.spmm_max_backward(dg, argpos, dZd, ews, mask=torch.from_numpy(X).to(DEV)).cpu().numpy()
+    np.testing.assert_array_equal(dXm, np.where(X > 0, ref, 0.0))
 
 
 def test_spmm_max_int32_positions(oracle_mod):
