@@ -688,17 +688,6 @@ __device__ __forceinline__ int wave_incl_add(int x) {
 #endif
 }
 
-// inclusive max-scan over the wave (values >= -1)
-__device__ __forceinline__ int wave_incl_max(int x) {
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));  // row_shr:1
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));  // row_shr:2
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));  // row_shr:4
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));  // row_shr:8
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return x;
-}
-
 __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   const int per = (n + kBlock - 1) / kBlock;
   const int b = threadIdx.x * per;
@@ -1084,13 +1073,6 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
 #define PG_PULL_MERGE 1  // split rows combined inside the pull (0: the sum_merge_kernel launch)
 #endif
 
-#ifndef PG_PULL_DENSE
-#define PG_PULL_DENSE 0  // dense 64-entry chunks across lists (0: one load per list segment)
-#endif
-#ifndef PG_PULL_D
-#define PG_PULL_D 2  // dense chunks' loads in flight per wave
-#endif
-
 #ifndef PG_PULL_U
 #define PG_PULL_U 8  // list segments in flight per wave (4-8 best on S0, 16 +6 %, 32 +25 %)
 #endif
@@ -1128,10 +1110,8 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
     const int32_t* __restrict__ tdst, const uint32_t* __restrict__ glist, R gp, int F,
     const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx, float* __restrict__ ws,
     int64_t ldw, PullMerge pm) {
-  [[maybe_unused]] constexpr int U = PG_PULL_U;
-  [[maybe_unused]] constexpr int D = PG_PULL_D;
-  // per wave: the row accumulator (+ 64 ints: the dense chunks' list starts)
-  __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF + (PG_PULL_DENSE ? kWave : 0)];
+  constexpr int U = PG_PULL_U;
+  __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][kGroupMaxF];
   const int wave = wave_id_uniform();
   const int it = blockIdx.x * kWavesPerBlock + wave;
   if (it >= n_items) return;
@@ -1161,50 +1141,6 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
       vf_next = tdst[tl_of(tw + kWave)] * F;
       if (!TR && tw + 2 * kWave < t1) ts_next = tslot[tl_of(tw + 2 * kWave)];
     }
-#if PG_PULL_DENSE
-    // dense chunks: entry e of the window's lists, concatenated in edge order, on lane e % 64
-    // of chunk e / 64 (a list of a few records no longer takes a whole load instruction);
-    // D chunks' loads in flight, then the adds list by list in edge order (a list never
-    // repeats a feature; two lists can, and add in ascending destination as before)
-    {
-      const int cnt = lane < nw ? dsc.y : 0;
-      const int incl = wave_incl_add(cnt);
-      const int excl = incl - cnt;
-      const int total = bcast(incl, kWave - 1);
-      const uint64_t nonempty = __ballot(cnt > 0);
-      const int last_list = nonempty ? 63 - __clzll(nonempty) : 0;
-      int* starts = reinterpret_cast<int*>(acc + kGroupMaxF);
-      for (int c0 = 0; c0 < total; c0 += kWave * D) {
-        int fe[D], oe[D];
-        float de[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-          const int cb = c0 + d * kWave;
-          // the owner of entry cb + lane: the last non-empty list starting at or before it
-          starts[lane] = -1;
-          wave_lds_sync();
-          if (cnt > 0 && excl >= cb && excl < cb + kWave) starts[excl - cb] = lane;
-          const uint64_t before = __ballot(cnt > 0 && excl < cb);
-          wave_lds_sync();
-          const int o = wave_incl_max(max(starts[lane], before ? 63 - __clzll(before) : -1));
-          // lanes past the end re-load the window's last entry (straight-line loads)
-          const bool live = cb + lane < total;
-          const int ol = live ? o : last_list;
-          const int el = live ? cb + lane : total - 1;
-          gp.get(__shfl(dsc.x, ol) + (el - __shfl(excl, ol)), fe[d], de[d]);
-          oe[d] = live ? ol : -1;
-        }
-        uint64_t lists = __ballot(cnt > 0 && incl > c0 && excl < c0 + kWave * D);
-        while (lists) {
-          const int i = __builtin_ctzll(lists);
-          lists &= lists - 1;
-#pragma unroll
-          for (int d = 0; d < D; ++d)
-            if (oe[d] == i) acc[fe[d]] += de[d];
-        }
-      }
-    }
-#else
     // segments: 64-entry pieces of single lists, U segments' loads in flight. Segment t
     // belongs to the edge i with excl_i <= t < excl_i + nseg_i, i.e.
     // i = popcount(ballot(excl <= t)) - 1.
@@ -1234,7 +1170,6 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
           if (u < nv && lane < ne[u]) acc[fe[u]] += de[u];
       }
     }
-#endif
   }
   wave_lds_sync();
   if (slot < 0) {
