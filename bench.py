@@ -666,12 +666,7 @@ def main(argv=None):
     ap.add_argument("--chunk-bwd", type=int, default=0, help=argparse.SUPPRESS)  # tuning experiments
     ap.add_argument("--separate-l1-head", action="store_true", help=argparse.SUPPRESS)  # A/B: unfused MLP head
     ap.add_argument("--separate-adam-prep", action="store_true", help=argparse.SUPPRESS)  # A/B: own prepare launch
-    ap.add_argument("--side-wgrad", default="", help=argparse.SUPPRESS)  # A/B: none | top | layers
     args = ap.parse_args(argv)
-    if args.side_wgrad:
-        import plagnn.engine
-
-        plagnn.engine.TrainEngine.SIDE_WGRAD = None if args.side_wgrad == "none" else args.side_wgrad
     if args.separate_l1_head:
         import plagnn.engine
 

@@ -95,13 +95,6 @@ class TrainEngine:
     _rec: Optional[list] = None    # gemm_bytes_per_step's dry-run record
     _split_buckets = False         # dp: the weight gradients as two grouped launches (grad_buckets)
     _ar_inline = None              # dp over RCCL: the BucketAllReduce launched from inside the backward
-    # single-model steps: grouped weight gradients of the upper layers on a second stream, each
-    # as soon as its layer's backward has issued them, beside the lower layers' backward;
-    # "top": the top SAGE layer + the MLP; "layers": every layer but the bottom one, one group
-    # each; None: all of them at the end of the backward (A/B knob)
-    SIDE_WGRAD: Optional[str] = None
-    _side = None                   # that stream (created on first use)
-    _side_used = False
 
     def __init__(self, graph: CSRGraph, features: torch.Tensor, labels: torch.Tensor,
                  dims: Sequence[int], class_weight, train_index, val_index=None,
@@ -246,12 +239,9 @@ class TrainEngine:
             self._gemm_plans[(M_, N_, K_)] = sk
             need = max(need, L.pg_gemm_f32_workspace(M_, N_, K_, sk))
         if self.GROUP_WGRAD:
-            # the grouped launches' slabs, sized from the shapes alone (transposed A, plain B);
-            # the side stream's groups (one after another there) have their own
+            # the grouped launches' slabs, sized from the shapes alone (transposed A, plain B)
             self.gws = torch.empty(self._group_ws_bytes(L.pg_gemm_f32_group_workspace), dtype=torch.uint8,
                                    device=dev)
-            self.gws_side = torch.empty(self._group_ws_bytes(L.pg_gemm_f32_group_workspace), dtype=torch.uint8,
-                                        device=dev) if self.SIDE_WGRAD and self.L > 1 else None
         need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C),
                    L.pg_mlp_l1_head_workspace(N, C, pd[-3], pd[-2]))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
@@ -268,7 +258,6 @@ class TrainEngine:
         groups = [order]
         if L > 1:
             groups += [order[:4], order[4:]]
-            groups += [order[4 + 2 * i:6 + 2 * i] for i in range(L - 1)]  # SIDE_WGRAD "layers"
         out = []
         for g in groups:
             out += [g[i:i + MAX_GROUP_PARTS] for i in range(0, len(g), MAX_GROUP_PARTS)]
@@ -544,14 +533,13 @@ class TrainEngine:
         if self.REDUCE_INLINE:  # combine now, while the slabs are still in the caches
             self._reduce_deferred()
 
-    def _reduce_deferred(self, gws: Optional[torch.Tensor] = None) -> None:
-        gws = self.gws if gws is None else gws
+    def _reduce_deferred(self) -> None:
         parts, self._parts = self._parts, []
         for i in range(0, len(parts), MAX_GROUP_PARTS):  # the library's part limit per launch
             chunk = parts[i:i + MAX_GROUP_PARTS]
             arr = (_lib.PgGemmPart * len(chunk))(*[q for q, _ in chunk])
             with self._t("gemm.wgrad.group", sum(w for _, w in chunk)):
-                self._call("pg_gemm_f32_group", arr, len(chunk), ptr(gws), gws.numel(), self._s())
+                self._call("pg_gemm_f32_group", arr, len(chunk), ptr(self.gws), self.gws.numel(), self._s())
         jobs, self._jobs = self._jobs, []
         for i in range(0, len(jobs), 16):
             part = jobs[i:i + 16]
@@ -658,45 +646,16 @@ class TrainEngine:
                 self._gemm(DYP, P[p + "Wstack"], self.DYP[l - 1][:, :Fi], act=LEAKY, dact=HM[:, :Fi],
                            tag=f"gemm.dgrad.stack.l{l + 1}")
         self._reduce_deferred()
-        self._side_join()
         self._bucket_done(len(self.grad_buckets()) - 1)
 
     def _wgrad_bucket_boundary(self, l: int) -> None:
-        """After layer l's weight gradients are issued. dp with two buckets: at the top SAGE
-        layer, run that bucket's grouped launch now, and with RCCL start its all-reduce, which
-        then overlaps the rest of the backward. Single model (SIDE_WGRAD): launch the pending
-        groups on the side stream, beside the lower layers' backward."""
-        if self._split_buckets:
-            if l == self.L - 1 and self.L > 1:
-                self._check_bucket_pending(0)
-                self._reduce_deferred()
-                self._bucket_done(0)
-            return
-        if l > 0 and self._side_ok() and (self.SIDE_WGRAD == "layers" or l == self.L - 1):
-            self._side_launch()
-
-    def _side_ok(self) -> bool:
-        # not while group_times captures one launch group: its timing is the group's own
-        return (bool(self.SIDE_WGRAD) and self.GROUP_WGRAD and self.L > 1 and self._filter is None
-                and getattr(self, "gws_side", None) is not None)
-
-    def _side_launch(self) -> None:
-        """The pending weight gradients as grouped launches on the side stream: they read only
-        this layer's and the MLP's saved activations and gradients (which the rest of the
-        backward does not write) and write only their own gradient blocks, with their own
-        slabs; the step stream joins the side stream before Adam (_side_join)."""
-        main = torch.cuda.current_stream(self.device)
-        if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
-        self._side.wait_stream(main)
-        with torch.cuda.stream(self._side):
-            self._reduce_deferred(self.gws_side)
-        self._side_used = True
-
-    def _side_join(self) -> None:
-        if self._side_used:
-            torch.cuda.current_stream(self.device).wait_stream(self._side)
-            self._side_used = False
+        """After the top SAGE layer's weight gradients are issued (dp with two buckets): run
+        that bucket's grouped launch now, and with RCCL start its all-reduce, which then
+        overlaps the rest of the backward."""
+        if self._split_buckets and l == self.L - 1 and self.L > 1:
+            self._check_bucket_pending(0)
+            self._reduce_deferred()
+            self._bucket_done(0)
 
     def _check_bucket_pending(self, i: int) -> None:
         """Bucket i's all-reduce may start only once every gradient inside its range has been

@@ -19,8 +19,6 @@ Widths are padded to multiples of 8 (16-B rows of bf16) instead of 4.
 """
 from __future__ import annotations
 
-from typing import Optional
-
 import numpy as np
 import torch
 
@@ -134,12 +132,9 @@ class TrainEngineBF16(TrainEngine):
             need = max(need, L.pg_gemm_bf16_workspace(M_, N_, K_, sk))
         self._parts = []
         if self.GROUP_WGRAD:
-            # the grouped weight gradients' slabs: sized from the shapes alone (the side
-            # stream's groups have their own)
+            # the grouped weight gradients' slabs: sized from the shapes alone
             self.gws = torch.empty(self._group_ws_bytes(L.pg_gemm_bf16_group_workspace), dtype=torch.uint8,
                                    device=dev)
-            self.gws_side = torch.empty(self._group_ws_bytes(L.pg_gemm_bf16_group_workspace), dtype=torch.uint8,
-                                        device=dev) if self.SIDE_WGRAD and self.L > 1 else None
         # the fused head (pg_mlp_head, run by forward()) and the standalone loss kernel
         need = max(need, L.pg_sigmoid_multi_loss_workspace(N, C), L.pg_mlp_head_workspace(N, C))
         self.ws = torch.zeros(max(int(need), 256), dtype=torch.uint8, device=dev)
@@ -228,20 +223,17 @@ class TrainEngineBF16(TrainEngine):
                     self._gemm(DYP, W[p + "Wstack"], self.DYP[l - 1][:, :Fi], act=LEAKY, dact=HM[:, :Fi],
                                tag=f"gemm.dgrad.stack.l{l + 1}")
         self._reduce_deferred()
-        self._side_join()
         self._bucket_done(len(self.grad_buckets()) - 1)
 
-    def _reduce_deferred(self, gws: Optional[torch.Tensor] = None) -> None:
-        """The pending weight gradients as one grouped split-K launch + one combine
-        (pg_gemm_bf16_group): they only feed Adam, so they wait for their layer's backward
-        (on the side stream, SIDE_WGRAD) or for the backward's end."""
-        gws = self.gws if gws is None else gws
+    def _reduce_deferred(self) -> None:
+        """Every weight gradient of the step as one grouped split-K launch + one combine
+        (pg_gemm_bf16_group): they only feed Adam, so they all wait for the backward's end."""
         parts, self._parts = self._parts, []
         for i in range(0, len(parts), MAX_GROUP_PARTS):  # the library's part limit per launch
             chunk = parts[i:i + MAX_GROUP_PARTS]
             arr = (_lib.PgGemmPart * len(chunk))(*[q for q, _ in chunk])
             with self._t("gemm.wgrad.group", sum(w for _, w in chunk)):
-                self._call("pg_gemm_bf16_group", arr, len(chunk), ptr(gws), gws.numel(), self._s())
+                self._call("pg_gemm_bf16_group", arr, len(chunk), ptr(self.gws), self.gws.numel(), self._s())
 
     def adam(self) -> None:
         super().adam()

@@ -123,45 +123,6 @@ def test_engine_graph_replay_equals_eager(trans):
     assert a.losses() == b.losses()
 
 
-@pytest.mark.parametrize("mode", ["top", "layers"])
-def test_side_stream_weight_gradients_bitwise(mode):
-    """SIDE_WGRAD: the upper layers' grouped weight gradients run on a second stream beside
-    the lower layers' backward. Against the same groups issued on the step's own stream (no
-    overlap), at full size (cfg2: long enough launches to overlap for real): the gradients of
-    one eager forward + backward, then three captured steps (graph replay), bit for bit."""
-    import plagnn
-    from plagnn import workload as W
-
-    wl = W.build("cfg2", device="cuda")
-
-    class OneStream(plagnn.TrainEngine):
-        SIDE_WGRAD = mode
-
-        def _side_launch(self):  # the same groups, in stream order
-            self._reduce_deferred(self.gws_side)
-
-    engs = []
-    for cls in (type("E", (plagnn.TrainEngine,), {"SIDE_WGRAD": mode}), OneStream):
-        engs.append(cls(wl.graph(), torch.from_numpy(wl.ds.feat), torch.from_numpy(wl.ds.loc.astype(np.float32)),
-                        wl.dims, wl.class_weight, wl.train_index, wl.val_index, device="cuda", seed=0))
-    for e in engs:
-        e.forward()
-        e.backward()
-    torch.cuda.synchronize()
-    assert engs[0]._side is not None and engs[1]._side is None
-    ga, gb = engs[0].grads(), engs[1].grads()
-    for k in gb:
-        assert torch.equal(ga[k], gb[k]), f"grad {k}: side stream != one stream"
-    for e in engs:
-        e.adam()
-        e.capture(warmup=1)
-        for _ in range(3):
-            e.step()
-    torch.cuda.synchronize()
-    assert torch.equal(engs[0].flat, engs[1].flat)
-    assert engs[0].losses() == engs[1].losses()
-
-
 def test_full_size_s0_properties():
     """BASELINE size (N = 24,041, E' ~ 1.23 M): size-independent properties of the max
     aggregation — every output equals its argmax source's value, that source is an
