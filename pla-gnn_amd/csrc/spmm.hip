@@ -21,11 +21,17 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <type_traits>
 
 #include "common.hpp"
 #include "x3_split.hpp"
 
 namespace {
+
+// global agent-scope words (split-row tickets) and the buffer builtins' vector types
+typedef __attribute__((address_space(1))) uint32_t pg_gu32;
+typedef uint32_t pg_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t pg_u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
@@ -164,21 +170,39 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int W, int NC, bool HAS_W, typename A, typename T = float>
+// In-launch combine of split rows for the whole-row forward (MERGE; replaces
+// max_merge_kernel's launch), the max backward's hand-off (max_bwd_pull_kernel): every piece
+// stores its partial maxima and positions write-through (sc1), drains them and draws a
+// ticket from its (row, feature tile) counter (zeroed by a clear launch ahead); the piece
+// that draws the last ticket reads the row's slots with sc1 loads and takes the maximum in
+// slot order with strict > (the earliest maximal edge wins, as in max_merge_kernel).
+struct FwdMerge {
+  int chunk;            // the schedule's chunk
+  uint32_t* tickets;    // [n_slots x n_ftiles]
+  uint32_t val_bytes;   // the slot regions (< 2 GiB each, checked on the host)
+  uint32_t arg_bytes;
+};
+
+template <int W, int NC, bool HAS_W, typename A, typename T = float, bool MERGE = false>
 __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
     const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
     const int32_t* __restrict__ eslot, const float* __restrict__ ew,
     const int4* __restrict__ items, int n_items, const T* __restrict__ X, int64_t ldx, int F,
     T* __restrict__ out, int64_t ldo, A* __restrict__ arg, int64_t lda,
-    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, int n_ftiles, int ftile, int dead_none) {
+    float* __restrict__ ws_val, A* __restrict__ ws_arg, int64_t ldw, int n_ftiles, int ftile, int dead_none,
+    FwdMerge fm = {}) {
   constexpr int U = EdgeU<W, NC>::value;
+  float* const val_base = ws_val;
+  A* const arg_base = ws_arg;
+  int ft = 0, f0 = 0;
   // n_ftiles > 1: all feature tiles of F in one launch, block b -> (item block b / n_ftiles,
   // tile b % n_ftiles), so every tile's longest items start first
   int bx = blockIdx.x;
   if (n_ftiles > 1) {
     const int t = bx % n_ftiles;
+    ft = t;
     bx /= n_ftiles;
-    const int f0 = t * ftile;
+    f0 = t * ftile;
     X += f0;
     out += f0;
     arg += f0;
@@ -261,6 +285,85 @@ __global__ __launch_bounds__(kBlock) void max_fwd_kernel(
       const int f = (c * kWave + lane) * W;
       store_tile<W, T>(orow, f, F, best[c]);
       store_arg<W, A>(arow, f, F, bpos[c]);
+    }
+  } else if constexpr (MERGE && W == 4) {
+    const __amdgpu_buffer_rsrc_t rv = pg_x3::rsrc(val_base, fm.val_bytes);
+    const __amdgpu_buffer_rsrc_t ra = pg_x3::rsrc(arg_base, fm.arg_bytes);
+    auto voff = [&](int sl, int f) { return ((uint32_t)sl * (uint32_t)ldw + (uint32_t)(f0 + f)) * 4u; };
+    auto aoff = [&](int sl, int f) { return ((uint32_t)sl * (uint32_t)ldw + (uint32_t)(f0 + f)) * (uint32_t)sizeof(A); };
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int f = (c * kWave + lane) * W;
+      if (f < F) {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(pg_u32x4, make_float4(best[c][0], best[c][1], best[c][2], best[c][3])), rv,
+            voff(slot, f), 0, 16);
+        if constexpr (sizeof(A) == 2) {
+          const pg_u32x2 a2 = {(uint32_t)(bpos[c][0] & 0xFFFF) | ((uint32_t)bpos[c][1] << 16),
+                               (uint32_t)(bpos[c][2] & 0xFFFF) | ((uint32_t)bpos[c][3] << 16)};
+          __builtin_amdgcn_raw_buffer_store_b64(a2, ra, aoff(slot, f), 0, 16);
+        } else {
+          const pg_u32x4 a4 = {(uint32_t)bpos[c][0], (uint32_t)bpos[c][1], (uint32_t)bpos[c][2], (uint32_t)bpos[c][3]};
+          __builtin_amdgcn_raw_buffer_store_b128(a4, ra, aoff(slot, f), 0, 16);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every payload store drained before the ticket
+    const int re = ptr[row + 1];
+    const int s0 = slot - (k0 - rs) / fm.chunk;
+    const int ns = (re - rs + fm.chunk - 1) / fm.chunk;
+    uint32_t ticket = 0;
+    if (lane == 0)
+      ticket = __hip_atomic_fetch_add((pg_gu32*)(fm.tickets + (int64_t)s0 * n_ftiles + ft), 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __builtin_amdgcn_readfirstlane(ticket);
+    if ((int)ticket != ns - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the ticket
+    T* orow = out + (int64_t)row * ldo;
+    A* arow = arg + (int64_t)row * lda;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int f = (c * kWave + lane) * W;
+      float bv[4] = {ninf, ninf, ninf, ninf};
+      int bp[4] = {arg_none<A>(), arg_none<A>(), arg_none<A>(), arg_none<A>()};
+      // 4 slots in flight, positions kept packed: the tail stays inside the main loop's
+      // registers (8 slots and unpacked positions took the kernel from 46 to 68 VGPRs and
+      // one wave per SIMD less for every item)
+      constexpr int kS = 4;
+      using AV = std::conditional_t<sizeof(A) == 2, pg_u32x2, pg_u32x4>;
+      for (int sb = s0; sb < s0 + ns; sb += kS) {
+        float4 v[kS];
+        AV a[kS];
+#pragma unroll
+        for (int e = 0; e < kS; ++e) {
+          const int sl = min(sb + e, s0 + ns - 1);
+          v[e] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rv, voff(sl, f), 0, 16));
+          if constexpr (sizeof(A) == 2) a[e] = __builtin_amdgcn_raw_buffer_load_b64(ra, aoff(sl, f), 0, 16);
+          else a[e] = __builtin_amdgcn_raw_buffer_load_b128(ra, aoff(sl, f), 0, 16);
+        }
+#pragma unroll
+        for (int e = 0; e < kS; ++e)
+          if (sb + e < s0 + ns) {
+            const float ve[4] = {v[e].x, v[e].y, v[e].z, v[e].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              int ai;
+              if constexpr (sizeof(A) == 2) ai = (int)((a[e][i >> 1] >> (16 * (i & 1))) & 0xFFFF);
+              else ai = (int)a[e][i];
+              if (ve[i] > bv[i]) {
+                bv[i] = ve[i];
+                bp[i] = ai;
+              }
+            }
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (__builtin_isinf(bv[i])) bv[i] = 0.f;
+        if (dead_none && bv[i] == 0.f) bp[i] = arg_none<A>();
+      }
+      store_tile<4, T>(orow, f, F, bv);
+      store_arg<4, A>(arow, f, F, bp);
     }
   } else {
     float* orow = ws_val + (int64_t)slot * ldw;
@@ -1069,6 +1172,10 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
   }
 }
 
+#ifndef PG_FWD_MERGE
+#define PG_FWD_MERGE 1  // split rows combined inside the whole-row forward (0: the max_merge_kernel launch)
+#endif
+
 #ifndef PG_PULL_MERGE
 #define PG_PULL_MERGE 1  // split rows combined inside the pull (0: the sum_merge_kernel launch)
 #endif
@@ -1101,8 +1208,6 @@ struct PullMerge {
   uint32_t ws_bytes;   // the slot region (< 2 GiB, checked on the host)
 };
 
-typedef __attribute__((address_space(1))) uint32_t pg_gu32;
-typedef uint32_t pg_u32x4 __attribute__((ext_vector_type(4)));
 
 template <typename T, typename R, bool TR, bool MERGE>
 __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
@@ -1493,7 +1598,7 @@ inline TilePlan plan_tiles(int64_t F, std::initializer_list<int64_t> lds,
 template <typename A, typename T>
 int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
                    int64_t ldo, A* arg, int64_t lda, float* ws_val, A* ws_arg, int64_t ldw,
-                   int dead_none, hipStream_t st) {
+                   int dead_none, hipStream_t st, uint32_t* tickets) {
   // argpos rows: u16 x4 = 8 B -> need 8-B alignment only; treat via the same 16-B check on
   // the float operands and an 8-B check on arg.
   TilePlan tp = plan_tiles(F, {ldx, ldo, lda}, {X, out, ws_val});
@@ -1553,14 +1658,31 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
   {
     const int64_t f0 = 0;
     const int Ft = (int)std::min<int64_t>(tp.tile, F);
+    // split rows combined inside the launch (max_merge_kernel's launch otherwise): the vector
+    // path, the schedule's chunk known, slot regions a 32-bit buffer offset covers
+    const size_t vbytes = round_up(g->n_slots * ldw * 4, 256), abytes = round_up(g->n_slots * ldw * (int64_t)sizeof(A), 256);
+    const bool merge_in = PG_FWD_MERGE && tp.vec && g->n_merges > 0 && g->chunk > 0 && tickets &&
+                          vbytes < ((size_t)1 << 31) && abytes < ((size_t)1 << 31);
+    if (merge_in) {  // the tickets start at zero: [n_slots x n_ft] words, a 256-B padded block
+      const int64_t n4 = round_up(g->n_slots * n_ft * 4, 256) / 16;
+      hipLaunchKernelGGL(clear_u4_kernel, dim3((unsigned)std::min<int64_t>(2048, (n4 + kBlock - 1) / kBlock)),
+                         dim3(kBlock), 0, st, reinterpret_cast<uint4*>(tickets), n4);
+    }
+    const FwdMerge fm{g->chunk, tickets, (uint32_t)vbytes, (uint32_t)abytes};
     auto go = [&](auto nc_c, auto w_c, auto hw_c) -> int {
       constexpr int NC = decltype(nc_c)::value;
       constexpr int W = decltype(w_c)::value;
       constexpr bool HW = decltype(hw_c)::value;
-      hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T>), dim3((unsigned)blocks * n_ft), dim3(kBlock), 0, st,
-                         g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
-                         X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, n_ft,
-                         (int)tp.tile, dead_none);
+      if (merge_in)
+        hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T, true>), dim3((unsigned)blocks * n_ft), dim3(kBlock), 0,
+                           st, g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
+                           X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, n_ft,
+                           (int)tp.tile, dead_none, fm);
+      else
+        hipLaunchKernelGGL((max_fwd_kernel<W, NC, HW, A, T, false>), dim3((unsigned)blocks * n_ft), dim3(kBlock), 0,
+                           st, g->ptr, g->col, g->eslot, g->ew, (const int4*)g->items, (int)g->n_items,
+                           X, ldx, n_ft > 1 ? (int)F : Ft, out, ldo, arg, lda, ws_val, ws_arg, ldw, n_ft,
+                           (int)tp.tile, dead_none, fm);
       return PG_OK;
     };
     int rc;
@@ -1574,7 +1696,7 @@ int launch_max_fwd(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out
                  : dispatch_nc_scalar(nc, [&](auto n) { return go(n, std::integral_constant<int, 1>{}, std::false_type{}); });
     }
     if (rc != PG_OK) return pg::set_error(rc, "pg_spmm_max_fwd: unsupported feature tile");
-    if (g->n_merges > 0) {
+    if (g->n_merges > 0 && !merge_in) {
       hipLaunchKernelGGL((max_merge_kernel<A, T>), dim3((unsigned)g->n_merges), dim3(kBlock), 0, st,
                          (const int4*)g->merges, (int)g->n_merges, (int)F, ws_val + f0, ws_arg + f0,
                          ldw, out + f0, ldo, arg + f0, lda, dead_none);
@@ -1640,7 +1762,9 @@ size_t pg_spmm_max_fwd_workspace(const pg_csr_t* g, int64_t F, int arg_kind) {
   const int64_t ldw = ws_ld(F);
   const size_t vals = round_up(g->n_slots * ldw * 4, 256);
   const size_t args = round_up(g->n_slots * ldw * (int64_t)pg::arg_bytes(arg_kind & ~PG_ARG_DEAD_NONE), 256);
-  return vals + args;
+  // the whole-row kernel's split-row tickets: one word per slot and 256-column feature tile
+  const size_t tickets = round_up(g->n_slots * ((F + 255) / 256) * 4, 256);
+  return vals + args + tickets;
 }
 
 }  // extern "C"
@@ -1668,12 +1792,16 @@ int max_fwd_entry(const pg_csr_t* g, const T* X, int64_t ldx, int64_t F, T* out,
   const int64_t ldw = ws_ld(F);
   float* ws_val = need ? (float*)ws : nullptr;
   void* ws_arg = need ? (char*)ws + round_up(g->n_slots * ldw * 4, 256) : nullptr;
+  // [slot values | slot positions | split-row tickets]
+  uint32_t* tickets = need ? (uint32_t*)((char*)ws_arg + round_up(g->n_slots * ldw * (int64_t)pg::arg_bytes(arg_kind), 256))
+                           : nullptr;
+  if (((uintptr_t)ws & 255) != 0) tickets = nullptr;  // (the in-launch combine wants aligned regions)
   hipStream_t st = (hipStream_t)stream;
   if (arg_kind == PG_ARG_U16)
     return launch_max_fwd<uint16_t, T>(g, X, ldx, F, out, ldo, (uint16_t*)argpos, lda, ws_val,
-                                       (uint16_t*)ws_arg, ldw, dead_none, st);
+                                       (uint16_t*)ws_arg, ldw, dead_none, st, tickets);
   return launch_max_fwd<int32_t, T>(g, X, ldx, F, out, ldo, (int32_t*)argpos, lda, ws_val,
-                                    (int32_t*)ws_arg, ldw, dead_none, st);
+                                    (int32_t*)ws_arg, ldw, dead_none, st, tickets);
 }
 
 }  // namespace

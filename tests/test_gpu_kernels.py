@@ -100,6 +100,40 @@ def test_spmm_max_fwd_ties_across_split_rows(oracle_mod, F, weighted):
     assert np.all(ref[~won] == 0)
 
 
+@pytest.mark.parametrize("F", [300, 1100])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("chunk", [4, 64])
+def test_spmm_max_fwd_whole_row_split_rows_race(oracle_mod, F, weighted, chunk):
+    """The whole-row forward (widths whose slices do not share out over the XCDs) combines
+    split rows inside the launch: with chunk = 4 almost every row is cut into pieces that
+    race for the last ticket. Bit-exact maxima and argmax against the oracle (ties at zero and
+    few distinct values: the earliest maximal edge wins), twice in a row (tickets restart)."""
+    from plagnn import ops
+
+    n = 700
+    src, dst = hub_graph(n, 2000, seed=F + chunk)
+    rng = np.random.default_rng(F + 7)
+    w = rng.choice(np.array([0.5, 1.0, 2.0], np.float32), len(src)) if weighted else None
+    g = _graph(src, dst, n, chunk=chunk)
+    assert g.fwd.n_merges >= (500 if chunk == 4 else 1)
+    og = oracle_mod.OracleGraph(src, dst, n, self_loop=False, edge_weight=w)
+    X = rng.integers(0, 4, (n, F)).astype(np.float32)
+    X[rng.random((n, F)) < 0.3] = 0.0
+    dg = g.on(DEV)
+    ews = dg.edge_weight_slots(None if w is None else torch.from_numpy(w))
+    Xd = torch.from_numpy(X).to(DEV)
+    out, argpos = ops.spmm_max(dg, Xd, ews)
+    out2, argpos2 = ops.spmm_max(dg, Xd, ews)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2) and torch.equal(argpos, argpos2)
+    ref, argx, _ = oracle_mod.spmm_max(og, X, use_weight=weighted)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    got = ops.argpos_to_src(dg, argpos).cpu().numpy()
+    won = got >= 0
+    np.testing.assert_array_equal(got[won], argx[won])
+    assert np.all(ref[~won] == 0)
+
+
 @pytest.mark.parametrize("F", [4, 65, 256, 503])
 @pytest.mark.parametrize("weighted", [False, True])
 @pytest.mark.parametrize("trans", [False, True])
