@@ -162,7 +162,9 @@ int pg_schedule_build(const int32_t* ptr, int64_t n_rows, int32_t chunk, int32_t
  * argpos[v,f] = k - ptr[v] of the winner. Rows with no entries: out = 0, argpos = none.
  * A +-inf result is stored as 0 (DGL's replace_inf_with_zero after a max reduce).
  * Requires X, out 4-byte aligned; the vector path is taken when ldx, ldo, F are
- * multiples of 4 and the base pointers are 16-byte aligned. */
+ * multiples of 4 and the base pointers are 16-byte aligned. Rows the schedule splits are
+ * combined in piece order (the earliest maximal entry wins); with a 256-byte aligned ws
+ * (at least the query's bytes) inside the same launch, else by a second launch. */
 size_t pg_spmm_max_fwd_workspace(const pg_csr_t* g, int64_t F, int arg_kind);
 int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, float* out,
                     int64_t ldo, void* argpos, int64_t lda, int arg_kind, void* ws,
@@ -179,7 +181,9 @@ int pg_spmm_max_fwd(const pg_csr_t* g, const float* X, int64_t ldx, int64_t F, f
  * output, X >= 0): every entry left has X[u,f] * w != 0, hence X[u,f] > 0, so the mask is
  * implied and mask_src is not read (an element no entry reaches is +0 either way). With
  * X < 0 somewhere the result is undefined.
- * Every dx element is written (no zero-fill needed). */
+ * Every dx element is written (no zero-fill needed). A source row the schedule of gt
+ * splits is summed piece by piece (each piece in ascending v from +0) and the pieces in
+ * order from +0, inside the pull's launch for 16-byte rows (F, ldx multiples of 4). */
 size_t pg_spmm_max_bwd_workspace(const pg_csr_t* gt, int64_t F);
 int pg_spmm_max_bwd(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int64_t lda,
                     int arg_kind, const float* dout, int64_t ldd, int64_t F,
