@@ -342,17 +342,6 @@ def _roofline(engine, gt, bf16):
                          peak_is="bf16 MFMA peak / 6 (three-piece f32 split, gemm_x3.hip)",
                          peak_f32_mfma=PEAK_F32_TFLOPS, frac_vs_f32_mfma=round(ach / PEAK_F32_TFLOPS, 4))
             return r
-        if gname == "head" and bf16:
-            # the fused bf16 MLP head (pg_mlp_l1_head_bf16): its MFMA work is small (one bf16
-            # product per block), its bytes are H3 read once and dH3 written once: HBM-bound
-            hb = float(engine.head_bytes_per_step())
-            ach = hb / sec / 1e9
-            return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(ach / PEAK_HBM_GBS, 4), **base, "bytes_per_step": int(hb),
-                    "flops_per_step": int(g["work"]), "tflops": round(g["work"] / sec / 1e12, 2),
-                    "what": "liner1 forward + liner2/sigmoid/multi_loss/dZ/dA4 + liner1 input gradient, one launch "
-                            "(+ the loss reduction); bytes: H3 read, A4 / dA4 / dH3 written, the per-row labels "
-                            "and outputs"}
         if gname == "head":
             # the fused MLP head (pg_mlp_l1_head): liner1's forward and input-gradient products
             # (three-piece MFMA) with the loss in between; its flops against the same ceiling
@@ -680,10 +669,8 @@ def main(argv=None):
     args = ap.parse_args(argv)
     if args.separate_l1_head:
         import plagnn.engine
-        import plagnn.engine_bf16
 
         plagnn.engine.TrainEngine.FUSED_L1_HEAD = False
-        plagnn.engine_bf16.TrainEngineBF16.FUSED_L1_HEAD = False
     if args.separate_adam_prep:
         import plagnn.engine
 

@@ -266,22 +266,6 @@ int pg_mlp_l1_head(const float* H3, int64_t ldh, int64_t n, int32_t F3, const fl
                    float* dz, int64_t lddz, float* dA4, int64_t ldg, float* dH3, int64_t lddh, float slope,
                    float* loss2, void* ws, size_t ws_bytes, float* adam_state, double lr, double beta1,
                    double beta2, pg_stream_t stream);
-/* The same pass for bf16 storage (ABI 13; replaces the bf16 engine's fwd.liner1 GEMM,
- * pg_mlp_head and dgrad.liner1 GEMM): H3 [n][F3], W1 [K1][F3], W1t = W1^T [F3][K1], A4, dA4
- * [n][K1] and dH3 [n][F3] bf16; b1, W2, b2, prob, dz f32, dz_bf16 (optional) the bf16 copy of
- * dz. A4, dA4 and dH3 are rounded to bf16 where the separate launches store them, and both
- * products run pg_gemm_bf16's MFMA steps (16 k, ascending, K padded with zeros to a multiple
- * of 64) with its epilogue arithmetic: every output equals the separate launches' bitwise.
- * F3 % 64 == 0, F3 <= 1024, K1 % 8 == 0, K1 <= 128, C <= 16; H3, W1, W1t, W2 16-B aligned with
- * leading dimensions multiples of 8 (W2: 4). Scratch: pg_mlp_head_workspace(n, C) bytes.
- * adam_state as for pg_mlp_l1_head. */
-int pg_mlp_l1_head_bf16(const void* H3, int64_t ldh, int64_t n, int32_t F3, const void* W1, int64_t ldw1,
-                        const void* W1t, int64_t ldw1t, const float* b1, int32_t K1, void* A4, int64_t lda4,
-                        const float* W2, int64_t ldw, const float* b2, int32_t C, const float* labels, int64_t ldl,
-                        const float* class_w, const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob,
-                        int64_t ldp, float* dz, void* dz_bf16, int64_t lddz, void* dA4, int64_t ldg, void* dH3,
-                        int64_t lddh, float slope, float* loss2, void* ws, size_t ws_bytes, float* adam_state,
-                        double lr, double beta1, double beta2, pg_stream_t stream);
 size_t pg_sigmoid_multi_loss_workspace(int64_t n_index, int32_t C);
 int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C,
                           const float* labels, int64_t ldl, const float* class_w,
@@ -542,8 +526,7 @@ int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-
                          relu' mask is applied, only PG_ARG_DEAD_NONE implies it;
                          9: pg_gemm_f32_group; 10: the in-CSR's epos = transposed
                          indices (transposed max-backward descriptors), pg_gemm_f32_cat;
-                         11: pg_pad2d_group; 12: pg_mlp_l1_head;
-                         13: pg_mlp_l1_head_bf16 */
+                         11: pg_pad2d_group; 12: pg_mlp_l1_head */
 
 #ifdef __cplusplus
 }

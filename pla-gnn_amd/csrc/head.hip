@@ -670,269 +670,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
   }
 }
 
-
-// ---- liner1 + head + liner1's input gradient, fused (bf16 storage) -----------------------
-// The bf16 engine's MLP (cfg5) as one pass over 32-row blocks, as the f32 kernel above but
-// with bf16 operands taken as they are (one v_mfma_f32_32x32x16_bf16 per 32 x 32 x 16 block,
-// no split): the H3 rows are read once, into LDS, for phase 1's A operand and (as their
-// sign bits) phase 3's leaky'; A4, dA4 and dH3 are rounded to bf16 exactly where the
-// separate launches store them (pg_gemm_bf16 + pg_mlp_head + pg_gemm_bf16), and every
-// product runs the same 16-k MFMA steps in the same order over the same zero-padded K
-// (F3 and K1 rounded up to 64, the bf16 GEMM's K tile), with the same epilogue arithmetic:
-// bitwise the separate launches' results. W1 is read as stored ([K1][F3], phase 1's B rows)
-// and as its transposed bf16 copy ([F3][K1], phase 3's B rows), both from L2.
-constexpr int kB1MaxF3 = 1024;  // the sign-bit mask's width
-__host__ __device__ inline int b1_region_bytes(int F3, int K1) {
-  const int S = (K1 + 3) / 4 * 4 + 4, K64 = (K1 + 63) / 64 * 64;
-  const int p1 = kRows * (F3 + 8) * 2;                         // phase 1: H3 [32][F3 + 8] bf16
-  const int p23 = kRows * S * 4 + kRows * (K64 + 8) * 2;       // A4 -> dA4 f32 [32][S], dA4 bf16 [32][K64 + 8]
-  return ((p1 > p23 ? p1 : p23) + 15) / 16 * 16;
-}
-
-__device__ __forceinline__ float b1_bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
-__device__ __forceinline__ uint16_t b1_f2bf(float x) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(x)); }
-
-__global__ __launch_bounds__(kBlock) void mlp_l1_head_bf16_kernel(
-    const uint16_t* __restrict__ h3, int64_t ldh, int n, int F3, const uint16_t* __restrict__ w1, int64_t ldw1,
-    const uint16_t* __restrict__ w1t, int64_t ldw1t, const float* __restrict__ b1, int K1,
-    uint16_t* __restrict__ a4g, int64_t lda4, const float* __restrict__ w2, int64_t ldw,
-    const float* __restrict__ b2, int C, const float* __restrict__ labels, int64_t ldl,
-    const float* __restrict__ cw, const int8_t* __restrict__ row_set, float inv_n_train,
-    float* __restrict__ prob, int64_t ldp, float* __restrict__ dz, int64_t lddz, uint16_t* __restrict__ dzb,
-    uint16_t* __restrict__ da4g, int64_t ldg, uint16_t* __restrict__ dh3, int64_t lddh, float slope,
-    float* __restrict__ part, int nb) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char region[];
-  __shared__ __attribute__((aligned(16))) float w[kMaxC * (kMaxK + 4)];
-  __shared__ float g[kRows][kMaxC];
-  __shared__ float terms[2][kRows][kMaxC];
-  __shared__ uint32_t pos[kRows][kB1MaxF3 / 32];  // H3 > 0, one bit per element
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int K4 = (K1 + 3) / 4 * 4, S = K4 + 4, K64 = (K1 + 63) / 64 * 64, SD = K64 + 8, SH = F3 + 8;
-  uint16_t* sh = reinterpret_cast<uint16_t*>(region);                  // phase 1: H3 [32][SH]
-  float* a = reinterpret_cast<float*>(region);                         // phase 2: A4 -> dA4 [32][S]
-  uint16_t* sd = reinterpret_cast<uint16_t*>(region + kRows * S * 4);  // phase 3: dA4 [32][SD]
-  const int r0 = blockIdx.x * kRows;
-  const int nr = min(kRows, n - r0);
-
-  // H3's rows into LDS (16-B units, rows past n clamped: never stored), 8 units per thread
-  // in flight (F3 = 512: all of them)
-  const int upr = F3 / 8, nu = kRows * upr;
-  for (int q0 = 0; q0 < nu; q0 += 8 * kBlock) {
-    uint4 hv[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int u = min(q0 + tid + q * kBlock, nu - 1);
-      const int row = u / upr, k8 = u - row * upr;
-      hv[q] = *reinterpret_cast<const uint4*>(h3 + (int64_t)min(r0 + row, n - 1) * ldh + 8 * k8);
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int u = q0 + tid + q * kBlock;
-      if (u < nu) {
-        const int row = u / upr, k8 = u - row * upr;
-        *reinterpret_cast<uint4*>(sh + row * SH + 8 * k8) = hv[q];
-      }
-    }
-  }
-  // W2 into LDS (the head's operand)
-  {
-    const int uw = C * (K4 / 4);
-    for (int u = tid; u < uw; u += kBlock) {
-      const int c = u / (K4 / 4), k = (u - c * (K4 / 4)) * 4;
-      *reinterpret_cast<float4*>(w + c * S + k) = ld4(w2, (int64_t)c * ldw, k, K1);
-    }
-  }
-  for (int i = tid; i < 2 * kRows * kMaxC; i += kBlock) (&terms[0][0][0])[i] = 0.f;
-  constexpr int kHH = kRows / (kBlock / kMaxC);
-  int hset[kHH];
-  float hlab[kHH];
-  const int hc = min(tid % kMaxC, C - 1);
-  const float hwc = cw[2 * hc], hwp1 = cw[2 * hc + 1], hb2 = b2[hc];
-#pragma unroll
-  for (int hh = 0; hh < kHH; ++hh) {
-    const int64_t r = min(r0 + tid / kMaxC + hh * (kBlock / kMaxC), n - 1);
-    hset[hh] = row_set[r];
-    hlab[hh] = labels[r * ldl + hc];
-  }
-  __syncthreads();
-  // leaky'(H3) for phase 3: the sign bits (H3 > 0) of every element
-  for (int u = tid; u < kRows * (F3 / 32); u += kBlock) {
-    const int row = u / (F3 / 32), wd = u - row * (F3 / 32);
-    uint32_t m = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint4 x = *reinterpret_cast<const uint4*>(sh + row * SH + 32 * wd + 8 * q);
-      const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        m |= (uint32_t)(b1_bf2f((uint16_t)(xs[e] & 0xFFFF)) > 0.f) << (8 * q + 2 * e);
-        m |= (uint32_t)(b1_bf2f((uint16_t)(xs[e] >> 16)) > 0.f) << (8 * q + 2 * e + 1);
-      }
-    }
-    pos[row][wd] = m;
-  }
-
-  // ---- phase 1: A4 = bf16(leaky(H3 W1^T + b1)) ----
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int n1 = 32 * wave + l32;  // this lane's A4 column (W1 row)
-  const bool live1 = n1 < K1;
-  const uint16_t* w1r = w1 + (int64_t)min(n1, K1 - 1) * ldw1 + 8 * h;
-  const int steps1 = F3 / 16;
-  constexpr int kPD = 8;  // W1 fragments in flight (K steps ahead)
-  bf16x8 bq[kPD];
-  auto ldw1f = [&](int s) {
-    const uint4 x = *reinterpret_cast<const uint4*>(w1r + 16 * min(s, steps1 - 1));
-    return __builtin_bit_cast(bf16x8, live1 ? x : make_uint4(0u, 0u, 0u, 0u));
-  };
-#pragma unroll
-  for (int i = 0; i < kPD; ++i) bq[i] = ldw1f(i);
-#pragma nounroll
-  for (int s0 = 0; s0 < steps1; s0 += kPD) {
-#pragma unroll
-    for (int i = 0; i < kPD; ++i) {
-      const int s = s0 + i;
-      if (s < steps1) {
-        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(sh + l32 * SH + 16 * s + 8 * h);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, bq[i], acc, 0, 0, 0);
-      }
-      bq[i] = ldw1f(s + kPD);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  __syncthreads();  // every wave past its H3 reads: the region becomes A4 / dA4
-  // epilogue (as pg_gemm_bf16's: 1 * acc, + bias, leaky, bf16): A4 out, and to LDS as f32
-  {
-    const float bb = live1 ? b1[n1] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      float o = 1.f * acc[r];
-      o = o + bb;
-      o = o > 0.f ? o : o * slope;
-      const uint16_t ob = b1_f2bf(o);
-      if (n1 < K4) a[row * S + n1] = live1 ? b1_bf2f(ob) : 0.f;
-      if (live1 && row < nr) a4g[(int64_t)(r0 + row) * lda4 + n1] = ob;
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 2: the head (head_kernel<bf16>'s arithmetic, A4 from LDS) ----
-  {
-    const int c = tid % kMaxC, rg = tid / kMaxC;
-#pragma unroll
-    for (int hh = 0; hh < kHH; ++hh) {
-      const int ri = rg + hh * (kBlock / kMaxC);
-      if (c < C && ri < nr) {
-        const int64_t r = r0 + ri;
-        const int set = hset[hh];
-        const float t = hlab[hh];
-        const float4* ar = reinterpret_cast<const float4*>(a + ri * S);
-        const float4* wr = reinterpret_cast<const float4*>(w + c * S);
-        float zz = 0.f;
-        for (int k4 = 0; k4 < K4 / 4; ++k4) {
-          const float4 x = ar[k4], y = wr[k4];
-          zz = fmaf(x.x, y.x, zz);
-          zz = fmaf(x.y, y.y, zz);
-          zz = fmaf(x.z, y.z, zz);
-          zz = fmaf(x.w, y.w, zz);
-        }
-        zz = zz + hb2;
-        const float pr = 1.f / (1.f + expf(-zz));
-        if (prob) prob[r * ldp + c] = pr;
-        float gz = 0.f;
-        if (set != 0) {
-          const float wc = hwc;
-          const float wp1 = hwp1;
-          const float cp = fminf(fmaxf(pr, 1e-9f), 10.f);
-          const float q = 1.f - pr;
-          const float cq = fminf(fmaxf(q, 1e-9f), 10.f);
-          const float la = logf(cp), lb = logf(cq);
-          terms[set - 1][ri][c] = ((t * la) * wc + (1.f - t) * lb) / wp1 * 2.f;
-          if (set == 1) {
-            float gg = -inv_n_train;
-            gg = gg * 2.f;
-            gg = gg / wp1;
-            float ga = (gg * wc) * t;
-            ga = ga / cp;
-            if (!(pr >= 1e-9f && pr <= 10.f)) ga = 0.f;
-            float gb = gg * (1.f - t);
-            gb = gb / cq;
-            if (!(q >= 1e-9f && q <= 10.f)) gb = 0.f;
-            const float dp = ga + (-gb);
-            gz = (dp * (1.f - pr)) * pr;
-          }
-        }
-        g[ri][c] = gz;
-        if (dz) dz[r * lddz + c] = gz;
-        if (dzb) dzb[r * lddz + c] = b1_f2bf(gz);
-      } else {
-        g[ri][c] = 0.f;
-      }
-    }
-  }
-  __syncthreads();
-  if (tid < 2 * C) {
-    const int set = tid / C, c = tid % C;
-    float s = 0.f;
-    for (int ri = 0; ri < nr; ++ri) s += terms[set][ri][c];
-    part[((int64_t)set * C + c) * nb + blockIdx.x] = s;
-  }
-  // dA4 = bf16((dz W2) * leaky'(A4)): out, and as phase 3's A operand (zero past K1 up to K64)
-  {
-    const int j = tid % kMaxK, r2 = tid / kMaxK;
-    if (j < K64) {
-      float wj[kMaxC];
-#pragma unroll
-      for (int c = 0; c < kMaxC; ++c) wj[c] = c < C && j < K1 ? w[c * S + j] : 0.f;
-      for (int ri = r2; ri < kRows; ri += kBlock / kMaxK) {
-        float s = 0.f;
-#pragma unroll
-        for (int c = 0; c < kMaxC; ++c) s = fmaf(g[ri][c], wj[c], s);
-        const float y = j < K4 ? a[ri * S + j] : 0.f;
-        const uint16_t db = b1_f2bf(y > 0.f ? s : s * slope);
-        sd[ri * SD + j] = j < K1 ? db : (uint16_t)0;
-        if (j < K1 && ri < nr) da4g[(int64_t)(r0 + ri) * ldg + j] = db;
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 3: dH3 = bf16((dA4 W1) * leaky'(H3)), one 32-column tile per wave and pass ----
-  const int steps3 = K64 / 16;
-  for (int c0 = 32 * wave; c0 < F3; c0 += 128) {
-    const int col = c0 + l32;
-    // W1^T row col at k = 16 s + 8 h (zero from K1 on; the loads unconditional, at clamped k)
-    const uint16_t* wtr = w1t + (int64_t)min(col, F3 - 1) * ldw1t;
-    bf16x8 bv[kL1K1 / 16];
-#pragma unroll
-    for (int s = 0; s < kL1K1 / 16; ++s) {
-      const int k = 16 * s + 8 * h;
-      const uint4 x = *reinterpret_cast<const uint4*>(wtr + min(k, K1 - 8));
-      bv[s] = __builtin_bit_cast(bf16x8, k < K1 ? x : make_uint4(0u, 0u, 0u, 0u));
-    }
-    f32x16 acc3;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc3[r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < kL1K1 / 16; ++s) {
-      if (s < steps3) {
-        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(sd + l32 * SD + 16 * s + 8 * h);
-        acc3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, bv[s], acc3, 0, 0, 0);
-      }
-    }
-    // epilogue (pg_gemm_bf16's EPI_DLEAKY: 1 * acc, y > 0 ? x : x slope, bf16)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float o = 1.f * acc3[r];
-      const bool pz = col < F3 && ((pos[row][col >> 5] >> (col & 31)) & 1u);
-      if (row < nr && col < F3) dh3[(int64_t)(r0 + row) * lddh + col] = b1_f2bf(pz ? o : o * slope);
-    }
-  }
-}
-
 }  // namespace
 
 extern "C" {
@@ -1027,43 +764,6 @@ int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const fl
                      n_val, loss2, adam_state, lr, beta1, beta2);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pg::set_error((int)e, "pg_mlp_l1_head: launch failed: %s", hipGetErrorString(e));
-  return pg::ok();
-}
-
-int pg_mlp_l1_head_bf16(const void* h3, int64_t ldh, int64_t n, int32_t F3, const void* w1, int64_t ldw1,
-                        const void* w1t, int64_t ldw1t, const float* b1, int32_t K1, void* a4, int64_t lda4,
-                        const float* w2, int64_t ldw, const float* b2, int32_t C, const float* labels, int64_t ldl,
-                        const float* class_w, const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob,
-                        int64_t ldp, float* dz, void* dz_bf16, int64_t lddz, void* da4, int64_t ldg, void* dh3,
-                        int64_t lddh, float slope, float* loss2, void* ws, size_t ws_bytes, float* adam_state,
-                        double lr, double beta1, double beta2, pg_stream_t stream) {
-  if (n < 0 || n > INT32_MAX || F3 <= 0 || F3 % 64 != 0 || F3 > kB1MaxF3 || K1 <= 0 || K1 % 8 != 0 || K1 > kL1K1 ||
-      K1 > kMaxK || C <= 0 || C > kMaxC || ldh < F3 || ldw1 < F3 || ldw1t < K1 || lda4 < K1 || ldw < K1 || ldl < C ||
-      (prob && ldp < C) || ((dz || dz_bf16) && lddz < C) || ldg < K1 || lddh < F3)
-    return pg::set_error(PG_ERR_INVALID,
-                         "pg_mlp_l1_head_bf16: bad shape (F3 %% 64 == 0, F3 <= %d, K1 %% 8 == 0, K1 <= %d, C <= %d)",
-                         kB1MaxF3, kL1K1, kMaxC);
-  if (n == 0) return pg::ok();
-  if (!h3 || !w1 || !w1t || !b1 || !a4 || !w2 || !b2 || !labels || !class_w || !row_set || !da4 || !dh3 || !loss2 ||
-      !ws)
-    return pg::set_error(PG_ERR_INVALID, "pg_mlp_l1_head_bf16: NULL buffer");
-  if (((uintptr_t)h3 & 15) || (ldh & 7) || ((uintptr_t)w1 & 15) || (ldw1 & 7) || ((uintptr_t)w1t & 15) ||
-      (ldw1t & 7) || ((uintptr_t)w2 & 15) || (ldw & 3))
-    return pg::set_error(PG_ERR_INVALID, "pg_mlp_l1_head_bf16: H3, W1, W1^T, W2 need 16-B aligned rows");
-  if (ws_bytes < pg_mlp_head_workspace(n, C))
-    return pg::set_error(PG_ERR_WORKSPACE, "pg_mlp_l1_head_bf16: workspace too small");
-  hipStream_t st = (hipStream_t)stream;
-  const int nb = (int)((n + kRows - 1) / kRows);
-  float* part = (float*)ws;
-  const float inv_n = n_train > 0 ? 1.0f / (float)n_train : 0.f;
-  hipLaunchKernelGGL(mlp_l1_head_bf16_kernel, dim3(nb), dim3(kBlock), (unsigned)b1_region_bytes(F3, K1), st,
-                     (const uint16_t*)h3, ldh, (int)n, (int)F3, (const uint16_t*)w1, ldw1, (const uint16_t*)w1t, ldw1t,
-                     b1, (int)K1, (uint16_t*)a4, lda4, w2, ldw, b2, (int)C, labels, ldl, class_w, row_set, inv_n, prob,
-                     ldp, dz, lddz, (uint16_t*)dz_bf16, (uint16_t*)da4, ldg, (uint16_t*)dh3, lddh, slope, part, nb);
-  hipLaunchKernelGGL(head_final_kernel, dim3(2), dim3(64 * kMaxC), 0, st, (const float*)part, nb, (int)C, n_train,
-                     n_val, loss2, adam_state, lr, beta1, beta2);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return pg::set_error((int)e, "pg_mlp_l1_head_bf16: launch failed: %s", hipGetErrorString(e));
   return pg::ok();
 }
 

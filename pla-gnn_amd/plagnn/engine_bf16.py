@@ -35,9 +35,7 @@ class TrainEngineBF16(TrainEngine):
     # the stacked input-gradient weights as [Fi][Fo + Fi] (B^T, a row image: the A B^T
     # ping-pong kernel of pg_gemm_bf16 takes the product) instead of [Fo + Fi][Fi] (a k image)
     STACK_T = True
-    # liner1's forward, the head and liner1's input gradient as one launch
-    # (pg_mlp_l1_head_bf16: bitwise the separate bf16 GEMMs + pg_mlp_head); False: three
-    # launches (A/B knob)
+    # the fused liner1 + head kernel is f32 only: bf16 storage keeps liner1 as bf16 GEMMs
     FUSED_L1_HEAD = False
 
     # ------------------------------------------------------------------ buffers
@@ -76,7 +74,6 @@ class TrainEngineBF16(TrainEngine):
             else:
                 wl.add(f"conv{l + 1}.Wstack", (Fo + Fi, Fi))  # [Wself ; Wpool]
         wl.add("liner1.W", (pd[-2], pd[-3]))
-        wl.add("liner1.WT", (pd[-3], pd[-2]))  # W1^T: the fused head's phase-3 operand
         idx = np.full(wl.size, -1, np.int64)
         flat_ids = self.flat_layout.views(torch.arange(self.flat_layout.size))  # flat index of every entry
 
@@ -101,9 +98,7 @@ class TrainEngineBF16(TrainEngine):
                 put(p + "WstackT", np.ascontiguousarray(stack.T))
             else:
                 put(p + "Wstack", stack)
-        w1 = ids("liner1.W", (pd[-2], pd[-3]))
-        put("liner1.W", w1)
-        put("liner1.WT", np.ascontiguousarray(w1.T))
+        put("liner1.W", ids("liner1.W", (pd[-2], pd[-3])))
         self.wb_layout = wl
         self.wb_map = torch.from_numpy(idx.astype(np.int32)).to(self.device)
         self.wb = torch.zeros(wl.size, dtype=torch.bfloat16, device=self.device)
@@ -188,36 +183,10 @@ class TrainEngineBF16(TrainEngine):
             out = self.HM[l + 1][:, :Fo] if l + 1 < self.L else self.A3
             self._gemm(HM, W[p + "Wcat"], out, transb=True, bias=P[p + "b"], act=LEAKY,
                        tag=f"gemm.fwd.cat.l{l + 1}")
-        if self._l1_fused():
-            self._mlp_l1_head()
-            return
         self._gemm(self.A3, W["liner1.W"], self.A4, transb=True, bias=P["liner1.b"], act=LEAKY,
                    tag="gemm.fwd.liner1")
         # liner2 + loss + dZ + dA4 (f32 W2 / b2; bf16 A4, dZ copy and dA4)
         self._head(BF16, self.A4, self.dZ, self.dZb, self.dA4)
-
-    def _l1_fused(self) -> bool:
-        pd = self.pd
-        return self.FUSED_L1_HEAD and pd[-2] <= 128 and pd[-2] % 8 == 0 and pd[-3] % 64 == 0 and pd[-3] <= 1024
-
-    def _mlp_l1_head(self) -> None:
-        """liner1 + liner2 + sigmoid + train/val loss + dZ + dA4 + liner1's input gradient
-        through the top SAGE layer's leaky_relu, bf16 storage, in one launch
-        (pg_mlp_l1_head_bf16; code/model.py:26-29, code/train.py:89-108, 199-207)."""
-        P, W, pd, C = self.P, self.Wb, self.pd, self.C
-        top = self.L - 1
-        dH3 = self.DYP[top][:, :pd[top + 1]]
-        fold = self._fold_prep and self.FOLD_ADAM_PREP
-        self._prepped = fold
-        with self._t("head.l1", 2.0 * 2 * self.N * pd[-3] * pd[-2]):
-            self._call("pg_mlp_l1_head_bf16", ptr(self.A3), self.A3.stride(0), self.N, pd[-3], ptr(W["liner1.W"]),
-                       W["liner1.W"].stride(0), ptr(W["liner1.WT"]), W["liner1.WT"].stride(0), ptr(P["liner1.b"]),
-                       pd[-2], ptr(self.A4), self.A4.stride(0), ptr(P["liner2.W"]), pd[-2], ptr(P["liner2.b"]), C,
-                       ptr(self.labels), pd[-1], ptr(self.cw), ptr(self.row_set), self.n_train, self.n_val,
-                       ptr(self.prob), pd[-1], ptr(self.dZ), ptr(self.dZb), pd[-1], ptr(self.dA4),
-                       self.dA4.stride(0), ptr(dH3), dH3.stride(0), LEAKY_SLOPE, ptr(self.loss), ptr(self.ws),
-                       self.ws_bytes, ptr(self.adam_state) if fold else None, self.lr, self.betas[0],
-                       self.betas[1], self._s())
 
     def backward(self) -> None:
         st = self._s()
@@ -228,9 +197,8 @@ class TrainEngineBF16(TrainEngine):
         self._gemm(self.dZb, self.A4, G["liner2.W"], transa=True, rowsum=G["liner2.b"], tag="gemm.wgrad.liner2")
         self._gemm(self.dA4, self.A3, G["liner1.W"], transa=True, rowsum=G["liner1.b"], tag="gemm.wgrad.liner1")
         top = self.L - 1
-        if not self._l1_fused():  # (fused: the head wrote the top layer's dY already)
-            self._gemm(self.dA4, W["liner1.W"], self.DYP[top][:, :pd[top + 1]], act=LEAKY, dact=self.A3,
-                       tag="gemm.dgrad.liner1")
+        self._gemm(self.dA4, W["liner1.W"], self.DYP[top][:, :pd[top + 1]], act=LEAKY, dact=self.A3,
+                   tag="gemm.dgrad.liner1")
         for l in reversed(range(self.L)):
             p = f"conv{l + 1}."
             Fi, Fo = pd[l], pd[l + 1]
@@ -273,13 +241,6 @@ class TrainEngineBF16(TrainEngine):
             self._cast_weights()
 
     # ------------------------------------------------------------------ accounting
-    def head_bytes_per_step(self) -> int:
-        """Algorithmic bytes of the fused bf16 MLP head (true dims): H3 read and dH3 written
-        (bf16), A4 and dA4 written (bf16), per row the labels read, prob and dZ written (f32)
-        and dZ's bf16 copy."""
-        N, d = self.N, self.dims
-        return 2 * 2 * N * d[-3] + 2 * 2 * N * d[-2] + N * d[-1] * (4 + 4 + 4 + 2)
-
     def spmm_bytes(self, layer: int) -> int:
         """SURVEY.md §8(d) B_fwd with s = 2 (bf16 features): 4(N+1) + 4E' + 2F E' + 2F N + aF N."""
         N, E, F = self.N, self.dg.num_edges, self.dims[layer]

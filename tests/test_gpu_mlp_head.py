@@ -156,97 +156,3 @@ def test_adam_scalars_folded_into_head_equal_separate_prepare():
     torch.cuda.synchronize()
     assert torch.equal(a.adam_state, before)
     assert isinstance(a, plagnn.TrainEngine)
-
-
-def _engine_pair_bf16(dims, n, e, seed):
-    import oracle
-    import plagnn
-
-    src, dst = random_graph(n, e, seed, self_loop=False)
-    rng = np.random.default_rng(seed)
-    x = torch.from_numpy(rng.standard_normal((n, dims[0])).astype(np.float32))
-    labels = torch.from_numpy((rng.random((n, dims[-1])) < 0.3).astype(np.float32))
-    w = oracle.weight_cal(labels.numpy().astype(np.float64))
-    idx = rng.permutation(n)
-    tr, va = idx[: n // 2], idx[n // 2: n // 2 + n // 5]
-    loops = np.arange(n)
-    g = plagnn.CSRGraph(np.concatenate([src, loops]), np.concatenate([dst, loops]), n)
-    from plagnn.model import GNN
-
-    torch.manual_seed(seed)
-    params = GNN(list(dims)).state_dict()
-    out = []
-    for fused in (True, False):
-        cls = type("EB", (plagnn.TrainEngineBF16,), {"FUSED_L1_HEAD": fused})
-        out.append(cls(g, x, labels, dims, w, tr, va, device="cuda", params=params))
-    return out
-
-
-def _run_bf16(eng):
-    r = _run(eng)
-    r["dZb"] = eng.dZb.detach().cpu().clone()
-    return r
-
-
-@pytest.mark.parametrize("dims,n,e", [
-    ((31, 24, 64, 40, 12), 600, 6000),                # F3 = 64: one K tile; K1 = 40
-    ((64, 48, 512, 100, 12), 1000, 12000),            # cfg5's MLP: F3 = 512, K1 = 100 -> 104
-    ((40, 192, 120, 3), 97, 900),                     # K1 = 120, C = 3, a ragged last block
-])
-def test_fused_head_bf16_equals_separate_launches_bitwise(dims, n, e):
-    """bf16 storage: pg_mlp_l1_head_bf16 == the bf16 GEMMs + pg_mlp_head bit for bit (A4, dA4,
-    dZ and its bf16 copy, prob, both losses, the top layer's dY and every gradient)."""
-    fused, sep = _engine_pair_bf16(dims, n, e, seed=len(dims) + n)
-    assert fused._l1_fused() and not sep._l1_fused()
-    a, b = _run_bf16(fused), _run_bf16(sep)
-    for k in b:
-        assert torch.equal(a[k], b[k]), f"{k}: fused != separate (max diff {(a[k].float() - b[k].float()).abs().max().item():.3e})"
-    assert fused.flops_per_step() + fused.head_flops_per_step() == sep.flops_per_step()
-
-
-def test_fused_head_bf16_many_blocks_replay():
-    """50 000 rows (1 563 blocks, cfg5's MLP widths): fused == separate after a forward +
-    backward, and two captured steps replay equal to two eager steps of a twin engine."""
-    dims = (64, 512, 100, 12)
-    fused, sep = _engine_pair_bf16(dims, 50000, 400000, seed=5)
-    a, b = _run_bf16(fused), _run_bf16(sep)
-    for k in b:
-        assert torch.equal(a[k], b[k]), f"{k}: fused != separate"
-    fused.adam()
-    st = fused.state_dict()
-    e1 = _engine_pair_bf16(dims, 50000, 400000, seed=5)[0]
-    e1.load_state_dict(st)
-    e1.m.copy_(fused.m)
-    e1.v.copy_(fused.v)
-    e1.adam_state.copy_(fused.adam_state)
-    fused.capture(warmup=0)
-    for _ in range(2):
-        fused.step()
-        e1.step_eager()
-    torch.cuda.synchronize()
-    assert torch.equal(fused.flat, e1.flat)
-    assert fused.losses() == e1.losses()
-
-
-def test_mlp_l1_head_bf16_rejects_bad_shapes():
-    from plagnn import _lib
-
-    L = _lib.lib()
-    ws = torch.zeros(int(L.pg_mlp_head_workspace(64, 12)), dtype=torch.uint8, device="cuda")
-    inp = torch.zeros(512, 512, dtype=torch.bfloat16, device="cuda")
-    f32 = torch.zeros(512, 512, device="cuda")
-    outs = [torch.zeros(64, 512, dtype=torch.bfloat16, device="cuda") for _ in range(3)]  # A4, dA4, dH3
-    loss = torch.zeros(2, device="cuda")
-    rs = torch.zeros(64, dtype=torch.int8, device="cuda")
-    p, q = inp.data_ptr(), f32.data_ptr()
-
-    def args(F3, K1, C):
-        return (p, 512, 64, F3, p, 512, p, 512, q, K1, outs[0].data_ptr(), 512, q, 512, q, C, q, 512, q,
-                rs.data_ptr(), 0, 0, None, 0, None, None, 0, outs[1].data_ptr(), 512, outs[2].data_ptr(), 512, 0.01,
-                loss.data_ptr(), ws.data_ptr(), ws.numel(), None, 0.0, 0.0, 0.0, None)
-
-    assert L.pg_mlp_l1_head_bf16(*args(512, 104, 12)) == 0
-    torch.cuda.synchronize()
-    assert not outs[0].float().any() and not outs[2].float().any()
-    for bad in ((500, 104, 12), (512, 100, 12), (512, 136, 12), (512, 104, 17), (2048, 104, 12)):
-        assert L.pg_mlp_l1_head_bf16(*args(*bad)) != 0, bad
