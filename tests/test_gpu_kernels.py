@@ -239,6 +239,38 @@ def test_spmm_max_bwd_split_rows_bitexact(oracle_mod, F, weighted, chunk_bwd, tr
     np.testing.assert_array_equal(dXm, np.where(X > 0, ref, 0.0))
 
 
+@pytest.mark.parametrize("F", [64, 256, 504])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("chunk_bwd", [4, 64])
+def test_spmm_max_bwd_bf16_split_rows_bitexact(F, weighted, chunk_bwd):
+    """bf16 storage (cfg5's records: 4-B {bf16 dout, f} unweighted, 8-B {w * dout, f}
+    weighted): every row bit-exact against the schedule's piecewise f32 sums of the bf16
+    upstream gradient, rounded once to bf16 at the end."""
+    import plagnn
+    from plagnn import ops
+
+    n = 700
+    src, dst = hub_graph(n, 1500, seed=F + chunk_bwd + 1)
+    rng = np.random.default_rng(F + 11)
+    w = rng.uniform(-1, 2, len(src)).astype(np.float32) if weighted else None
+    g = plagnn.CSRGraph(src, dst, n, chunk=256, chunk_bwd=chunk_bwd)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    X[rng.random((n, F)) < 0.4] = 0.0
+    Xb = torch.from_numpy(X).to(DEV).to(torch.bfloat16)
+    dZb = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(DEV).to(torch.bfloat16)
+    dg = g.on(DEV)
+    ews = dg.edge_weight_slots(None if w is None else torch.from_numpy(w))
+    out, argpos = ops.spmm_max(dg, Xb, ews)
+    dX = ops.spmm_max_backward(dg, argpos, dZb, ews)
+    dX2 = ops.spmm_max_backward(dg, argpos, dZb, ews)
+    torch.cuda.synchronize()
+    assert dX.dtype == torch.bfloat16 and torch.equal(dX, dX2)
+    ref = _piecewise_max_bwd(g, argpos.cpu().numpy(), dZb.float().cpu().numpy(),
+                             None if ews is None else ews.cpu().numpy())
+    np.testing.assert_array_equal(dX.float().cpu().numpy(),
+                                  torch.from_numpy(ref).to(torch.bfloat16).float().numpy())
+
+
 def test_spmm_max_int32_positions(oracle_mod):
     """A row of >= 65535 entries forces int32 argmax positions."""
     from plagnn import _lib, ops
