@@ -161,13 +161,6 @@ struct EdgeU {
   static constexpr int value = (NC * W <= 8) ? PG_EDGE_U : 4;
 };
 
-#ifndef PG_PACK_PERSIST
-#define PG_PACK_PERSIST 0  // vector pack: short rows dealt over a capped grid, next row prefetched
-#endif
-#ifndef PG_PACK_BLOCKS
-#define PG_PACK_BLOCKS 2048  // the capped grid's short-row workgroups (4 waves each)
-#endif
-
 // ---- max forward ---------------------------------------------------------------------
 constexpr int kPackWaveMax = 256;  // longest row grouped by one wave (forward chunk)
 
@@ -911,64 +904,28 @@ __device__ __forceinline__ void pack_short_row(
 template <int NV>
 constexpr int pack_wave_ints() { return kPackWaveMax + 4 + NV * 512; }  // hist | records (8 B)
 
-// One row's pack inputs as loaded (packed: 4 positions and 4 gradients per lane and chunk),
-// so a wave can hold the next row's in flight while it packs this one.
-template <int NV, typename A, typename T>
-struct PackRaw {
-  using AV = std::conditional_t<sizeof(A) == 2, uint2, int4>;
-  using TV = std::conditional_t<sizeof(T) == 2, uint2, float4>;
-  int rs, re;
-  AV a[NV];
-  TV d[NV];
-};
-
-// straight-line loads at clamped columns (F % 4 == 0 here), masked when unpacked: no branch
-// between the record and gradient loads, so both are in flight before the first wait
-template <int NV, typename A, typename T>
-__device__ __forceinline__ void pack_load(PackRaw<NV, A, T>& r, int v, const int32_t* __restrict__ ptr,
-                                          const A* __restrict__ arg, int64_t lda, int F,
-                                          const T* __restrict__ dout, int64_t ldd) {
-  using AV = typename PackRaw<NV, A, T>::AV;
-  using TV = typename PackRaw<NV, A, T>::TV;
-  r.rs = ptr[v];
-  r.re = ptr[v + 1];
-  const int lane = lane_id();
-#pragma unroll
-  for (int c = 0; c < NV; ++c) {
-    const int fc = min((c * kWave + lane) * 4, F - 4);
-    r.a[c] = *reinterpret_cast<const AV*>(arg + (int64_t)v * lda + fc);
-    r.d[c] = *reinterpret_cast<const TV*>(dout + (int64_t)v * ldd + fc);
-  }
-}
-
 template <int NV, typename A, typename T, typename R, typename D>
 __device__ __forceinline__ void pack_short_row_v(
-    int v, const PackRaw<NV, A, T>& raw, int wave,
+    int v, int wave, const int32_t* __restrict__ ptr,
     const A* __restrict__ arg, int64_t lda, int F, const T* __restrict__ dout, int64_t ldd,
     const T* __restrict__ fout, int64_t ldf, const float* __restrict__ ew, R gp, D dsc,
     int* __restrict__ lds) {
   const int lane = lane_id();
-  const int rs = raw.rs;
-  const int deg = raw.re - rs;
+  const int rs = ptr[v];
+  const int deg = ptr[v + 1] - rs;
   if (deg > kPackWaveMax || deg == 0) return;
   int a[NV][4];
   float d[NV][4];
+  // straight-line loads at clamped columns (F % 4 == 0 here), masked afterwards: no branch
+  // between the record and gradient loads, so both are in flight before the first wait
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
     const int f = (c * kWave + lane) * 4;
+    const int fc = min(f, F - 4);
     int ac[4];
     float dc[4];
-    if constexpr (sizeof(A) == 2) {
-      ac[0] = raw.a[c].x & 0xFFFF; ac[1] = raw.a[c].x >> 16; ac[2] = raw.a[c].y & 0xFFFF; ac[3] = raw.a[c].y >> 16;
-    } else {
-      ac[0] = raw.a[c].x; ac[1] = raw.a[c].y; ac[2] = raw.a[c].z; ac[3] = raw.a[c].w;
-    }
-    if constexpr (sizeof(T) == 2) {
-      dc[0] = to_f((uint16_t)(raw.d[c].x & 0xFFFF)); dc[1] = to_f((uint16_t)(raw.d[c].x >> 16));
-      dc[2] = to_f((uint16_t)(raw.d[c].y & 0xFFFF)); dc[3] = to_f((uint16_t)(raw.d[c].y >> 16));
-    } else {
-      dc[0] = raw.d[c].x; dc[1] = raw.d[c].y; dc[2] = raw.d[c].z; dc[3] = raw.d[c].w;
-    }
+    load_arg<4, A>(arg + (int64_t)v * lda, fc, F, ac);
+    load_tile<4, T>(dout + (int64_t)v * ldd, fc, F, dc, 0.f);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       a[c][i] = f < F ? ac[i] : arg_none<A>();
@@ -1205,27 +1162,12 @@ __global__ __launch_bounds__(kBlock) void group_pack_kernel(
   } else {
     const int wave = wave_id_uniform();
     const int v = (b - n_long) * kWavesPerBlock + wave;
-    if constexpr (NV > 0 && PG_PACK_PERSIST) {
-      // the short rows dealt over the launch's waves (row v, v + waves, ...: every row's work
-      // is its F features, whatever its degree, so a static deal is balanced), the next row's
-      // positions and gradients in flight while this one is packed
-      const int nw = ((int)gridDim.x - n_long) * kWavesPerBlock;
-      if (v >= n_rows) return;
-      PackRaw<NV, A, T> cur, nxt;
-      pack_load<NV, A, T>(cur, v, ptr, arg, lda, F, dout, ldd);
-      for (int u = v; u < n_rows; u += nw) {
-        pack_load<NV, A, T>(nxt, min(u + nw, n_rows - 1), ptr, arg, lda, F, dout, ldd);
-        pack_short_row_v<NV, A, T, R>(u, cur, wave, arg, lda, F, dout, ldd, fout, ldf, ew, gp, dsc, lds);
-        cur = nxt;
-      }
-    } else if (v < n_rows) {
-      if constexpr (NV > 0) {
-        PackRaw<NV, A, T> cur;
-        pack_load<NV, A, T>(cur, v, ptr, arg, lda, F, dout, ldd);
-        pack_short_row_v<NV, A, T, R>(v, cur, wave, arg, lda, F, dout, ldd, fout, ldf, ew, gp, dsc, lds);
-      } else {
+    if (v < n_rows)
+    {
+      if constexpr (NV > 0)
+        pack_short_row_v<NV, A, T, R>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, dsc, lds);
+      else
         pack_short_row<A, T, R>(v, wave, ptr, arg, lda, F, dout, ldd, fout, ldf, ew, gp, dsc, lds);
-      }
     }
   }
 }
@@ -1956,9 +1898,7 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     constexpr uintptr_t kTa = 4 * sizeof(T) - 1;
     const bool vec = F % 4 == 0 && lda % 4 == 0 && ldd % 4 == 0 && (!fwd_out || ldf % 4 == 0) &&
                      ((uintptr_t)argpos & 7) == 0 && ((uintptr_t)dout & kTa) == 0 && ((uintptr_t)fwd_out & kTa) == 0;
-    // the vector pack deals the short rows over a capped grid (PG_PACK_PERSIST)
-    const int short_blocks = (vec && PG_PACK_PERSIST) ? std::min(n_short_blocks, PG_PACK_BLOCKS) : n_short_blocks;
-    const dim3 pgrid((unsigned)(n_long + short_blocks));
+    const dim3 pgrid((unsigned)(n_long + n_short_blocks));
     const int4* prow = listed ? (const int4*)g->merges : nullptr;
     // transposed descriptors when the in-CSR slots' transposed indices are given (g->epos)
     const bool tr = g->epos != nullptr && PG_BWD_TRANS && ((uintptr_t)glist & 15) == 0;
