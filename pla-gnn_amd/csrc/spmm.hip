@@ -791,16 +791,6 @@ __device__ __forceinline__ int wave_incl_add(int x) {
 #endif
 }
 
-// inclusive add-scan inside each 32-lane half of the wave (row_bcast:31 left out)
-__device__ __forceinline__ int half_incl_add(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 (rows 1 and 3)
-  return x;
-}
-
 __device__ int block_exclusive_scan(int* s, int n, int* wsum) {
   const int per = (n + kBlock - 1) / kBlock;
   const int b = threadIdx.x * per;
@@ -1339,152 +1329,6 @@ __global__ __launch_bounds__(kBlock) void max_bwd_pull_kernel(
   } else {
     float* wr = ws + (int64_t)slot * ldw;
     for (int f = lane; f < F; f += kWave) wr[f] = acc[f];
-  }
-}
-
-#ifndef PG_PULL_PAIRS
-#define PG_PULL_PAIRS 0  // two schedule items per wave, one per 32-lane half (F <= 512)
-#endif
-
-// The pull with two items per wave (PG_PULL_PAIRS): half h (lanes 32 h .. 32 h + 31) takes
-// item 2 p + h of the longest-first schedule (neighbours: similar lengths) in windows of 32
-// out-edges, each half with its own row accumulator in LDS. Every load, ballot and LDS
-// read-add-write instruction then serves both items, so a wave keeps two dependent
-// descriptor -> list chains in flight and runs max(segments) add steps instead of their sum.
-// Per half the arithmetic is max_bwd_pull_kernel's: the lists in edge (ascending
-// destination) order, the same sums, the same split-row combine.
-template <typename T, typename R, bool TR, bool MERGE>
-__global__ __launch_bounds__(kBlock) void max_bwd_pull2_kernel(
-    const int32_t* __restrict__ tslot, const int4* __restrict__ items, int n_items,
-    const int32_t* __restrict__ tdst, const uint32_t* __restrict__ glist, R gp, int F,
-    const T* __restrict__ mask, int64_t ldm, T* __restrict__ dx, int64_t ldx, float* __restrict__ ws,
-    int64_t ldw, PullMerge pm) {
-  constexpr int U = PG_PULL_U;
-  constexpr int H = 32;
-  constexpr int kHF = kGroupMaxF / 2;  // F <= 512 (host)
-  __shared__ __attribute__((aligned(16))) float accs[kWavesPerBlock][2][kHF];
-  const int wave = wave_id_uniform();
-  const int pr = blockIdx.x * kWavesPerBlock + wave;
-  if (2 * pr >= n_items) return;
-  const int lane = lane_id(), h = lane >> 5, hl = lane & 31;
-  const bool has = 2 * pr + h < n_items;  // (the last wave's second half may have no item)
-  const int4 item = items[min(2 * pr + h, n_items - 1)];
-  const int row = item.x, t0 = item.y, t1 = has ? item.z : item.y, slot = item.w;
-  float* acc = accs[wave][h];
-  for (int f = hl; f < (MERGE ? (int)ldw : F); f += H) acc[f] = 0.f;
-  // windows of 32 out-edges per half, the descriptors one window ahead and their in-CSR slots
-  // two; every index clamped into [0, nnz) (an exhausted or empty half reads a valid entry it
-  // does not use), so the loads are unconditional
-  const int nwin = (t1 - t0 + H - 1) / H;
-  const int K = max(__builtin_amdgcn_readlane(nwin, 0), __builtin_amdgcn_readlane(nwin, 32));
-  auto tl_of = [&](int tw) { return max(tw + min(hl, t1 - tw - 1), 0); };
-  uint32_t dsc_next = glist[TR ? tl_of(t0) : tslot[tl_of(t0)]];
-  int vf_next = tdst[tl_of(t0)] * F;
-  int ts_next = TR ? 0 : tslot[tl_of(t0 + H)];
-  for (int k = 0; k < K; ++k) {
-    const int tw = t0 + k * H;
-    const int nw = max(0, min(H, t1 - tw));
-    const int2 dsc = make_int2(vf_next + (int)(dsc_next & 0xFFFFu), (int)(dsc_next >> 16));
-    if (k + 1 < K) {
-      dsc_next = glist[TR ? tl_of(tw + H) : ts_next];
-      vf_next = tdst[tl_of(tw + H)] * F;
-      if (!TR) ts_next = tslot[tl_of(tw + 2 * H)];
-    }
-    // segments: 32-entry pieces of single lists, per half; U of each half's in flight
-    const int nseg = hl < nw ? (dsc.y + H - 1) / H : 0;
-    const int incl = half_incl_add(nseg);
-    const int excl = incl - nseg;
-    const int tot0 = __builtin_amdgcn_readlane(incl, 31), tot1 = __builtin_amdgcn_readlane(incl, 63);
-    const int totmax = max(tot0, tot1);
-    for (int s0 = 0; s0 < totmax; s0 += U) {
-      const int nv0 = min(U, tot0 - s0), nv1 = min(U, tot1 - s0);  // <= 0: that half is done
-      int fe[U], ne[U];
-      float de[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int ta = s0 + max(0, min(u, nv0 - 1)), tb = s0 + max(0, min(u, nv1 - 1));
-        const uint64_t bal = __ballot(excl <= (h ? tb : ta));
-        const int i0 = max(0, __popc((uint32_t)bal) - 1), i1 = 32 + max(0, __popc((uint32_t)(bal >> 32)) - 1);
-        const int ex = h ? bcast(excl, i1) : bcast(excl, i0);
-        const int lx = h ? bcast(dsc.x, i1) : bcast(dsc.x, i0);
-        const int ly = h ? bcast(dsc.y, i1) : bcast(dsc.y, i0);
-        const bool on = u < (h ? nv1 : nv0);
-        const int seg = (h ? tb : ta) - ex;
-        const int n = on ? min(H, ly - seg * H) : 0;
-        ne[u] = n;
-        // a half with no segment here reads record 0 (valid, unused)
-        gp.get((on ? lx + seg * H : 0) + min(hl, max(n, 1) - 1), fe[u], de[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (hl < ne[u]) acc[fe[u]] += de[u];
-    }
-  }
-  wave_lds_sync();
-  if (!MERGE || slot < 0) {
-    if (has && slot < 0) {
-      T* xr = dx + (int64_t)row * ldx;
-      const T* mr = mask ? mask + (int64_t)row * ldm : nullptr;
-      for (int f = hl; f < F; f += H) {
-        float a = acc[f];
-        if (mr && !(to_f(mr[f]) > 0.f)) a = 0.f;
-        xr[f] = from_f<T>(a);
-      }
-    } else if (has) {
-      float* wr = ws + (int64_t)slot * ldw;
-      for (int f = hl; f < F; f += H) wr[f] = acc[f];
-    }
-  }
-  if constexpr (MERGE) {
-    // the split-row combine of max_bwd_pull_kernel, per half (both halves' payloads drained
-    // before either ticket)
-    const bool piece = has && slot >= 0;
-    const __amdgpu_buffer_rsrc_t rs = pg_x3::rsrc(ws, pm.ws_bytes);
-    if (piece) {
-      const uint32_t sbase = (uint32_t)slot * (uint32_t)ldw * 4u;
-      for (int f = hl * 4; f < F; f += H * 4)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pg_u32x4, *reinterpret_cast<const float4*>(acc + f)),
-                                               rs, sbase + (uint32_t)f * 4u, 0, 16);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every payload store drained before the tickets
-    int s0 = 0, ns = 0;
-    uint32_t ticket = 0;
-    if (piece) {
-      const int rb = pm.ptr[row], re = pm.ptr[row + 1];
-      s0 = slot - (t0 - rb) / pm.chunk;
-      ns = (re - rb + pm.chunk - 1) / pm.chunk;
-      if (hl == 0)
-        ticket = __hip_atomic_fetch_add((pg_gu32*)(pm.tickets + s0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const int tk = h ? __builtin_amdgcn_readlane((int)ticket, 32) : __builtin_amdgcn_readlane((int)ticket, 0);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the tickets
-    if (piece && tk == ns - 1) {
-      T* xr = dx + (int64_t)row * ldx;
-      const T* mr = mask ? mask + (int64_t)row * ldm : nullptr;
-      for (int f = hl * 4; f < F; f += H * 4) {
-        float a[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int s = s0; s < s0 + ns; s += 8) {
-          float4 v[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            v[e] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                rs, (uint32_t)min(s + e, s0 + ns - 1) * (uint32_t)ldw * 4u + (uint32_t)f * 4u, 0, 16));
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (s + e < s0 + ns) {
-              a[0] += v[e].x; a[1] += v[e].y; a[2] += v[e].z; a[3] += v[e].w;
-            }
-        }
-        if (mr) {
-          float mk[4];
-          load_tile<4, T>(mr, f, F, mk, 0.f);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (!(mk[i] > 0.f)) a[i] = 0.f;
-        }
-        store_tile<4, T>(xr, f, F, a);
-      }
-    }
   }
 }
 
@@ -2084,17 +1928,7 @@ int max_bwd_entry(const pg_csr_t* g, const pg_csr_t* gt, const void* argpos, int
     // sums to +0, which the mask would leave +0. With fwd_out alone the mask is applied.
     if (dead_none) mask_src = nullptr;
     const PullMerge pm{gt->ptr, gt->chunk, tickets, (uint32_t)pbytes};
-    if (PG_PULL_PAIRS && F <= kGroupMaxF / 2 && gt->nnz > 0) {  // two items per wave
-      const int pblocks = grid_for((gt->n_items + 1) / 2);
-      if (merge_in)
-        hipLaunchKernelGGL((max_bwd_pull2_kernel<T, R, TR, true>), dim3(pblocks), dim3(kBlock), 0, st, gt->eslot,
-                           (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
-                           dx, ldx, w, ws_ld(F), pm);
-      else
-        hipLaunchKernelGGL((max_bwd_pull2_kernel<T, R, TR, false>), dim3(pblocks), dim3(kBlock), 0, st, gt->eslot,
-                           (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
-                           dx, ldx, w, ws_ld(F), pm);
-    } else if (merge_in)
+    if (merge_in)
       hipLaunchKernelGGL((max_bwd_pull_kernel<T, R, TR, true>), dim3(blocks), dim3(kBlock), 0, st, gt->eslot,
                          (const int4*)gt->items, (int)gt->n_items, gt->col, glist, gp, (int)F, mask_src, ldm,
                          dx, ldx, w, ws_ld(F), pm);
