@@ -664,6 +664,7 @@ def main(argv=None):
     ap.add_argument("--dump-breakdown", default="", help="write the per-launch-site breakdown (JSON)")
     ap.add_argument("--dropin-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--chunk-bwd", type=int, default=0, help=argparse.SUPPRESS)  # tuning experiments
+    ap.add_argument("--bwd-trans-min", type=int, default=-1, help=argparse.SUPPRESS)  # A/B: transposed descriptors from E
     ap.add_argument("--separate-l1-head", action="store_true", help=argparse.SUPPRESS)  # A/B: unfused MLP head
     ap.add_argument("--separate-adam-prep", action="store_true", help=argparse.SUPPRESS)  # A/B: own prepare launch
     args = ap.parse_args(argv)
@@ -675,6 +676,10 @@ def main(argv=None):
         import plagnn.engine
 
         plagnn.engine.TrainEngine.FOLD_ADAM_PREP = False
+    if args.bwd_trans_min >= 0:
+        import plagnn.graph
+
+        plagnn.graph.TRANS_MIN_EDGES = args.bwd_trans_min
     if args.chunk_bwd:
         import plagnn.graph
 
