@@ -727,8 +727,9 @@ inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& 
 
 // Tile of the three-piece kernel (measured per cfg2 shape with each tile forced, within 1-3 %
 // of the best everywhere): 128 x 128 (4 waves of 64 x 64: 0.5 fragment reads per MFMA)
-// wherever that gives >= 2 workgroups per CU, or >= 1 for K >= 1000; else 128 x 64, else
-// 64 x 64. Split products: 128 x 128, ~2 workgroups per CU (512: 1.636 ms/step, 768: 1.667,
+// wherever that gives >= 2 workgroups per CU; else 128 x 64, else 64 x 64. (Round 6: a
+// long-K product with 256-511 128 x 128 tiles, cfg2's fwd.cat.l1, runs 87.2 instead of 91.0
+// us on 128 x 64 tiles: 752 tiles share out over 256 CUs, 376 leave 136 CUs one tile idle.) Split products: 128 x 128, ~2 workgroups per CU (512: 1.636 ms/step, 768: 1.667,
 // 1024: 1.721).
 inline void pick_tile_x3(int64_t M, int64_t N, int64_t K, int split, int& bm, int& bn) {
   if constexpr (PG_X3_TILE_FORCE != 0) {  // variant builds only
@@ -743,7 +744,10 @@ inline void pick_tile_x3(int64_t M, int64_t N, int64_t K, int split, int& bm, in
     return;
   }
   bm = bn = 64;
-  if (tiles(128, 128) >= 512 || (tiles(128, 128) >= 256 && K >= 1000)) bm = bn = 128;
+#ifndef PG_X3_LONGK_128
+#define PG_X3_LONGK_128 0  // 1: long-K products with 256-511 128 x 128 tiles keep 128 x 128
+#endif
+  if (tiles(128, 128) >= 512 || (PG_X3_LONGK_128 && tiles(128, 128) >= 256 && K >= 1000)) bm = bn = 128;
   else if (tiles(128, 64) >= 512) bm = 128;
 }
 
