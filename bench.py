@@ -667,6 +667,7 @@ def main(argv=None):
     ap.add_argument("--bwd-trans-min", type=int, default=-1, help=argparse.SUPPRESS)  # A/B: transposed descriptors from E
     ap.add_argument("--separate-l1-head", action="store_true", help=argparse.SUPPRESS)  # A/B: unfused MLP head
     ap.add_argument("--separate-adam-prep", action="store_true", help=argparse.SUPPRESS)  # A/B: own prepare launch
+    ap.add_argument("--split-l1-per-call", action="store_true", help=argparse.SUPPRESS)  # A/B: head splits W1
     args = ap.parse_args(argv)
     if args.separate_l1_head:
         import plagnn.engine
@@ -676,6 +677,10 @@ def main(argv=None):
         import plagnn.engine
 
         plagnn.engine.TrainEngine.FOLD_ADAM_PREP = False
+    if args.split_l1_per_call:
+        import plagnn.engine
+
+        plagnn.engine.TrainEngine.KEEP_L1_PIECES = False
     if args.bwd_trans_min >= 0:
         import plagnn.graph
 

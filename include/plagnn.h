@@ -266,6 +266,27 @@ int pg_mlp_l1_head(const float* H3, int64_t ldh, int64_t n, int32_t F3, const fl
                    float* dz, int64_t lddz, float* dA4, int64_t ldg, float* dH3, int64_t lddh, float slope,
                    float* loss2, void* ws, size_t ws_bytes, float* adam_state, double lr, double beta1,
                    double beta2, pg_stream_t stream);
+/* (ABI 13) W1's three bf16 pieces kept by the caller instead of split in each call:
+ * pg_mlp_l1_split writes them (two fragment-native layouts, pg_mlp_l1_pieces_bytes(F3, K1)
+ * bytes, 256-B aligned) from W1; pg_mlp_l1_head_ex is pg_mlp_l1_head reading them (W1
+ * itself is then not read); pg_adam_apply_l1 is pg_adam_apply over the n flat parameters
+ * that also rewrites, for W1 = param + w1_offset ([K1][ldw1] inside the n), the pieces of
+ * every element it updates: after it the pieces equal pg_mlp_l1_split of the new W1 bitwise,
+ * so a training step needs no split launch. The pieces go stale if W1 is written any other
+ * way: split again. Results are bitwise those of pg_mlp_l1_head / pg_adam_apply. */
+size_t pg_mlp_l1_pieces_bytes(int32_t F3, int32_t K1);
+int pg_mlp_l1_split(const float* W1, int64_t ldw1, int32_t F3, int32_t K1, void* pieces, pg_stream_t stream);
+int pg_mlp_l1_head_ex(const float* H3, int64_t ldh, int64_t n, int32_t F3, const float* W1, int64_t ldw1,
+                      const float* b1, int32_t K1, float* A4, int64_t lda4, const float* W2, int64_t ldw,
+                      const float* b2, int32_t C, const float* labels, int64_t ldl, const float* class_w,
+                      const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob, int64_t ldp,
+                      float* dz, int64_t lddz, float* dA4, int64_t ldg, float* dH3, int64_t lddh, float slope,
+                      float* loss2, void* ws, size_t ws_bytes, float* adam_state, double lr, double beta1,
+                      double beta2, const void* w1_pieces, pg_stream_t stream);
+int pg_adam_apply_l1(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                     const float* state, double beta1, double beta2, double eps, double weight_decay,
+                     int64_t w1_offset, int64_t ldw1, int32_t F3, int32_t K1, void* w1_pieces,
+                     pg_stream_t stream);
 size_t pg_sigmoid_multi_loss_workspace(int64_t n_index, int32_t C);
 int pg_sigmoid_multi_loss(const float* z, int64_t ldz, int64_t n_rows, int32_t C,
                           const float* labels, int64_t ldl, const float* class_w,
@@ -526,7 +547,8 @@ int pg_version(void); /* 2: pg_csr_t.einv; 3: pg_spmm_max_bwd fwd_out; 5: no in-
                          relu' mask is applied, only PG_ARG_DEAD_NONE implies it;
                          9: pg_gemm_f32_group; 10: the in-CSR's epos = transposed
                          indices (transposed max-backward descriptors), pg_gemm_f32_cat;
-                         11: pg_pad2d_group; 12: pg_mlp_l1_head */
+                         11: pg_pad2d_group; 12: pg_mlp_l1_head;
+                         13: pg_mlp_l1_split, pg_mlp_l1_head_ex, pg_adam_apply_l1 */
 
 #ifdef __cplusplus
 }

@@ -229,16 +229,8 @@ __global__ __launch_bounds__(kBlock) void adam_apply_kernel(
   const float step_size = state[1];
   const float bc2s = state[2];
   for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kBlock) {
-    float gi = g[i];
-    if (wd != 0.f) gi = gi + wd * p[i];
-    const float mi = m[i] * beta1 + a1 * gi;        // exp_avg.mul_(b1).add_(g, alpha=1-b1)
-    const float vi = v[i] * beta2 + a2 * gi * gi;   // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-    const float denom = sqrtf(vi) / bc2s + eps;     // (sqrt / sqrt(bc2)).add_(eps)
-    p[i] = p[i] + (-step_size) * (mi / denom);      // addcdiv_(m, denom, -step_size)
-    m[i] = mi;
-    v[i] = vi;
-  }
+       i += (int64_t)gridDim.x * kBlock)
+    pg_adam::elem(p, g, m, v, i, step_size, bc2s, beta1, beta2, a1, a2, eps, wd);
 }
 
 // bf16 storage helpers: dst[i] = bf16(src[map ? map[i] : i]) (round to nearest even;

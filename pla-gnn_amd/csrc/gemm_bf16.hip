@@ -58,6 +58,12 @@ constexpr int BK = 64;  // bf16 k-values per K step (two-stage kernels; deep one
 #ifndef PG_BF16_DEEP
 #define PG_BF16_DEEP 0
 #endif
+#ifndef PG_BF16_T2  // variant builds: 256 x 128 tiles, KB = 32, two workgroups per CU
+#define PG_BF16_T2 0
+#endif
+#ifndef PG_BF16_T2_NS
+#define PG_BF16_T2_NS 2
+#endif
 
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
@@ -749,8 +755,9 @@ int launch_epi(int epi, dim3 grid, hipStream_t st, const Args& a) {
   // x 4 stages and counted vmcnt instead; measured slower (fwd.cat 670 us either way, 8192^3
   // 1580 vs 1180 us): the DMA latency is not what holds this structure back.
   constexpr bool deep = PG_BF16_DEEP && BM == 256 && BN == 256;
-  constexpr int KB = deep ? 32 : 64;
-  constexpr int NS = deep ? 4 : 2;
+  constexpr bool t2 = PG_BF16_T2 && BM == 256 && BN == 128;
+  constexpr int KB = deep || t2 ? 32 : 64;
+  constexpr int NS = deep ? 4 : t2 ? PG_BF16_T2_NS : 2;
 #define PG_L(EPI_)                                                                                    \
   hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, KB, NS, TA, TB, EPI_, OBF>), grid, dim3(64 * WM * WN), 0, st, \
                      a.M, a.N, a.K, a.kps, a.tiles_n, a.tiles, a.alpha, a.A, a.lda, a.B, a.ldb,   \
@@ -840,7 +847,10 @@ inline void pick_tile(int64_t M, int64_t N, int64_t K, int split, int& bm, int& 
     }
   }
   // (a short K leaves a 256 x 256 workgroup, alone on its CU, mostly in its epilogue)
-  if (N >= 256 && K >= 384 && tiles(256, 256) >= 256) {
+  if (PG_BF16_T2 && N >= 128 && K >= 384 && tiles(256, 128) >= 512) {
+    bm = 256;
+    bn = 128;
+  } else if (N >= 256 && K >= 384 && tiles(256, 256) >= 256) {
     bm = bn = 256;
   } else if (N > 64 && tiles(128, 128) >= 512) {
     bm = bn = 128;

@@ -35,7 +35,7 @@ extern "C" {
 
 const char* pg_last_error_string(void) { return pg::error_buffer(); }
 
-int pg_version(void) { return 12; }
+int pg_version(void) { return 13; }
 
 int pg_csr_from_coo(const int64_t* src, const int64_t* dst, int64_t nnz, int64_t n_src,
                     int64_t n_dst, int32_t* ptr, int32_t* col, int32_t* eid) {

@@ -14,6 +14,7 @@
 // final workgroup sums the blocks in a fixed order: deterministic.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "adam_step.hpp"
@@ -324,6 +325,63 @@ __global__ __launch_bounds__(kBlock) void l1_split_kernel(const float* __restric
   pg_x3::split4(make_float4(v[4], v[5], v[6], v[7]), b);
 #pragma unroll
   for (int p = 0; p < 3; ++p) *reinterpret_cast<uint4*>(dst + p * plane) = make_uint4(a[p].x, a[p].y, b[p].x, b[p].y);
+}
+
+// one f32 value's three pieces, as split4 forms each lane of its quad
+__device__ __forceinline__ void split1(float x, uint16_t (&q)[3]) {
+#pragma unroll
+  for (int piece = 0; piece < 3; ++piece) {
+    const uint32_t pk = pg_x3::pk_bf16(x, 0.f);
+    q[piece] = (uint16_t)(pk & 0xFFFFu);
+    if (piece < 2) x = x - pg_x3::lo_f(pk);
+  }
+}
+
+// Adam over the flat parameters (pg_adam_apply's update, pg_adam::elem) that also keeps W1's
+// pieces current: the thread that writes W1[r][k] (k < F3, r < K1) stores its three pieces at
+// that element's places in both fragment-native layouts (l1_split_kernel's p1 and p3). W1's
+// elements go to the first blocks of the grid, the other parameters to the rest. The
+// pieces' zero pads are never touched, so one pg_mlp_l1_split before the first step keeps
+// them. Replaces the split launch that each fused-head call made before (the step's W1
+// changes only here).
+__global__ __launch_bounds__(kBlock) void adam_apply_l1_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v, int64_t n,
+    const float* __restrict__ state, float beta1, float beta2, float a1, float a2, float eps, float wd,
+    int64_t w1_off, int ldw1, int K1, int F3, uint16_t* __restrict__ p1, uint16_t* __restrict__ p3, int nb1) {
+  const float step_size = state[1];
+  const float bc2s = state[2];
+  const int64_t nw1 = (int64_t)K1 * ldw1;
+  if ((int)blockIdx.x < nb1) {
+    // the first nb1 blocks: W1's elements (their piece stores are the slow part, so these
+    // blocks start first)
+    const int F16 = (F3 + 15) / 16 * 16, K16 = (K1 + 15) / 16 * 16;
+    const int64_t pl1 = l1_p1_plane(F3), pl3 = l1_p3_plane(F3, K1);
+    for (int64_t j = blockIdx.x * (int64_t)kBlock + threadIdx.x; j < nw1; j += (int64_t)nb1 * kBlock) {
+      const float pi = pg_adam::elem(p, g, m, v, w1_off + j, step_size, bc2s, beta1, beta2, a1, a2, eps, wd);
+      const int r = (int)(j / ldw1), k = (int)(j - (int64_t)r * ldw1);
+      if (k < F3) {
+        uint16_t q[3];
+        split1(pi, q);
+        // p1: block (r / 32, k / 8), lane r % 32, element k % 8
+        const int64_t e1 = ((int64_t)((r >> 5) * (F16 / 8) + (k >> 3)) * 32 + (r & 31)) * 8 + (k & 7);
+        // p3 (W1^T): block (k / 32, r / 8), lane k % 32, element r % 8
+        const int64_t e3 = ((int64_t)((k >> 5) * (K16 / 8) + (r >> 3)) * 32 + (k & 31)) * 8 + (r & 7);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          p1[e1 + c * pl1] = q[c];
+          p3[e3 + c * pl3] = q[c];
+        }
+      }
+    }
+    return;
+  }
+  // the rest: every other parameter, as pg_adam_apply
+  const int64_t nrest = n - nw1;
+  const int nb = (int)gridDim.x - nb1;
+  for (int64_t u = (blockIdx.x - nb1) * (int64_t)kBlock + threadIdx.x; u < nrest; u += (int64_t)nb * kBlock) {
+    const int64_t i = u < w1_off ? u : u + nw1;
+    pg_adam::elem(p, g, m, v, i, step_size, bc2s, beta1, beta2, a1, a2, eps, wd);
+  }
 }
 
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WAVES))) void mlp_l1_head_kernel(
@@ -670,6 +728,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PG_L1_WA
   }
 }
 
+bool l1_shape_ok(int32_t F3, int32_t K1) { return F3 > 0 && F3 % 4 == 0 && F3 <= 4096 && K1 > 0 && K1 <= kL1K1; }
+void l1_split_launch(const float* w1, int64_t ldw1, int32_t F3, int32_t K1, uint16_t* p1, uint16_t* p3,
+                     hipStream_t st) {
+  const int units = (int)(kL1K1 * ((F3 + 15) / 16 * 2) + ((F3 + 31) / 32 * 32) * ((K1 + 15) / 16 * 2));
+  hipLaunchKernelGGL(l1_split_kernel, dim3((units + kBlock - 1) / kBlock), dim3(kBlock), 0, st, w1, ldw1, (int)K1,
+                     (int)F3, p1, p3);
+}
+uint16_t* l1_p3_of(void* pieces, int32_t F3) {
+  return (uint16_t*)pieces + ((size_t)(3 * l1_p1_plane(F3) * 2 + 255) / 256 * 256) / 2;
+}
+
 }  // namespace
 
 extern "C" {
@@ -721,13 +790,48 @@ size_t pg_mlp_l1_head_workspace(int64_t n, int32_t C, int32_t F3, int32_t K1) {
   return head + p1 + (size_t)(3 * l1_p3_plane(F3, K1) * 2);
 }
 
-int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const float* w1, int64_t ldw1,
+size_t pg_mlp_l1_pieces_bytes(int32_t F3, int32_t K1) {
+  if (F3 <= 0 || K1 <= 0) return 0;
+  return (size_t)(3 * l1_p1_plane(F3) * 2 + 255) / 256 * 256 + (size_t)(3 * l1_p3_plane(F3, K1) * 2);
+}
+
+int pg_mlp_l1_split(const float* w1, int64_t ldw1, int32_t F3, int32_t K1, void* pieces, pg_stream_t stream) {
+  if (!l1_shape_ok(F3, K1) || ldw1 < F3) return pg::set_error(PG_ERR_INVALID, "pg_mlp_l1_split: bad shape");
+  if (!w1 || !pieces || ((uintptr_t)pieces & 255))
+    return pg::set_error(PG_ERR_INVALID, "pg_mlp_l1_split: NULL W1, or pieces not 256-B aligned");
+  l1_split_launch(w1, ldw1, F3, K1, (uint16_t*)pieces, l1_p3_of(pieces, F3), (hipStream_t)stream);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pg::set_error((int)e, "pg_mlp_l1_split: launch failed: %s", hipGetErrorString(e));
+  return pg::ok();
+}
+
+int pg_adam_apply_l1(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                     const float* state, double beta1, double beta2, double eps, double weight_decay,
+                     int64_t w1_offset, int64_t ldw1, int32_t F3, int32_t K1, void* pieces, pg_stream_t stream) {
+  if (n < 0 || !state) return pg::set_error(PG_ERR_INVALID, "pg_adam_apply_l1: bad arguments");
+  if (!l1_shape_ok(F3, K1) || ldw1 < F3 || ldw1 > INT32_MAX || w1_offset < 0 || w1_offset + (int64_t)K1 * ldw1 > n)
+    return pg::set_error(PG_ERR_INVALID, "pg_adam_apply_l1: W1 [K1][ldw1] must lie inside the n parameters");
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !pieces || ((uintptr_t)pieces & 255))
+    return pg::set_error(PG_ERR_INVALID, "pg_adam_apply_l1: NULL buffer, or pieces not 256-B aligned");
+  const int64_t nw1 = (int64_t)K1 * ldw1;
+  const int nb1 = (int)std::min<int64_t>((nw1 + kBlock - 1) / kBlock, 4096);
+  const int64_t blocks = nb1 + std::max<int64_t>(1, std::min<int64_t>((n - nw1 + kBlock - 1) / kBlock, 32768));
+  hipLaunchKernelGGL(adam_apply_l1_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, param,
+                     grad, exp_avg, exp_avg_sq, n, state, (float)beta1, (float)beta2, (float)(1.0 - beta1),
+                     (float)(1.0 - beta2), (float)eps, (float)weight_decay, w1_offset, (int)ldw1, (int)K1, (int)F3,
+                     (uint16_t*)pieces, l1_p3_of(pieces, F3), nb1);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pg::set_error((int)e, "pg_adam_apply_l1: launch failed: %s", hipGetErrorString(e));
+  return pg::ok();
+}
+
+static int mlp_l1_head_impl(const float* h3, int64_t ldh, int64_t n, int32_t F3, const float* w1, int64_t ldw1,
                    const float* b1, int32_t K1, float* a4, int64_t lda4, const float* w2, int64_t ldw,
                    const float* b2, int32_t C, const float* labels, int64_t ldl, const float* class_w,
                    const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob, int64_t ldp,
                    float* dz, int64_t lddz, float* da4, int64_t ldg, float* dh3, int64_t lddh, float slope,
                    float* loss2, void* ws, size_t ws_bytes, float* adam_state, double lr, double beta1,
-                   double beta2, pg_stream_t stream) {
+                   double beta2, const void* pieces, pg_stream_t stream) {
   if (n < 0 || n > INT32_MAX || F3 <= 0 || F3 % 4 != 0 || F3 > 4096 || K1 <= 0 || K1 > kL1K1 || K1 > kMaxK ||
       C <= 0 || C > kMaxC || ldh < F3 || ldw1 < F3 || lda4 < K1 || ldw < K1 || ldl < C || (prob && ldp < C) ||
       (dz && lddz < C) || ldg < K1 || lddh < F3)
@@ -748,12 +852,15 @@ int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const fl
   float* part = (float*)ws;
   uint16_t* p1 = nullptr;
   uint16_t* p3 = nullptr;
-  if (PG_L1_PRESPLIT) {
+  if (pieces) {  // kept current by the caller (pg_mlp_l1_split, pg_adam_apply_l1)
+    if (!PG_L1_PRESPLIT || ((uintptr_t)pieces & 255))
+      return pg::set_error(PG_ERR_INVALID, "pg_mlp_l1_head_ex: pieces not 256-B aligned");
+    p1 = (uint16_t*)pieces;
+    p3 = l1_p3_of((void*)pieces, F3);
+  } else if (PG_L1_PRESPLIT) {
     p1 = (uint16_t*)((char*)ws + (pg_mlp_head_workspace(n, C) + 255) / 256 * 256);
-    p3 = p1 + ((size_t)(3 * l1_p1_plane(F3) * 2 + 255) / 256 * 256) / 2;
-    const int units = (int)(kL1K1 * ((F3 + 15) / 16 * 2) + ((F3 + 31) / 32 * 32) * ((K1 + 15) / 16 * 2));
-    hipLaunchKernelGGL(l1_split_kernel, dim3((units + kBlock - 1) / kBlock), dim3(kBlock), 0, st, w1, ldw1, (int)K1,
-                       (int)F3, p1, p3);
+    p3 = l1_p3_of(p1, F3);
+    l1_split_launch(w1, ldw1, F3, K1, p1, p3, st);
   }
   const float inv_n = n_train > 0 ? 1.0f / (float)n_train : 0.f;
   hipLaunchKernelGGL(mlp_l1_head_kernel, dim3(nb), dim3(kBlock), (unsigned)l1_region_bytes(K1), st, h3, ldh, (int)n,
@@ -765,6 +872,31 @@ int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const fl
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pg::set_error((int)e, "pg_mlp_l1_head: launch failed: %s", hipGetErrorString(e));
   return pg::ok();
+}
+
+int pg_mlp_l1_head(const float* h3, int64_t ldh, int64_t n, int32_t F3, const float* w1, int64_t ldw1,
+                   const float* b1, int32_t K1, float* a4, int64_t lda4, const float* w2, int64_t ldw,
+                   const float* b2, int32_t C, const float* labels, int64_t ldl, const float* class_w,
+                   const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob, int64_t ldp,
+                   float* dz, int64_t lddz, float* da4, int64_t ldg, float* dh3, int64_t lddh, float slope,
+                   float* loss2, void* ws, size_t ws_bytes, float* adam_state, double lr, double beta1,
+                   double beta2, pg_stream_t stream) {
+  return mlp_l1_head_impl(h3, ldh, n, F3, w1, ldw1, b1, K1, a4, lda4, w2, ldw, b2, C, labels, ldl, class_w, row_set,
+                          n_train, n_val, prob, ldp, dz, lddz, da4, ldg, dh3, lddh, slope, loss2, ws, ws_bytes,
+                          adam_state, lr, beta1, beta2, nullptr, stream);
+}
+
+int pg_mlp_l1_head_ex(const float* h3, int64_t ldh, int64_t n, int32_t F3, const float* w1, int64_t ldw1,
+                      const float* b1, int32_t K1, float* a4, int64_t lda4, const float* w2, int64_t ldw,
+                      const float* b2, int32_t C, const float* labels, int64_t ldl, const float* class_w,
+                      const int8_t* row_set, int64_t n_train, int64_t n_val, float* prob, int64_t ldp,
+                      float* dz, int64_t lddz, float* da4, int64_t ldg, float* dh3, int64_t lddh, float slope,
+                      float* loss2, void* ws, size_t ws_bytes, float* adam_state, double lr, double beta1,
+                      double beta2, const void* w1_pieces, pg_stream_t stream) {
+  if (!w1_pieces) return pg::set_error(PG_ERR_INVALID, "pg_mlp_l1_head_ex: NULL pieces");
+  return mlp_l1_head_impl(h3, ldh, n, F3, w1, ldw1, b1, K1, a4, lda4, w2, ldw, b2, C, labels, ldl, class_w, row_set,
+                          n_train, n_val, prob, ldp, dz, lddz, da4, ldg, dh3, lddh, slope, loss2, ws, ws_bytes,
+                          adam_state, lr, beta1, beta2, w1_pieces, stream);
 }
 
 }  // extern "C"

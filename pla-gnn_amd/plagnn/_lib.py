@@ -13,7 +13,7 @@ import warnings
 import torch  # noqa: F401  (load order: see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 12  # pg_version() of the library this package binds (include/plagnn.h)
+ABI_VERSION = 13  # pg_version() of the library this package binds (include/plagnn.h)
 # PLAGNN_LIB overrides the library path (A/B builds of tuning variants)
 LIB_PATH = os.environ.get("PLAGNN_LIB") or os.path.join(_HERE, "libplagnn.so")
 
@@ -162,6 +162,12 @@ SIGNATURES = {
     "pg_mlp_l1_head": (_i, [_vp, _i64, _i64, _i32, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _i64, _vp, _i32, _vp,
                             _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _f, _vp,
                             _vp, _sz, _vp, _d, _d, _d, _vp]),
+    "pg_mlp_l1_pieces_bytes": (_sz, [_i32, _i32]),
+    "pg_mlp_l1_split": (_i, [_vp, _i64, _i32, _i32, _vp, _vp]),
+    "pg_mlp_l1_head_ex": (_i, [_vp, _i64, _i64, _i32, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _i64, _vp, _i32, _vp,
+                               _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _f, _vp,
+                               _vp, _sz, _vp, _d, _d, _d, _vp, _vp]),
+    "pg_adam_apply_l1": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _d, _d, _d, _d, _i64, _i64, _i32, _i32, _vp, _vp]),
     "pg_adam_prepare": (_i, [_vp, _d, _d, _d, _vp]),
     "pg_adam_apply": (_i, [_vp, _vp, _vp, _vp, _i64, _vp, _d, _d, _d, _d, _vp]),
     "pg_gemm_f32_split_k": (_i, [_i64, _i64, _i64]),

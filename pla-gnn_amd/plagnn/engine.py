@@ -86,6 +86,9 @@ class TrainEngine:
     # with it, the fused head's final kernel also forms the step's Adam scalars (pg_adam_prepare's
     # work): one launch fewer per step (A/B knob)
     FOLD_ADAM_PREP = True
+    # with it, W1's bf16 pieces live in their own buffer, rewritten by the step's Adam
+    # (pg_adam_apply_l1), so the head splits nothing: one launch fewer per step (A/B knob)
+    KEEP_L1_PIECES = True
     _fold_prep = False             # set by the step paths (step_eager, capture, group_times)
     _prepped = False               # the head of this step formed the Adam scalars
     WIDTH_ALIGN = 4  # every padded width is a multiple of this
@@ -188,6 +191,14 @@ class TrainEngine:
         self.n_val = 0 if val_index is None else len(np.asarray(val_index))
         self._alloc_buffers(features)
         self._alloc_workspace()
+        # W1's bf16 pieces for the fused head, kept current by the step's Adam
+        # (pg_adam_apply_l1) instead of split in every head call (pg_mlp_l1_split here and
+        # whenever the parameters are written from outside the step)
+        self.l1_pieces: Optional[torch.Tensor] = None
+        if self._l1_fused() and self.KEEP_L1_PIECES:
+            nb = int(_lib.lib().pg_mlp_l1_pieces_bytes(self.pd[-3], self.pd[-2]))
+            self.l1_pieces = torch.zeros(nb, dtype=torch.uint8, device=dev)
+            self._split_l1()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_adam: Optional[torch.cuda.CUDAGraph] = None
         self.allreduce = None
@@ -314,6 +325,13 @@ class TrainEngine:
             self.P["liner1.b"][:d[-2]] = sd["liner1.bias"]
             self.P["liner2.W"][:d[-1], :d[-2]] = sd["liner2.weight"]
             self.P["liner2.b"][:d[-1]] = sd["liner2.bias"]
+        if getattr(self, "l1_pieces", None) is not None:
+            self._split_l1()
+
+    def _split_l1(self) -> None:
+        W1 = self.P["liner1.W"]
+        self._call("pg_mlp_l1_split", ptr(W1), W1.stride(0), self.pd[-3], self.pd[-2], ptr(self.l1_pieces),
+                   self._s())
 
     def _unpad(self, views: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         out = {}
@@ -337,7 +355,9 @@ class TrainEngine:
 
     def params_updated(self) -> None:
         """Call after writing `flat` from outside the engine (e.g. a broadcast from rank 0):
-        refreshes whatever the engine derives from the parameters (nothing in fp32)."""
+        refreshes whatever the engine derives from the parameters (in fp32: W1's pieces)."""
+        if self.l1_pieces is not None:
+            self._split_l1()
 
     def broadcast_params(self, src: int = 0) -> None:
         """Every rank takes rank `src`'s parameters (multi-GPU replicas start identical)."""
@@ -589,13 +609,15 @@ class TrainEngine:
         fold = self._fold_prep and self.FOLD_ADAM_PREP
         self._prepped = fold
         with self._t("head.l1", 2.0 * 2 * self.N * pd[-3] * pd[-2]):
-            self._call("pg_mlp_l1_head", ptr(self.A3), self.A3.stride(0), self.N, pd[-3], ptr(P["liner1.W"]),
+            fn = "pg_mlp_l1_head" if self.l1_pieces is None else "pg_mlp_l1_head_ex"
+            pieces = () if self.l1_pieces is None else (ptr(self.l1_pieces),)
+            self._call(fn, ptr(self.A3), self.A3.stride(0), self.N, pd[-3], ptr(P["liner1.W"]),
                        P["liner1.W"].stride(0), ptr(P["liner1.b"]), pd[-2], ptr(self.A4), self.A4.stride(0),
                        ptr(P["liner2.W"]), pd[-2], ptr(P["liner2.b"]), C, ptr(self.labels), pd[-1], ptr(self.cw),
                        ptr(self.row_set), self.n_train, self.n_val, ptr(self.prob), pd[-1], ptr(self.dZ), pd[-1],
                        ptr(self.dA4), self.dA4.stride(0), ptr(dH3), dH3.stride(0), LEAKY_SLOPE, ptr(self.loss),
                        ptr(self.ws), self.ws_bytes, ptr(self.adam_state) if fold else None, self.lr, self.betas[0],
-                       self.betas[1], self._s())
+                       self.betas[1], *pieces, self._s())
 
     def _head(self, a_dtype, A4, dZ, dZb, dA4) -> None:
         """liner2 + sigmoid + train/val multi_loss + dZ + dA4 = (dZ W2) * leaky'(A4): one
@@ -689,6 +711,13 @@ class TrainEngine:
         with self._t("adam", 16.0 * self.flat.numel()):
             if not prepped:  # (else this step's head formed the scalars)
                 self._call("pg_adam_prepare", ptr(self.adam_state), self.lr, self.betas[0], self.betas[1], st)
+            if self.l1_pieces is not None:  # (also W1's pieces for the next step's head)
+                W1 = self.P["liner1.W"]
+                self._call("pg_adam_apply_l1", ptr(self.flat), ptr(self.gflat), ptr(self.m), ptr(self.v),
+                           self.flat.numel(), ptr(self.adam_state), self.betas[0], self.betas[1], self.eps, 0.0,
+                           (W1.data_ptr() - self.flat.data_ptr()) // 4, W1.stride(0), self.pd[-3], self.pd[-2],
+                           ptr(self.l1_pieces), st)
+                return
             self._call("pg_adam_apply", ptr(self.flat), ptr(self.gflat), ptr(self.m), ptr(self.v),
                  self.flat.numel(), ptr(self.adam_state), self.betas[0], self.betas[1], self.eps, 0.0, st)
 

@@ -1,4 +1,5 @@
-"""The fused MLP head (pg_mlp_l1_head, ABI 12): liner1's forward, the head (liner2 +
+"""The fused MLP head (pg_mlp_l1_head, ABI 12; pg_mlp_l1_head_ex with W1's pieces kept by
+pg_adam_apply_l1, ABI 13): liner1's forward, the head (liner2 +
 sigmoid + train/val multi_loss + dZ + dA4) and liner1's input gradient through the top SAGE
 layer's leaky_relu, in one launch. It computes both products exactly as the three-piece
 GEMM does (same split, same 16-k steps and MFMA sequence, zero past K), so a TrainEngine
@@ -66,6 +67,62 @@ def test_fused_head_equals_separate_launches_bitwise(dims, n, e):
     for k in b:
         assert torch.equal(a[k], b[k]), f"{k}: fused != separate (max diff {(a[k] - b[k]).abs().max().item():.3e})"
     assert fused.flops_per_step() + fused.head_flops_per_step() == sep.flops_per_step()
+
+
+@pytest.mark.parametrize("dims,n,e", [((31, 24, 20, 16, 10, 12), 600, 6000), ((64, 48, 200, 100, 12), 1000, 12000)])
+def test_fused_head_steps_equal_separate_bitwise(dims, n, e):
+    """Three whole training steps: the fused engine's head reads W1's pieces that its Adam
+    (pg_adam_apply_l1) rewrote, the separate engine's GEMMs split W1 themselves; parameters,
+    moments and losses stay bitwise equal."""
+    fused, sep = _engine_pair(dims, n, e, seed=n)
+    assert fused.l1_pieces is not None and sep.l1_pieces is None
+    for _ in range(3):
+        fused.step_eager()
+        sep.step_eager()
+    torch.cuda.synchronize()
+    for a, b in ((fused.flat, sep.flat), (fused.m, sep.m), (fused.v, sep.v)):
+        assert torch.equal(a, b)
+    assert fused.losses() == sep.losses()
+
+
+@pytest.mark.parametrize("F3,K1,ldw1,off", [(256, 100, 256, 1000), (200, 28, 204, 37), (512, 128, 512, 0)])
+def test_adam_apply_l1_equals_adam_and_split(F3, K1, ldw1, off):
+    """pg_adam_apply_l1 == pg_adam_apply on every parameter and moment (bitwise), and the
+    pieces it leaves == pg_mlp_l1_split of the updated W1 (bitwise, pads included)."""
+    from plagnn import _lib
+
+    L = _lib.lib()
+    g = torch.Generator(device="cpu").manual_seed(F3 + K1)
+    n = off + K1 * ldw1 + 333
+    p0 = torch.randn(n, generator=g).cuda()
+    gr = torch.randn(n, generator=g).cuda()
+    m0 = torch.randn(n, generator=g).cuda() * 0.1
+    v0 = torch.rand(n, generator=g).cuda() * 0.01
+    st = torch.zeros(4, device="cuda")
+    assert L.pg_adam_prepare(st.data_ptr(), 1e-3, 0.9, 0.999, None) == 0
+    nb = int(L.pg_mlp_l1_pieces_bytes(F3, K1))
+    pieces = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+    ref = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+    W1 = lambda p: p[off:off + K1 * ldw1].view(K1, ldw1)  # noqa: E731
+    # the pieces start as the split of the old W1 (the pads are the split's zeros)
+    assert L.pg_mlp_l1_split(W1(p0).data_ptr(), ldw1, F3, K1, pieces.data_ptr(), None) == 0
+    a = [t.clone() for t in (p0, m0, v0)]
+    b = [t.clone() for t in (p0, m0, v0)]
+    assert L.pg_adam_apply_l1(a[0].data_ptr(), gr.data_ptr(), a[1].data_ptr(), a[2].data_ptr(), n, st.data_ptr(),
+                              0.9, 0.999, 1e-8, 0.0, off, ldw1, F3, K1, pieces.data_ptr(), None) == 0
+    assert L.pg_adam_apply(b[0].data_ptr(), gr.data_ptr(), b[1].data_ptr(), b[2].data_ptr(), n, st.data_ptr(),
+                           0.9, 0.999, 1e-8, 0.0, None) == 0
+    assert L.pg_mlp_l1_split(W1(b[0]).data_ptr(), ldw1, F3, K1, ref.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert not torch.equal(a[0], p0)
+    assert torch.equal(pieces, ref)
+    # W1 outside the n parameters, misaligned pieces: refused
+    assert L.pg_adam_apply_l1(a[0].data_ptr(), gr.data_ptr(), a[1].data_ptr(), a[2].data_ptr(), n, st.data_ptr(),
+                              0.9, 0.999, 1e-8, 0.0, n - 10, ldw1, F3, K1, pieces.data_ptr(), None) != 0
+    assert L.pg_adam_apply_l1(a[0].data_ptr(), gr.data_ptr(), a[1].data_ptr(), a[2].data_ptr(), n, st.data_ptr(),
+                              0.9, 0.999, 1e-8, 0.0, off, ldw1, F3, K1, pieces.data_ptr() + 16, None) != 0
 
 
 def test_fused_head_full_size_cfg2_bitwise_and_replay():

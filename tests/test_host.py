@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(_lib.SIGNATURES), "ctypes signatures out of sync with header"
-    assert L.pg_version() == 12
+    assert L.pg_version() == 13
 
 
 def test_error_reporting():
